@@ -1,0 +1,138 @@
+"""ctypes binding of libbcmpc.so (include/bcmpc.h).
+
+The library is built in-tree (``make`` / ``__graft_entry__.build()``) and is
+the only compute path: if it is missing this module raises ImportError --
+there is no CPU fallback.
+
+PyTorch-ROCm ships its own ``libamdhip64.so.7`` (same SONAME as
+/opt/rocm's).  Importing torch first makes the dynamic linker reuse torch's
+HIP runtime for libbcmpc, so device pointers from torch tensors and from the
+engine live in ONE runtime.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+try:  # single HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbcmpc.so")
+
+MAX_LAYERS = 8
+MAX_STATE = 32
+MAX_ACTION = 16
+ABI_VERSION = 1
+
+OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
+ACT_TANH, ACT_RELU = 0, 1
+COST_CHEETAH, COST_NONE = 0, 1
+PREC_FP32 = 0
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("state_dim", ctypes.c_int32),
+        ("action_dim", ctypes.c_int32),
+        ("hidden", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("activation", ctypes.c_int32),
+        ("layer_norm", ctypes.c_int32),
+        ("horizon", ctypes.c_int32),
+        ("cost", ctypes.c_int32),
+        ("num_paths", ctypes.c_int64),
+        ("precision", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 8),
+    ]
+
+
+_FP = ctypes.POINTER(ctypes.c_float)
+_DP = ctypes.POINTER(ctypes.c_double)
+
+
+class Weights(ctypes.Structure):
+    _fields_ = [
+        ("kernels", ctypes.POINTER(_FP)),
+        ("biases", ctypes.POINTER(_FP)),
+        ("ln_gamma", ctypes.POINTER(_FP)),
+        ("ln_beta", ctypes.POINTER(_FP)),
+        ("mean_obs", _DP),
+        ("std_obs", _DP),
+        ("mean_action", _DP),
+        ("std_action", _DP),
+        ("mean_deltas", _DP),
+        ("std_deltas", _DP),
+    ]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [
+        ("best_index", ctypes.c_int64),
+        ("best_cost", ctypes.c_double),
+        ("first_action", ctypes.c_double * MAX_ACTION),
+    ]
+
+
+# (name, restype, argtypes) -- every symbol include/bcmpc.h declares
+SIGNATURES = [
+    ("bcmpc_abi_version", ctypes.c_int, []),
+    ("bcmpc_last_error", ctypes.c_char_p, []),
+    ("bcmpc_create", ctypes.c_int, [ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_void_p)]),
+    ("bcmpc_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("bcmpc_set_weights", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Weights), ctypes.c_uint64]),
+    ("bcmpc_weights_version", ctypes.c_uint64, [ctypes.c_void_p]),
+    ("bcmpc_set_action_bounds", ctypes.c_int, [ctypes.c_void_p, _DP, _DP]),
+    ("bcmpc_get_action", ctypes.c_int,
+     [ctypes.c_void_p, _DP, _DP, ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(Result), _DP]),
+    ("bcmpc_rollout_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("bcmpc_stream", ctypes.c_void_p, [ctypes.c_void_p]),
+    ("bcmpc_last_kernel_ms", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+    ("bcmpc_engine_info", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
+      ctypes.POINTER(ctypes.c_int32)]),
+]
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libbcmpc.so once; raise ImportError (loudly) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libbcmpc.so not found at {LIB_PATH}: build it with `make` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.bcmpc_abi_version() != ABI_VERSION:
+        raise ImportError(f"libbcmpc ABI {lib.bcmpc_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+class BcmpcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[bcmpc status {code}] {msg}")
+        self.code = code
+
+
+def check(code: int) -> None:
+    if code == OK:
+        return
+    msg = load().bcmpc_last_error().decode(errors="replace")
+    if code == ERR_EMPTY:
+        raise ValueError(msg)                  # np.argmin on an empty sequence
+    if code in (ERR_ARG, ERR_UNSUPPORTED):
+        raise ValueError(f"[bcmpc status {code}] {msg}")
+    raise BcmpcError(code, msg)

@@ -1,0 +1,198 @@
+"""Drop-in controllers with the reference's API (controllers.py:6-88).
+
+``MPCcontroller(env, dyn_model, horizon, cost_fn, num_simulated_paths, gamma)``
+and ``get_action(state) -> np.ndarray (A,) float64`` keep the reference's
+signatures so ``train_mpc_ppo.py:218-222`` / ``utils.py:202`` run unchanged.
+The rollout itself -- state fan-out, H x dynamics MLP, cheetah cost, argmin --
+runs in libbcmpc's HIP kernels (``bc_mpc_amd/csrc/rollout.hip``).
+
+Action source (``rng=``):
+
+* ``"numpy"`` (default, parity mode): exactly one
+  ``np.random.uniform(low, high, size=[H, K, A])`` draw from the global legacy
+  stream per call, as controllers.py:53 does, so a seeded driver
+  (train_mpc_ppo.py:499) sees the same RNG side effects and the same actions.
+  The returned action is ``action_paths[0, argmin, :].copy()`` of that array
+  (controllers.py:84-85), bit-identical to the reference.
+* ``"device"`` (perf mode): actions are drawn inside the kernel with
+  Philox4x32-10 keyed by (seed, global candidate, step, draw); one 64-bit seed
+  per call is taken from ``np.random`` (or from ``seed=`` if given).
+
+Multi-GPU: when torch.distributed is initialised each rank owns a contiguous
+slice of the K candidates (``distributed.shard_range``) and the ranks agree on
+the argmin through one all-gather of (3 + A) doubles per step.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import distributed as _dist
+from . import weights as _weights
+from .cost_functions import is_cheetah_cost, trajectory_cost_fn
+from .engine import RolloutEngine
+
+
+class Controller():
+    """controllers.py:6-12."""
+
+    def __init__(self):
+        pass
+
+    def get_action(self, state):
+        pass
+
+
+class RandomController(Controller):
+    """controllers.py:15-24 (uniform env.action_space.sample())."""
+
+    def __init__(self, env):
+        self.env = env
+
+    def get_action(self, state):
+        return self.env.action_space.sample()
+
+
+def _default_device() -> int:
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"])
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.cuda.current_device()
+    except Exception:  # pragma: no cover
+        pass
+    return 0
+
+
+class MPCcontroller(Controller):
+    """Random-shooting MPC (controllers.py:26-88) on the MI355X rollout engine."""
+
+    def __init__(self,
+                 env,
+                 dyn_model,
+                 horizon=5,
+                 cost_fn=None,
+                 num_simulated_paths=10,
+                 gamma=1.,
+                 *,
+                 rng: str = "numpy",
+                 seed: Optional[int] = None,
+                 device: Optional[int] = None,
+                 process_group=None):
+        self.env = env
+        self.dyn_model = dyn_model
+        self.horizon = horizon
+        self.cost_fn = cost_fn
+        self.num_simulated_paths = num_simulated_paths
+        self.gamma = gamma                      # stored, unused (as in the reference)
+        if rng not in ("numpy", "device"):
+            raise ValueError("rng must be 'numpy' or 'device'")
+        self.rng = rng
+        self._seed_rng = np.random.RandomState(seed) if seed is not None else None
+        self._device = device
+        self._group = process_group
+        self._engine: Optional[RolloutEngine] = None
+        self._engine_key = None
+        self._traj_buf = None
+        # diagnostics of the last call (not part of the reference API)
+        self.last_cost = None
+        self.last_index = None
+        self.last_costs = None
+        self.keep_costs = False
+
+    # controllers.py:43-55
+    def sample_random_actions(self):
+        np_action_paths = np.random.uniform(low=self.env.action_space.low, high=self.env.action_space.high,
+                                            size=[self.horizon, self.num_simulated_paths,
+                                                  len(self.env.action_space.high)])
+        return np_action_paths
+
+    # ------------------------------------------------------------------ engine
+    def _dims(self):
+        S = int(np.prod(self.env.observation_space.shape))
+        A = len(self.env.action_space.high)
+        return S, A
+
+    def _engine_for(self, spec, S, A, k_local, fused) -> RolloutEngine:
+        dev = _default_device() if self._device is None else self._device
+        key = (S, A, spec.hidden, spec.n_layers, spec.activation, spec.layer_norm, int(self.horizon),
+               int(k_local), dev, fused)
+        if self._engine is None or self._engine_key != key:
+            if self._engine is not None:
+                self._engine.close()
+            self._engine = RolloutEngine(S, A, spec.hidden, spec.n_layers, spec.activation, spec.layer_norm,
+                                         int(self.horizon), int(k_local), device=dev,
+                                         cost="cheetah" if fused else "none")
+            self._engine.set_action_bounds(np.asarray(self.env.action_space.low, dtype=np.float64),
+                                           np.asarray(self.env.action_space.high, dtype=np.float64))
+            self._engine_key = key
+            self._traj_buf = None
+        return self._engine
+
+    def _next_seed(self) -> int:
+        src = self._seed_rng if self._seed_rng is not None else np.random
+        return int(src.randint(0, 2**62, dtype=np.int64))
+
+    # controllers.py:57-88
+    def get_action(self, state):
+        S, A = self._dims()
+        K = int(self.num_simulated_paths)
+        if self.horizon < 1:
+            raise IndexError("index 0 is out of bounds for axis 0 with size 0")   # controllers.py:85 at H=0
+        state = np.asarray(state, dtype=np.float64).reshape(-1)
+        rank, ws = _dist.world(self._group)
+        lo, hi = _dist.shard_range(K, rank, ws)
+        spec, norm, version = _weights.extract(self.dyn_model)
+        fused = is_cheetah_cost(self.cost_fn, S, A)
+        if not fused and self.rng != "numpy":
+            raise ValueError("a non-cheetah cost_fn needs rng='numpy' (actions must exist on the host)")
+
+        action_paths = None
+        seed = 0
+        if self.rng == "numpy":
+            action_paths = self.sample_random_actions()      # every rank draws the full [H, K, A]
+        else:
+            seed = self._next_seed()
+        if K == 0:
+            raise ValueError("attempt to get argmin of an empty sequence")
+
+        valid, cost, index, first = False, float("inf"), -1, None
+        if hi > lo:
+            eng = self._engine_for(spec, S, A, hi - lo, fused)
+            eng.set_weights(spec, norm, version)            # no-op unless the version changed
+            local = None if action_paths is None else np.ascontiguousarray(action_paths[:, lo:hi, :])
+            if fused:
+                res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
+                valid, cost, index, first = True, res.best_cost, res.best_index, res.first_action
+                self.last_costs = res.costs
+            else:
+                costs = self._trajectory_costs(eng, state, local)
+                i = int(np.argmin(costs))
+                valid, cost, index, first = True, float(costs[i]), lo + i, local[0, i, :].copy()
+                self.last_costs = costs
+
+        cost, index, first_g = _dist.allgather_minloc(valid, cost, index, first, A, self._group)
+        self.last_cost, self.last_index = cost, index
+        if action_paths is not None:
+            opt_action_path = action_paths[:, index, :]     # controllers.py:84-85
+            return opt_action_path[0].copy()
+        return first_g
+
+    def _trajectory_costs(self, eng: RolloutEngine, state, local_actions) -> np.ndarray:
+        """Non-fused cost_fn: the engine returns states_paths_all (controllers.py:65-74)
+        and the caller's cost_fn scores them through trajectory_cost_fn (:80)."""
+        import torch
+        dev = torch.device("cuda", eng.device)
+        H, Kl, A = local_actions.shape
+        S = eng.state_dim
+        d_state = torch.from_numpy(state).to(dev)
+        d_act = torch.from_numpy(local_actions).to(dev)
+        d_traj = torch.empty((H + 1, Kl, S), dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        eng.rollout_async(d_state.data_ptr(), 0, d_act.data_ptr(), 0, 0, None, d_traj.data_ptr(), None,
+                          stream.cuda_stream)
+        traj = d_traj.cpu().numpy()                       # synchronises the stream
+        return np.asarray(trajectory_cost_fn(self.cost_fn, traj[:-1], local_actions, traj[1:]), dtype=np.float64)

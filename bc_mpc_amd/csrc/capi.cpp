@@ -1,0 +1,316 @@
+// capi.cpp -- C ABI of libbcmpc (include/bcmpc.h): engine lifetime, weight
+// packing into MFMA fragment order, host<->device staging, launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bcmpc.h"
+#include "kernels.h"
+
+using namespace bcmpc;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(BCMPC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+int padded_hidden(int h) {
+    for (int hp : {64, 128, 256, 512})
+        if (h <= hp) return hp;
+    return -1;
+}
+
+// Dense kernel W [in][out] (tf.layers.dense layout) -> fragment order
+// [tb][u][j][lane][r], t = tb*TB + j: element W[16u + 4(lane>>4) + r][16t + (lane&15)]
+// (zero outside in x out).  See the layout note at the top of rollout.hip.
+void pack_layer(const float* W, int in, int out, int Tin, int Tout, int TB, float* dst) {
+    for (int t = 0; t < Tout; ++t) {
+        const int tb = t / TB, j = t % TB;
+        for (int u = 0; u < Tin; ++u)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int r = 0; r < 4; ++r) {
+                    const int k = 16 * u + 4 * (lane >> 4) + r;
+                    const int n = 16 * t + (lane & 15);
+                    const size_t o = ((((size_t)tb * Tin + u) * TB + j) * 64 + lane) * 4 + r;
+                    dst[o] = (k < in && n < out) ? W[(size_t)k * out + n] : 0.f;
+                }
+    }
+}
+
+}  // namespace
+
+struct bcmpc_engine {
+    bcmpc_config cfg{};
+    int HP = 0, T = 0, wpb = 4;
+    hipStream_t stream = nullptr;
+    // device buffers
+    float* d_w = nullptr;   size_t w_floats = 0;
+    size_t w_off[BCMPC_MAX_LAYERS + 1]{};
+    float* d_b = nullptr;   size_t b_off[BCMPC_MAX_LAYERS + 1]{};
+    float* d_ln = nullptr;  // [2][L][HP]
+    double* d_consts = nullptr;
+    double* d_state = nullptr;
+    double* d_actions = nullptr; size_t actions_cap = 0;
+    double* d_costs = nullptr;
+    bcmpc_result* d_result = nullptr;
+    bcmpc_result* h_result = nullptr;   // pinned
+    double h_consts[kConstRows * kConstCols]{};
+    uint64_t version = 0;
+    bool has_weights = false;
+    hipEvent_t ev[3]{};
+    bool timed = false;
+};
+
+extern "C" {
+
+int bcmpc_abi_version(void) { return BCMPC_ABI_VERSION; }
+const char* bcmpc_last_error(void) { return g_last_error.c_str(); }
+
+int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
+    if (!cfg || !out) return fail(BCMPC_ERR_ARG, "null argument");
+    *out = nullptr;
+    const bcmpc_config& c = *cfg;
+    if (c.state_dim < 1 || c.state_dim > BCMPC_MAX_STATE) return fail(BCMPC_ERR_UNSUPPORTED, "state_dim must be in [1, 32]");
+    if (c.action_dim < 1 || c.action_dim > BCMPC_MAX_ACTION) return fail(BCMPC_ERR_UNSUPPORTED, "action_dim must be in [1, 16]");
+    if (c.state_dim + c.action_dim > BCMPC_MAX_INPUT) return fail(BCMPC_ERR_UNSUPPORTED, "state_dim + action_dim must be <= 32");
+    if (c.n_layers < 1 || c.n_layers > BCMPC_MAX_LAYERS) return fail(BCMPC_ERR_UNSUPPORTED, "n_layers must be in [1, 8]");
+    if (padded_hidden(c.hidden) < 0 || c.hidden < 1) return fail(BCMPC_ERR_UNSUPPORTED, "hidden must be in [1, 512] in this build");
+    if (c.activation != BCMPC_ACT_TANH && c.activation != BCMPC_ACT_RELU) return fail(BCMPC_ERR_UNSUPPORTED, "activation must be tanh or relu");
+    if (c.horizon < 1) return fail(BCMPC_ERR_ARG, "horizon must be >= 1");
+    if (c.num_paths < 0) return fail(BCMPC_ERR_ARG, "num_paths must be >= 0");
+    if (c.cost != BCMPC_COST_CHEETAH && c.cost != BCMPC_COST_NONE) return fail(BCMPC_ERR_UNSUPPORTED, "unknown cost");
+    if (c.cost == BCMPC_COST_CHEETAH && c.state_dim < 18) return fail(BCMPC_ERR_UNSUPPORTED, "cheetah cost needs state_dim >= 18");
+    if (c.precision != BCMPC_PREC_FP32) return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (c.device < 0 || c.device >= ndev) return fail(BCMPC_ERR_ARG, "device ordinal out of range");
+    HIP_TRY(hipSetDevice(c.device));
+
+    bcmpc_engine* e = new bcmpc_engine();
+    e->cfg = c;
+    e->HP = padded_hidden(c.hidden);
+    e->T = e->HP / 16;
+    // small K: one wave per block spreads candidates over more CUs
+    const int64_t waves = (c.num_paths + 15) / 16;
+    e->wpb = waves >= 4 * 256 ? 4 : 1;
+    const int L = c.n_layers, T = e->T;
+    size_t off = 0;
+    e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;                   // [S+A -> h]
+    for (int l = 1; l < L; ++l) { e->w_off[l] = off; off += (size_t)T * T * 64 * 4; }
+    e->w_off[L] = off; off += (size_t)2 * T * 64 * 4;                   // [h -> S]
+    e->w_floats = off;
+    size_t boff = 0;
+    for (int l = 0; l < L; ++l) { e->b_off[l] = boff; boff += e->HP; }
+    e->b_off[L] = boff; boff += 32;
+    auto cleanup = [&](int code) { bcmpc_destroy(e); return code; };
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&e->d_w, e->w_floats * sizeof(float)) != hipSuccess ||
+        hipMalloc(&e->d_b, boff * sizeof(float)) != hipSuccess ||
+        hipMalloc(&e->d_ln, 2 * (size_t)L * e->HP * sizeof(float)) != hipSuccess ||
+        hipMalloc(&e->d_consts, sizeof(e->h_consts)) != hipSuccess ||
+        hipMalloc(&e->d_state, BCMPC_MAX_STATE * sizeof(double)) != hipSuccess ||
+        hipMalloc(&e->d_costs, std::max<int64_t>(1, c.num_paths) * sizeof(double)) != hipSuccess ||
+        hipMalloc(&e->d_result, sizeof(bcmpc_result)) != hipSuccess ||
+        hipHostMalloc(&e->h_result, sizeof(bcmpc_result), hipHostMallocDefault) != hipSuccess) {
+        g_last_error = "device allocation failed";
+        return cleanup(BCMPC_ERR_HIP);
+    }
+    for (int i = 0; i < 3; ++i)
+        if (hipEventCreate(&e->ev[i]) != hipSuccess) { g_last_error = "event create failed"; return cleanup(BCMPC_ERR_HIP); }
+    // default action bounds: HalfCheetah ctrlrange [-1, 1]
+    for (int j = 0; j < BCMPC_MAX_ACTION && j < kConstCols; ++j) {
+        e->h_consts[6 * kConstCols + j] = -1.0;
+        e->h_consts[7 * kConstCols + j] = 1.0;
+    }
+    *out = e;
+    return BCMPC_OK;
+}
+
+int bcmpc_destroy(bcmpc_engine* e) {
+    if (!e) return BCMPC_OK;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
+                    (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result})
+        if (p) (void)hipFree(p);
+    if (e->h_result) (void)hipHostFree(e->h_result);
+    for (auto& ev : e->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return BCMPC_OK;
+}
+
+uint64_t bcmpc_weights_version(const bcmpc_engine* e) { return e ? e->version : 0; }
+
+int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version) {
+    if (!e || !w || !w->kernels || !w->biases) return fail(BCMPC_ERR_ARG, "null argument");
+    if (e->has_weights && version == e->version) return BCMPC_OK;    // idempotent re-sync
+    const bcmpc_config& c = e->cfg;
+    const int L = c.n_layers, S = c.state_dim, A = c.action_dim, h = c.hidden, HP = e->HP, T = e->T;
+    if (c.layer_norm && (!w->ln_gamma || !w->ln_beta)) return fail(BCMPC_ERR_ARG, "layer_norm enabled but LN params missing");
+    if (!w->mean_obs || !w->std_obs || !w->mean_action || !w->std_action || !w->mean_deltas || !w->std_deltas)
+        return fail(BCMPC_ERR_ARG, "normalization stats missing");
+    for (int l = 0; l <= L; ++l)
+        if (!w->kernels[l] || !w->biases[l]) return fail(BCMPC_ERR_ARG, "null kernel/bias pointer");
+    HIP_TRY(hipSetDevice(c.device));
+    std::vector<float> hw(e->w_floats, 0.f);
+    pack_layer(w->kernels[0], S + A, h, 2, T, 4, hw.data() + e->w_off[0]);
+    for (int l = 1; l < L; ++l) pack_layer(w->kernels[l], h, h, T, T, 4, hw.data() + e->w_off[l]);
+    pack_layer(w->kernels[L], h, S, T, 2, 2, hw.data() + e->w_off[L]);
+    std::vector<float> hb((size_t)L * HP + 32, 0.f);
+    for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
+    std::memcpy(hb.data() + e->b_off[L], w->biases[L], sizeof(float) * S);
+    std::vector<float> hln(2 * (size_t)L * HP, 0.f);
+    if (c.layer_norm)
+        for (int l = 0; l < L; ++l) {
+            std::memcpy(hln.data() + (size_t)l * HP, w->ln_gamma[l], sizeof(float) * h);
+            std::memcpy(hln.data() + (size_t)(L + l) * HP, w->ln_beta[l], sizeof(float) * h);
+        }
+    double* C = e->h_consts;
+    for (int i = 0; i < kConstCols; ++i) {
+        C[0 * 32 + i] = i < S ? w->mean_obs[i] : 0.0;
+        C[1 * 32 + i] = i < S ? w->std_obs[i] + 1e-10 : 1.0;       // dynamics.py:109 (std + 1e-10)
+        C[2 * 32 + i] = i < A ? w->mean_action[i] : 0.0;
+        C[3 * 32 + i] = i < A ? w->std_action[i] + 1e-10 : 1.0;    // dynamics.py:110
+        C[4 * 32 + i] = i < S ? w->mean_deltas[i] : 0.0;
+        C[5 * 32 + i] = i < S ? w->std_deltas[i] : 0.0;
+    }
+    HIP_TRY(hipMemcpyAsync(e->d_w, hw.data(), hw.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_b, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_ln, hln.data(), hln.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_consts, C, sizeof(e->h_consts), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));   // host vectors die at scope exit
+    e->version = version;
+    e->has_weights = true;
+    return BCMPC_OK;
+}
+
+int bcmpc_set_action_bounds(bcmpc_engine* e, const double* low, const double* high) {
+    if (!e || !low || !high) return fail(BCMPC_ERR_ARG, "null argument");
+    for (int j = 0; j < e->cfg.action_dim; ++j) {
+        e->h_consts[6 * 32 + j] = low[j];
+        e->h_consts[7 * 32 + j] = high[j];
+    }
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    HIP_TRY(hipMemcpyAsync(e->d_consts, e->h_consts, sizeof(e->h_consts), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return BCMPC_OK;
+}
+
+void* bcmpc_stream(bcmpc_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, const double* d_actions,
+                        uint64_t seed, int64_t cand_offset, double* d_costs, double* d_traj,
+                        bcmpc_result* d_result, hipStream_t st) {
+    const bcmpc_config& c = e->cfg;
+    if (!e->has_weights) return fail(BCMPC_ERR_STATE, "bcmpc_set_weights has not been called");
+    if (c.num_paths == 0) return fail(BCMPC_ERR_EMPTY, "attempt to get argmin of an empty sequence");
+    if (stride != 0 && stride != c.state_dim) return fail(BCMPC_ERR_ARG, "state_stride must be 0 or state_dim");
+    if (c.cost == BCMPC_COST_CHEETAH && !d_costs) return fail(BCMPC_ERR_ARG, "cheetah cost needs a costs buffer");
+    if (d_result && c.cost != BCMPC_COST_CHEETAH) return fail(BCMPC_ERR_ARG, "argmin needs the fused cost");
+    RolloutArgs a{};
+    for (int l = 0; l <= c.n_layers; ++l) {
+        a.w[l] = reinterpret_cast<const float __attribute__((ext_vector_type(4)))*>(e->d_w + e->w_off[l]);
+        a.b[l] = e->d_b + e->b_off[l];
+    }
+    for (int l = 0; l < c.n_layers; ++l) {
+        a.lng[l] = e->d_ln + (size_t)l * e->HP;
+        a.lnb[l] = e->d_ln + (size_t)(c.n_layers + l) * e->HP;
+    }
+    a.consts = e->d_consts;
+    a.state = d_state; a.state_stride = stride;
+    a.actions = d_actions; a.costs = d_costs; a.traj = d_traj;
+    a.seed = seed; a.cand_offset = cand_offset; a.K = c.num_paths;
+    a.H = c.horizon; a.S = c.state_dim; a.A = c.action_dim; a.L = c.n_layers;
+    a.hidden = c.hidden; a.act = c.activation; a.ln = c.layer_norm; a.cost = c.cost;
+    HIP_TRY(hipEventRecord(e->ev[0], st));
+    HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
+    HIP_TRY(hipEventRecord(e->ev[1], st));
+    if (d_result) {
+        ArgminArgs m{};
+        m.costs = d_costs; m.actions = d_actions; m.consts = e->d_consts; m.out = d_result;
+        m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
+        HIP_TRY(launch_argmin(m, st));
+    }
+    HIP_TRY(hipEventRecord(e->ev[2], st));
+    e->timed = d_result != nullptr;
+    return BCMPC_OK;
+}
+
+int bcmpc_rollout_async(bcmpc_engine* e, const double* d_state, int64_t state_stride, const double* d_actions,
+                        uint64_t seed, int64_t cand_offset, double* d_costs, double* d_traj,
+                        bcmpc_result* d_result, void* stream) {
+    if (!e || !d_state) return fail(BCMPC_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    // `stream` is used verbatim: NULL is HIP's null stream (bcmpc_stream() gives the engine's own)
+    return rollout_impl(e, d_state, state_stride, d_actions, seed, cand_offset, d_costs, d_traj, d_result,
+                        (hipStream_t)stream);
+}
+
+int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions, uint64_t seed,
+                     int64_t cand_offset, bcmpc_result* out, double* costs_out) {
+    if (!e || !state || !out) return fail(BCMPC_ERR_ARG, "null argument");
+    const bcmpc_config& c = e->cfg;
+    if (c.cost != BCMPC_COST_CHEETAH) return fail(BCMPC_ERR_ARG, "get_action needs the fused cheetah cost");
+    HIP_TRY(hipSetDevice(c.device));
+    HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
+    const double* d_act = nullptr;
+    if (actions) {
+        const size_t n = (size_t)c.horizon * (size_t)c.num_paths * (size_t)c.action_dim;
+        if (n > e->actions_cap) {
+            if (e->d_actions) (void)hipFree(e->d_actions);
+            e->d_actions = nullptr;
+            e->actions_cap = 0;
+            HIP_TRY(hipMalloc(&e->d_actions, n * sizeof(double)));
+            e->actions_cap = n;
+        }
+        HIP_TRY(hipMemcpyAsync(e->d_actions, actions, n * sizeof(double), hipMemcpyHostToDevice, e->stream));
+        d_act = e->d_actions;
+    }
+    int rc = rollout_impl(e, e->d_state, 0, d_act, seed, cand_offset, e->d_costs, nullptr, e->d_result, e->stream);
+    if (rc != BCMPC_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream));
+    if (costs_out)
+        HIP_TRY(hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    *out = *e->h_result;
+    return BCMPC_OK;
+}
+
+int bcmpc_last_kernel_ms(bcmpc_engine* e, float* rollout_ms, float* argmin_ms) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    float r = 0.f, m = 0.f;
+    HIP_TRY(hipEventSynchronize(e->ev[2]));
+    HIP_TRY(hipEventElapsedTime(&r, e->ev[0], e->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&m, e->ev[1], e->ev[2]));
+    if (rollout_ms) *rollout_ms = r;
+    if (argmin_ms) *argmin_ms = m;
+    return BCMPC_OK;
+}
+
+int bcmpc_engine_info(const bcmpc_engine* e, int32_t* hidden_padded, int64_t* packed_weight_bytes,
+                      int32_t* waves_per_block) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    if (hidden_padded) *hidden_padded = e->HP;
+    if (packed_weight_bytes) *packed_weight_bytes = (int64_t)(e->w_floats * sizeof(float));
+    if (waves_per_block) *waves_per_block = e->wpb;
+    return BCMPC_OK;
+}
+
+}  // extern "C"

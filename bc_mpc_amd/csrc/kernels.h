@@ -1,0 +1,47 @@
+// kernels.h -- device-side argument blocks and launchers (internal to libbcmpc).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bcmpc.h"
+
+namespace bcmpc {
+
+// consts block: [8][32] doubles
+//   0 mean_obs   1 std_obs + 1e-10   2 mean_action   3 std_action + 1e-10
+//   4 mean_deltas  5 std_deltas      6 action low    7 action high
+constexpr int kConstRows = 8;
+constexpr int kConstCols = 32;
+
+struct RolloutArgs {
+    const float __attribute__((ext_vector_type(4)))* w[BCMPC_MAX_LAYERS + 1];  // packed kernels
+    const float* b[BCMPC_MAX_LAYERS + 1];    // padded biases
+    const float* lng[BCMPC_MAX_LAYERS];      // padded LN gamma (0 on pad lanes)
+    const float* lnb[BCMPC_MAX_LAYERS];      // padded LN beta
+    const double* consts;
+    const double* state;
+    int64_t state_stride;                    // 0 (tiled, controllers.py:63) or S (per-candidate)
+    const double* actions;                   // [H][K][A] or nullptr => Philox
+    double* costs;                           // [K] or nullptr
+    double* traj;                            // [H+1][K][S] or nullptr
+    uint64_t seed;
+    int64_t cand_offset;
+    int64_t K;
+    int32_t H, S, A, L, hidden, act, ln, cost;
+};
+
+struct ArgminArgs {
+    const double* costs;
+    const double* actions;   // [H][K][A] or nullptr
+    const double* consts;
+    bcmpc_result* out;
+    uint64_t seed;
+    int64_t cand_offset;
+    int64_t K;
+    int32_t A;
+};
+
+hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st);
+hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
+
+}  // namespace bcmpc

@@ -1,0 +1,378 @@
+// rollout.hip -- MI355X (gfx950) random-shooting MPC rollout kernels.
+//
+// One launch == one MPCcontroller.get_action (controllers.py:57-88) on this
+// device's shard of the K candidates:
+//   * per-candidate state fan-out (np.tile, controllers.py:63) into registers,
+//   * H serial steps of NNDynamicsModel.predict (dynamics.py:106-119):
+//       f64 normalise -> f32 cast (TF feed, dynamics.py:23-24) ->
+//       dense/act[/LayerNorm] x L -> dense (dynamics.py:54-71) ->
+//       f64 de-normalise + residual add,
+//     with every dense layer on v_mfma_f32_16x16x4_f32 (exact f32 fma chain),
+//   * the cheetah cost (cost_functions.py:10-30) accumulated per step in f64
+//     registers in the reference's operation order (trajectory_cost_fn :59-63),
+//   * np.argmin (controllers.py:82) in a second tiny kernel (first NaN, else
+//     first minimum -> lowest index wins ties).
+//
+// Layout ("transposed" MLP, activations never leave the wave):
+//   A wave owns 16 candidates (MFMA column j = lane & 15).  Each dense layer is
+//   computed as D[neuron][cand] = W^T[neuron][k] * X[k][cand], weights as the
+//   MFMA A operand, activations as the B operand.  The D fragment of a
+//   16-neuron tile (lane (q=lane>>4, m) holds neurons 4q+r, r=0..3) is exactly
+//   the B fragment of k-steps r=0..3 of the next layer when the weights are
+//   pre-packed in that k order on the host -- so the x registers of one layer
+//   feed the next with no lane movement.  Outputs of a layer are produced one
+//   4-tile block at a time (runtime loop) and parked in a wave-private LDS
+//   slab, then re-read into registers for the next layer.
+//   State (f64) lives in the lanes that own the matching input/output rows:
+//   row/dim d = 16v + 4q + r (v = 0,1).
+//
+// Weights are streamed from L2 (1 KiB per wave-instruction, float4 per lane,
+// fragment order, see pack_layer in capi.cpp); all waves of a CU walk the
+// same stream, so it is shared through the CU's L1.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bcmpc.h"
+#include "kernels.h"
+
+namespace bcmpc {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- Philox ---
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]);
+        const uint32_t lo0 = 0xD2511F53u * c[0];
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        const uint32_t lo1 = 0xCD9E8D57u * c[2];
+        const uint32_t n0 = hi1 ^ c[1] ^ k0;
+        const uint32_t n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+// Uniform action j of global candidate g at step h (oracle.device_rng_actions).
+__device__ __forceinline__ double rng_action(uint64_t seed, uint64_t g, int h, int j,
+                                             double lo, double hi) {
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)h, (uint32_t)(j >> 1)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t a = (j & 1) ? c[2] : c[0];
+    const uint32_t b = (j & 1) ? c[3] : c[1];
+    // NumPy legacy random_sample: ((a >> 5) * 2^26 + (b >> 6)) / 2^53 (exact in f64)
+    const double u = ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+    return __dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u));   // low + (high-low)*u, no FMA
+}
+
+// -------------------------------------------------------------- MLP tiles ---
+// acc[j] = sum_u sum_r W[t0+j][u][r] * x[u][r] for a block of TB output tiles.
+// wblk points at the packed block [u][j][lane] (f4 per lane).
+template <int TIN, int TB>
+__device__ __forceinline__ void mm_tiles(const f4* __restrict__ wblk, const float (&x)[TIN][4],
+                                         f4 (&acc)[TB], int lane) {
+#pragma unroll
+    for (int j = 0; j < TB; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < TIN; ++u) {
+        f4 w[TB];
+#pragma unroll
+        for (int j = 0; j < TB; ++j) w[j] = wblk[(u * TB + j) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int j = 0; j < TB; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j][r], x[u][r], acc[j], 0, 0, 0);
+        }
+    }
+}
+
+__device__ __forceinline__ float activate(float v, int act) {
+    return act == BCMPC_ACT_RELU ? fmaxf(v, 0.f) : tanhf(v);
+}
+
+// bias + activation of a finished 4-tile block, parked in the wave's LDS slab.
+template <int TB>
+__device__ __forceinline__ void store_block(const f4 (&acc)[TB], int t0, const float* __restrict__ bias,
+                                            int act, f4* y, int lane) {
+    const int q = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < TB; ++j) {
+        const int t = t0 + j;
+        const f4 bv = *reinterpret_cast<const f4*>(bias + 16 * t + 4 * q);
+        f4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = activate(acc[j][r] + bv[r], act);   // BiasAdd then act
+        y[t * 64 + lane] = v;
+    }
+}
+
+// tf.contrib.layers.layer_norm over the true hidden width (dynamics.py:68-69).
+template <int T>
+__device__ __forceinline__ void layer_norm(float (&x)[T][4], const float* __restrict__ g,
+                                           const float* __restrict__ bta, int hidden, int lane) {
+    const int q = lane >> 4;
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < T; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum += x[u][r];          // padded neurons are exactly 0
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum / (float)hidden;
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < T; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float d = x[u][r] - mean;
+            ss += (16 * u + 4 * q + r < hidden) ? d * d : 0.f;
+        }
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    const float var = ss / (float)hidden;
+    const float rs = 1.0f / sqrtf(var + 1e-12f);
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        const f4 gv = *reinterpret_cast<const f4*>(g + 16 * u + 4 * q);
+        const f4 bv = *reinterpret_cast<const f4*>(bta + 16 * u + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float inv = rs * gv[r];
+            x[u][r] = x[u][r] * inv + (bv[r] - mean * inv);   // nn.batch_normalization form
+        }
+    }
+}
+
+template <int T>
+__device__ __forceinline__ void reload(float (&x)[T][4], const f4* y, int lane) {
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        const f4 v = y[u * 64 + lane];
+        x[u][0] = v[0]; x[u][1] = v[1]; x[u][2] = v[2]; x[u][3] = v[3];
+    }
+}
+
+// ------------------------------------------------------------ the kernel ---
+template <int HP>
+__global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
+    constexpr int T = HP / 16;     // hidden tiles
+    constexpr int TB = 4;          // output tiles per block (packing granule)
+    static_assert(T % TB == 0, "hidden tiles must be a multiple of 4");
+    extern __shared__ __attribute__((aligned(16))) f4 lds_y[];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int q = lane >> 4;
+    const int m = lane & 15;
+    const int64_t cand = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 16 + m;
+    const bool valid = cand < a.K;
+    f4* y = lds_y + (size_t)wave * T * 64;
+
+    const double* __restrict__ C = a.consts;   // [8][32]
+    const int S = a.S, A = a.A;
+
+    // state of candidate `cand`, dims d = 16v + 4q + r
+    double s[2][4];
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int d = 16 * v + 4 * q + r;
+            s[v][r] = (valid && d < S) ? a.state[cand * a.state_stride + d] : 0.0;
+        }
+    if (a.traj && valid) {
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * v + 4 * q + r;
+                if (d < S) a.traj[cand * S + d] = s[v][r];
+            }
+    }
+    double cost = 0.0;   // trajectory_cost = 0 (cost_functions.py:60)
+    const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
+
+    for (int h = 0; h < a.H; ++h) {
+        // ---- predict: normalise (dynamics.py:109-110), cast to f32 (TF feed) ----
+        float x0[2][4];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * v + 4 * q + r;
+                float xv = 0.f;
+                if (i < S) {
+                    xv = (float)__ddiv_rn(__dsub_rn(s[v][r], C[0 * 32 + i]), C[1 * 32 + i]);
+                } else if (i < S + A) {
+                    const int j = i - S;
+                    double av = 0.0;
+                    if (valid) {
+                        av = a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
+                                       : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
+                    }
+                    xv = (float)__ddiv_rn(__dsub_rn(av, C[2 * 32 + j]), C[3 * 32 + j]);
+                }
+                x0[v][r] = xv;
+            }
+
+        // ---- layer 0: [S+A -> h] ----
+        float x[T][4];
+        {
+            const f4* W = a.w[0];
+            for (int tb = 0; tb < T / TB; ++tb) {
+                f4 acc[TB];
+                mm_tiles<2, TB>(W + (size_t)tb * 2 * TB * 64, x0, acc, lane);
+                store_block<TB>(acc, tb * TB, a.b[0], a.act, y, lane);
+            }
+            reload<T>(x, y, lane);
+            if (a.ln) layer_norm<T>(x, a.lng[0], a.lnb[0], a.hidden, lane);
+        }
+        // ---- hidden layers 1..L-1: [h -> h] ----
+        for (int l = 1; l < a.L; ++l) {
+            const f4* W = a.w[l];
+            for (int tb = 0; tb < T / TB; ++tb) {
+                f4 acc[TB];
+                mm_tiles<T, TB>(W + (size_t)tb * T * TB * 64, x, acc, lane);
+                store_block<TB>(acc, tb * TB, a.b[l], a.act, y, lane);
+            }
+            reload<T>(x, y, lane);
+            if (a.ln) layer_norm<T>(x, a.lng[l], a.lnb[l], a.hidden, lane);
+        }
+        // ---- output layer: [h -> S], no activation (dynamics.py:70) ----
+        f4 o[2];
+        mm_tiles<T, 2>(a.w[a.L], x, o, lane);
+
+        // ---- de-normalise + residual (dynamics.py:113,116), f64, no FMA ----
+        double sn[2][4];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const f4 bv = *reinterpret_cast<const f4*>(a.b[a.L] + 16 * v + 4 * q);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * v + 4 * q + r;
+                if (d < S) {
+                    const float dn = o[v][r] + bv[r];                  // BiasAdd (f32)
+                    const double ud = __dadd_rn(__dmul_rn((double)dn, C[5 * 32 + d]), C[4 * 32 + d]);
+                    sn[v][r] = __dadd_rn(s[v][r], ud);
+                } else {
+                    sn[v][r] = 0.0;
+                }
+            }
+        }
+
+        // ---- cheetah cost (cost_functions.py:10-30), accumulated (:59-63) ----
+        if (a.cost == BCMPC_COST_CHEETAH) {
+            // dims 5,6,7 live in lane group q=1 (v=0, r=1..3); dim 17 in q=0 (v=1, r=1)
+            double pen = 0.0;
+            if (s[0][1] >= 0.2) pen += 10.0;
+            if (s[0][2] >= 0.0) pen += 10.0;
+            if (s[0][3] >= 0.0) pen += 10.0;
+            pen = __shfl(pen, m + 16);
+            const double score = __dsub_rn(pen, __ddiv_rn(__dsub_rn(sn[1][1], s[1][1]), 0.01));
+            cost = __dadd_rn(cost, score);
+        }
+        if (a.traj && valid) {
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int d = 16 * v + 4 * q + r;
+                    if (d < S) a.traj[((int64_t)(h + 1) * a.K + cand) * S + d] = sn[v][r];
+                }
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[v][r] = sn[v][r];
+    }
+    if (a.costs && valid && q == 0) a.costs[cand] = cost;
+}
+
+// ------------------------------------------------------------ argmin -------
+struct Best {
+    double c;
+    int64_t i;
+};
+
+// np.argmin: a NaN beats every number (first NaN wins); else smaller value;
+// equal values -> lower index.
+__device__ __forceinline__ bool better(const Best& a, const Best& b) {
+    const bool an = a.c != a.c, bn = b.c != b.c;
+    if (an != bn) return an;
+    if (!an && a.c != b.c) return a.c < b.c;
+    return a.i < b.i;
+}
+
+__global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
+    __shared__ double sc[16];
+    __shared__ int64_t si[16];
+    Best best{__builtin_inf(), INT64_MAX};
+    for (int64_t i = threadIdx.x; i < a.K; i += blockDim.x) {
+        const Best c{a.costs[i], i};
+        if (better(c, best)) best = c;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        Best o{__shfl_xor(best.c, off), __shfl_xor(best.i, off)};
+        if (better(o, best)) best = o;
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) { sc[wave] = best.c; si[wave] = best.i; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            const Best o{sc[w], si[w]};
+            if (better(o, best)) best = o;
+        }
+        bcmpc_result* out = a.out;
+        out->best_index = a.cand_offset + best.i;
+        out->best_cost = best.c;
+        for (int j = 0; j < BCMPC_MAX_ACTION; ++j) out->first_action[j] = 0.0;
+        if (best.i < a.K) {
+            for (int j = 0; j < a.A; ++j) {
+                out->first_action[j] =
+                    a.actions ? a.actions[best.i * a.A + j]     // action_paths[0, i*, :] (controllers.py:84-85)
+                              : rng_action(a.seed, (uint64_t)(a.cand_offset + best.i), 0, j,
+                                           a.consts[6 * 32 + j], a.consts[7 * 32 + j]);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------ launchers ----
+template <int HP>
+static hipError_t launch_hp(const RolloutArgs& a, int waves_per_block, hipStream_t st) {
+    const size_t lds = (size_t)waves_per_block * (HP / 16) * 64 * sizeof(f4);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)rollout_fp32<HP>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * (HP / 16) * 64 * 16));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int64_t waves = (a.K + 15) / 16;
+    const int64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
+    hipLaunchKernelGGL(rollout_fp32<HP>, dim3((unsigned)blocks), dim3(64 * waves_per_block), lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st) {
+    switch (hidden_padded) {
+        case 64: return launch_hp<64>(a, waves_per_block, st);
+        case 128: return launch_hp<128>(a, waves_per_block, st);
+        case 256: return launch_hp<256>(a, waves_per_block, st);
+        case 512: return launch_hp<512>(a, waves_per_block, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(1024), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace bcmpc

@@ -1,0 +1,89 @@
+"""Candidate sharding across ranks + the one per-step min-loc exchange.
+
+The K candidates of one control step are independent rollouts of the same
+initial state (controllers.py:63-71); the only cross-candidate operation is
+``np.argmin`` (controllers.py:82).  With one process per GPU
+(torch.distributed, backend "nccl" = RCCL over xGMI), rank r owns the
+contiguous global range ``shard_range(K, r, world)`` and after its local
+rollout contributes one record ``[valid, cost, index, first_action...]``.
+
+Exchange: a single ``all_gather_into_tensor`` of (3 + A) doubles per rank.
+An exact min-loc needs the f64 cost AND the index (np.argmin tie-break:
+lowest index; NaN wins) -- 128 bits that do not fit a 64-bit
+``all_reduce(MIN)`` key without rounding the cost, so the exchange is an
+all-gather of the tiny records (latency-bound, one collective per step) and
+every rank applies the same deterministic selection.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+
+def world(group=None) -> Tuple[int, int]:
+    try:
+        import torch.distributed as dist
+    except Exception:  # pragma: no cover
+        return 0, 1
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def shard_range(K: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous global candidate range of ``rank``; the first K % world ranks get one more."""
+    base, rem = divmod(int(K), int(world_size))
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def better(a: Sequence[float], b: Sequence[float]) -> bool:
+    """np.argmin order on records (valid, cost, index): invalid records lose;
+    a NaN cost beats every number; smaller cost wins; ties -> lower index."""
+    av, bv = a[0] > 0.5, b[0] > 0.5
+    if av != bv:
+        return av
+    if not av:
+        return False
+    an, bn = math.isnan(a[1]), math.isnan(b[1])
+    if an != bn:
+        return an
+    if not an and a[1] != b[1]:
+        return a[1] < b[1]
+    return a[2] < b[2]
+
+
+def select(records: np.ndarray) -> np.ndarray:
+    best = records[0]
+    for r in records[1:]:
+        if better(r, best):
+            best = r
+    return best
+
+
+def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optional[np.ndarray],
+                     action_dim: int, group=None) -> Tuple[float, int, np.ndarray]:
+    """One collective per control step; returns the global (cost, index, first_action)."""
+    import torch
+    import torch.distributed as dist
+    rank, ws = world(group)
+    rec = np.zeros(3 + action_dim, dtype=np.float64)
+    rec[0] = 1.0 if valid else 0.0
+    rec[1] = cost
+    rec[2] = float(index)
+    if first_action is not None:
+        rec[3:] = first_action
+    if ws == 1:
+        return float(rec[1]), int(rec[2]), rec[3:].copy()
+    backend = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    t = torch.from_numpy(rec).to(dev)
+    out = torch.empty(ws * rec.size, dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, t, group=group)
+    recs = out.view(ws, rec.size).cpu().numpy()
+    best = select(recs)
+    if best[0] < 0.5:
+        raise ValueError("attempt to get argmin of an empty sequence")
+    return float(best[1]), int(best[2]), best[3:].copy()

@@ -1,0 +1,122 @@
+"""NNDynamicsModel weight container (dynamics.py:7-119 API) for the engine.
+
+The reference builds a TF1 graph (dynamics.py:54-71) whose variables the
+rollout engine must read.  This class is the MI355X-side container: the
+same constructor signature, the dense kernels in TF layout ``[in, out]`` held
+as torch tensors (PyTorch-ROCm is used as the weight store only), the
+normalization stats of dynamics.py:41, and a ``version`` stamp that the
+controller's re-sync hook compares.
+
+``predict`` (dynamics.py:106-119) runs one horizon step of the same HIP
+kernel in per-candidate-state mode; it never computes on the host.
+``fit`` (dynamics.py:81-104, Adam on normalized deltas) is outside the
+rollout hot path and not provided here.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .engine import MLPSpec, RolloutEngine
+from .weights import _act_name
+
+
+class NNDynamicsModel():
+    def __init__(self,
+                 env,
+                 n_layers,
+                 size,
+                 activation,
+                 output_activation,
+                 normalization,
+                 batch_size,
+                 iterations,
+                 learning_rate,
+                 sess=None,
+                 layer_norm: bool = False,
+                 seed: int = 0,
+                 device: Optional[int] = None):
+        import torch
+        if output_activation is not None:
+            raise ValueError("output_activation must be None (train_mpc_ppo.py:540)")
+        self.env = env
+        S = int(np.prod(env.observation_space.shape))
+        A = int(np.prod(env.action_space.shape))
+        self.state_dim, self.action_dim = S, A
+        self.n_layers, self.size = int(n_layers), int(size)
+        self.activation = _act_name(activation)
+        self.layer_norm = bool(layer_norm)
+        (self.mean_obs, self.std_obs, self.mean_action, self.std_action, self.mean_reward, self.std_reward,
+         self.mean_nxt_state, self.std_nxt_state, self.mean_deltas, self.std_deltas) = normalization
+        self.batch_size, self.iterations, self.learning_rate, self.sess = batch_size, iterations, learning_rate, sess
+        self.device = device
+        dims = [S + A] + [self.size] * self.n_layers + [S]
+        g = torch.Generator().manual_seed(seed)
+        # tf.layers.dense defaults: glorot_uniform kernel, zero bias
+        self.kernels = []
+        for i in range(len(dims) - 1):
+            lim = float(np.sqrt(6.0 / (dims[i] + dims[i + 1])))
+            self.kernels.append((torch.rand(dims[i], dims[i + 1], generator=g) * 2 - 1) * lim)
+        self.biases = [torch.zeros(d) for d in dims[1:]]
+        self.ln_gamma = [torch.ones(self.size) for _ in range(self.n_layers)] if self.layer_norm else None
+        self.ln_beta = [torch.zeros(self.size) for _ in range(self.n_layers)] if self.layer_norm else None
+        self.version = 1
+        self._engines = {}
+
+    # ------------------------------------------------------------ weights I/O
+    def load_weights(self, kernels: Sequence, biases: Sequence, ln_gamma: Optional[Sequence] = None,
+                     ln_beta: Optional[Sequence] = None) -> None:
+        """Replace the weights (e.g. after an external fit); bumps ``version``."""
+        import torch
+        if len(kernels) != self.n_layers + 1 or len(biases) != self.n_layers + 1:
+            raise ValueError("expected n_layers + 1 kernels and biases")
+        for i, (k, b) in enumerate(zip(kernels, biases)):
+            k = torch.as_tensor(np.asarray(k, dtype=np.float32))
+            b = torch.as_tensor(np.asarray(b, dtype=np.float32))
+            if k.shape != self.kernels[i].shape or b.shape != self.biases[i].shape:
+                raise ValueError(f"layer {i}: shape {tuple(k.shape)} != {tuple(self.kernels[i].shape)}")
+            self.kernels[i], self.biases[i] = k.clone(), b.clone()
+        if self.layer_norm:
+            if ln_gamma is None or ln_beta is None:
+                raise ValueError("layer_norm model needs ln_gamma / ln_beta")
+            self.ln_gamma = [torch.as_tensor(np.asarray(x, dtype=np.float32)).clone() for x in ln_gamma]
+            self.ln_beta = [torch.as_tensor(np.asarray(x, dtype=np.float32)).clone() for x in ln_beta]
+        self.version += 1
+
+    def mlp_spec(self) -> MLPSpec:
+        f = lambda t: t.detach().cpu().numpy().astype(np.float32)  # noqa: E731
+        return MLPSpec([f(k) for k in self.kernels], [f(b) for b in self.biases], self.activation,
+                       [f(x) for x in self.ln_gamma] if self.layer_norm else None,
+                       [f(x) for x in self.ln_beta] if self.layer_norm else None)
+
+    def normalization(self) -> List[np.ndarray]:
+        return [self.mean_obs, self.std_obs, self.mean_action, self.std_action, self.mean_reward,
+                self.std_reward, self.mean_nxt_state, self.std_nxt_state, self.mean_deltas, self.std_deltas]
+
+    # ------------------------------------------------------------ dynamics.py:106-119
+    def predict(self, unnormalized_state, unnormalized_action):
+        import torch
+        s = np.ascontiguousarray(unnormalized_state, dtype=np.float64)
+        a = np.ascontiguousarray(unnormalized_action, dtype=np.float64)
+        if s.ndim != 2 or a.ndim != 2 or s.shape[0] != a.shape[0]:
+            raise ValueError("predict expects states [K, S] and actions [K, A]")
+        K = s.shape[0]
+        dev_index = self.device if self.device is not None else torch.cuda.current_device()
+        eng = self._engines.get(K)
+        if eng is None:
+            eng = RolloutEngine(self.state_dim, self.action_dim, self.size, self.n_layers, self.activation,
+                                self.layer_norm, 1, K, device=dev_index, cost="none")
+            self._engines[K] = eng
+        eng.set_weights(self.mlp_spec(), self.normalization(), self.version)
+        dev = torch.device("cuda", dev_index)
+        d_s = torch.from_numpy(s).to(dev)
+        d_a = torch.from_numpy(a).to(dev).reshape(1, K, self.action_dim)
+        d_traj = torch.empty((2, K, self.state_dim), dtype=torch.float64, device=dev)
+        eng.rollout_async(d_s.data_ptr(), self.state_dim, d_a.data_ptr(), 0, 0, None, d_traj.data_ptr(), None,
+                          torch.cuda.current_stream(dev).cuda_stream)
+        return d_traj[1].cpu().numpy()
+
+    def fit(self, data):  # dynamics.py:81-104
+        raise NotImplementedError("dynamics training is outside the rollout engine (SURVEY 8f rank 4); "
+                                  "fit elsewhere and call load_weights()")

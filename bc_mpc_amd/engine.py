@@ -1,0 +1,199 @@
+"""RolloutEngine: one device's share of MPCcontroller.get_action on libbcmpc.
+
+Thin host wrapper over the C ABI (include/bcmpc.h).  All arithmetic happens in
+the HIP kernels; this file only marshals pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+
+_ACT = {"tanh": _lib.ACT_TANH, "relu": _lib.ACT_RELU}
+
+
+@dataclass
+class MLPSpec:
+    """Dense stack in TF layout: kernels[l] is ``[in, out]`` (tf.layers.dense,
+    dynamics.py:67,70), biases[l] ``[out]``; LN params per hidden layer."""
+    kernels: List[np.ndarray]
+    biases: List[np.ndarray]
+    activation: str = "tanh"
+    ln_gamma: Optional[List[np.ndarray]] = None
+    ln_beta: Optional[List[np.ndarray]] = None
+
+    @property
+    def n_layers(self) -> int:
+        return len(self.kernels) - 1
+
+    @property
+    def hidden(self) -> int:
+        return int(np.shape(self.kernels[0])[1])
+
+    @property
+    def layer_norm(self) -> bool:
+        return self.ln_gamma is not None
+
+
+@dataclass
+class StepResult:
+    best_index: int            # global candidate index (np.argmin semantics)
+    best_cost: float
+    first_action: np.ndarray   # (A,) f64
+    costs: Optional[np.ndarray] = None
+
+
+def _f32(a) -> np.ndarray:
+    if hasattr(a, "detach"):
+        a = a.detach().cpu().numpy()
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _f64(a) -> np.ndarray:
+    if hasattr(a, "detach"):
+        a = a.detach().cpu().numpy()
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class RolloutEngine:
+    """Owns one bcmpc_engine (one device, one candidate shard of size K)."""
+
+    def __init__(self, state_dim: int, action_dim: int, hidden: int, n_layers: int,
+                 activation: str, layer_norm: bool, horizon: int, num_paths: int,
+                 device: int = 0, cost: str = "cheetah"):
+        self._lib = _lib.load()
+        if activation not in _ACT:
+            raise ValueError(f"unsupported activation {activation!r} (tanh | relu)")
+        cfg = _lib.Config()
+        cfg.state_dim, cfg.action_dim, cfg.hidden, cfg.n_layers = state_dim, action_dim, hidden, n_layers
+        cfg.activation = _ACT[activation]
+        cfg.layer_norm = int(bool(layer_norm))
+        cfg.horizon = int(horizon)
+        cfg.cost = _lib.COST_CHEETAH if cost == "cheetah" else _lib.COST_NONE
+        cfg.num_paths = int(num_paths)
+        cfg.precision = _lib.PREC_FP32
+        cfg.device = int(device)
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.state_dim, self.action_dim = state_dim, action_dim
+        self.hidden, self.n_layers, self.activation = hidden, n_layers, activation
+        self.layer_norm, self.horizon, self.num_paths = bool(layer_norm), horizon, num_paths
+        self.device, self.cost = device, cost
+        self._keep = []
+
+    # ------------------------------------------------------------------ weights
+    def set_weights(self, spec: MLPSpec, normalization: Sequence, version: int) -> None:
+        """Re-sync hook; idempotent on ``version``."""
+        if spec.n_layers != self.n_layers or spec.hidden != self.hidden:
+            raise ValueError("weight shapes do not match the engine configuration")
+        ks = [_f32(k) for k in spec.kernels]
+        bs = [_f32(b) for b in spec.biases]
+        S, A, h = self.state_dim, self.action_dim, self.hidden
+        exp = [(S + A, h)] + [(h, h)] * (self.n_layers - 1) + [(h, S)]
+        for k, b, e in zip(ks, bs, exp):
+            if k.shape != e or b.shape != (e[1],):
+                raise ValueError(f"kernel {k.shape}/bias {b.shape} != expected {e}")
+        FP = ctypes.POINTER(ctypes.c_float)
+        karr = (FP * len(ks))(*[k.ctypes.data_as(FP) for k in ks])
+        barr = (FP * len(bs))(*[b.ctypes.data_as(FP) for b in bs])
+        w = _lib.Weights()
+        w.kernels, w.biases = karr, barr
+        keep = [ks, bs, karr, barr]
+        if self.layer_norm:
+            if not spec.layer_norm:
+                raise ValueError("engine built with layer_norm but weights have no LN params")
+            gs = [_f32(g) for g in spec.ln_gamma]
+            bts = [_f32(b) for b in spec.ln_beta]
+            garr = (FP * len(gs))(*[g.ctypes.data_as(FP) for g in gs])
+            btarr = (FP * len(bts))(*[b.ctypes.data_as(FP) for b in bts])
+            w.ln_gamma, w.ln_beta = garr, btarr
+            keep += [gs, bts, garr, btarr]
+        (mean_obs, std_obs, mean_action, std_action, *_rest) = normalization
+        mean_deltas, std_deltas = normalization[8], normalization[9]
+        stats = [_f64(x) for x in (mean_obs, std_obs, mean_action, std_action, mean_deltas, std_deltas)]
+        for x, n in zip(stats, (S, S, A, A, S, S)):
+            if x.shape != (n,):
+                raise ValueError(f"normalization vector of shape {x.shape}, expected ({n},)")
+        (w.mean_obs, w.std_obs, w.mean_action, w.std_action, w.mean_deltas, w.std_deltas) = [_dp(x) for x in stats]
+        keep.append(stats)
+        _lib.check(self._lib.bcmpc_set_weights(self._h, ctypes.byref(w), ctypes.c_uint64(version)))
+
+    @property
+    def weights_version(self) -> int:
+        return int(self._lib.bcmpc_weights_version(self._h))
+
+    def set_action_bounds(self, low, high) -> None:
+        lo, hi = _f64(low), _f64(high)
+        _lib.check(self._lib.bcmpc_set_action_bounds(self._h, _dp(lo), _dp(hi)))
+
+    # ------------------------------------------------------------------ rollout
+    def get_action(self, state, actions: Optional[np.ndarray] = None, seed: int = 0,
+                   cand_offset: int = 0, return_costs: bool = False) -> StepResult:
+        """Synchronous host-memory control step (bcmpc_get_action)."""
+        st = _f64(state).reshape(-1)
+        if st.shape[0] != self.state_dim:
+            raise ValueError(f"state has {st.shape[0]} dims, expected {self.state_dim}")
+        act_p = None
+        if actions is not None:
+            actions = _f64(actions)
+            if actions.shape != (self.horizon, self.num_paths, self.action_dim):
+                raise ValueError(f"actions shape {actions.shape} != (H, K, A) = "
+                                 f"{(self.horizon, self.num_paths, self.action_dim)}")
+            act_p = _dp(actions)
+        res = _lib.Result()
+        costs = np.empty(self.num_paths, dtype=np.float64) if return_costs else None
+        _lib.check(self._lib.bcmpc_get_action(
+            self._h, _dp(st), act_p, ctypes.c_uint64(seed & (2**64 - 1)), ctypes.c_int64(cand_offset),
+            ctypes.byref(res), _dp(costs) if costs is not None else None))
+        return StepResult(int(res.best_index), float(res.best_cost),
+                          np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
+
+    def rollout_async(self, d_state: int, state_stride: int, d_actions: Optional[int], seed: int,
+                      cand_offset: int, d_costs: Optional[int], d_traj: Optional[int],
+                      d_result: Optional[int], stream: Optional[int] = None) -> None:
+        """Device-pointer form (bcmpc_rollout_async); no host synchronisation.
+
+        ``stream`` is a raw hipStream_t (e.g. ``torch.cuda.current_stream().cuda_stream``;
+        0 is the null stream); ``None`` means the engine's own stream."""
+        if stream is None:
+            stream = self.stream
+        _lib.check(self._lib.bcmpc_rollout_async(
+            self._h, ctypes.c_void_p(d_state), ctypes.c_int64(state_stride),
+            ctypes.c_void_p(d_actions) if d_actions else None, ctypes.c_uint64(seed & (2**64 - 1)),
+            ctypes.c_int64(cand_offset), ctypes.c_void_p(d_costs) if d_costs else None,
+            ctypes.c_void_p(d_traj) if d_traj else None, ctypes.c_void_p(d_result) if d_result else None,
+            ctypes.c_void_p(stream)))
+
+    @property
+    def stream(self) -> int:
+        return int(self._lib.bcmpc_stream(self._h) or 0)
+
+    def last_kernel_ms(self) -> Tuple[float, float]:
+        r, m = ctypes.c_float(), ctypes.c_float()
+        _lib.check(self._lib.bcmpc_last_kernel_ms(self._h, ctypes.byref(r), ctypes.byref(m)))
+        return float(r.value), float(m.value)
+
+    def info(self) -> dict:
+        hp, wb, wpb = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+        _lib.check(self._lib.bcmpc_engine_info(self._h, ctypes.byref(hp), ctypes.byref(wb), ctypes.byref(wpb)))
+        return dict(hidden_padded=hp.value, packed_weight_bytes=wb.value, waves_per_block=wpb.value)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.bcmpc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,111 @@
+"""Pull the dynamics-MLP weights and normalization out of a ``dyn_model``.
+
+``MPCcontroller`` receives ``dyn_model`` (controllers.py:30) and the reference
+only ever calls ``dyn_model.predict`` (controllers.py:70).  The engine instead
+runs the MLP on the GPU, so it needs the weights.  Supported containers:
+
+1. ``bc_mpc_amd.dynamics.NNDynamicsModel`` (the torch weight container),
+2. any object whose ``.weights`` has ``kernels``/``biases``/``activation``
+   (+ ``ln_gamma``/``ln_beta``) -- e.g. NumPy stand-ins of NNDynamicsModel,
+3. the reference's TF1 ``dynamics.NNDynamicsModel``: variables
+   ``NNDynamicsModel/dense{,_1,..}/{kernel,bias}:0`` and
+   ``NNDynamicsModel/LayerNorm{,_1,..}/{gamma,beta}:0`` read through its
+   ``sess`` (dynamics.py:31-38, 44); the activation is read from the graph's
+   op types.  Its ``fit`` (dynamics.py:81) is wrapped to bump a version stamp
+   so weights are re-synced after every refit (train_mpc_ppo.py:279).
+
+Normalization stats are the attributes set at dynamics.py:41.
+"""
+from __future__ import annotations
+
+import hashlib
+import re
+from typing import List, Tuple
+
+import numpy as np
+
+from .engine import MLPSpec
+
+_NORM_ATTRS = ("mean_obs", "std_obs", "mean_action", "std_action", "mean_reward", "std_reward",
+               "mean_nxt_state", "std_nxt_state", "mean_deltas", "std_deltas")
+
+
+def normalization_of(dyn_model) -> List[np.ndarray]:
+    out = []
+    for name in _NORM_ATTRS:
+        v = getattr(dyn_model, name, None)
+        out.append(np.zeros(1) if v is None else np.asarray(v, dtype=np.float64))
+    return out
+
+
+def _act_name(act) -> str:
+    if isinstance(act, str):
+        return act.lower()
+    name = getattr(act, "__name__", "") or type(act).__name__
+    name = name.lower()
+    if "tanh" in name:
+        return "tanh"
+    if "relu" in name:
+        return "relu"
+    raise ValueError(f"unsupported activation {act!r}")
+
+
+def _tf_weights(dyn_model) -> MLPSpec:  # pragma: no cover - TF1 is absent in this image
+    import tensorflow as tf
+    scope = getattr(dyn_model, "scope", "NNDynamicsModel")
+    var_list = [v for v in tf.global_variables() if v.name.startswith(scope + "/")]
+    vals = dyn_model.sess.run(var_list)
+    by_name = {v.name: x for v, x in zip(var_list, vals)}
+
+    def idx(name, base):
+        m = re.match(rf"{scope}/{base}(?:_(\d+))?/", name)
+        return None if m is None else (0 if m.group(1) is None else int(m.group(1)))
+
+    dense = sorted({idx(n, "dense") for n in by_name if idx(n, "dense") is not None})
+    kernels = [by_name[f"{scope}/dense{'' if i == 0 else f'_{i}'}/kernel:0"] for i in dense]
+    biases = [by_name[f"{scope}/dense{'' if i == 0 else f'_{i}'}/bias:0"] for i in dense]
+    lns = sorted({idx(n, "LayerNorm") for n in by_name if idx(n, "LayerNorm") is not None})
+    g = [by_name[f"{scope}/LayerNorm{'' if i == 0 else f'_{i}'}/gamma:0"] for i in lns] or None
+    b = [by_name[f"{scope}/LayerNorm{'' if i == 0 else f'_{i}'}/beta:0"] for i in lns] or None
+    ops = {op.type for op in dyn_model.sess.graph.get_operations() if op.name.startswith(scope + "/dense")}
+    act = "tanh" if "Tanh" in ops else "relu"
+    return MLPSpec(kernels, biases, act, g, b)
+
+
+def _install_fit_hook(dyn_model) -> None:
+    if getattr(dyn_model, "_bcmpc_fit_hooked", False) or not hasattr(dyn_model, "fit"):
+        return
+    fit = dyn_model.fit
+
+    def fit_and_bump(*args, **kwargs):
+        out = fit(*args, **kwargs)
+        dyn_model._bcmpc_version = getattr(dyn_model, "_bcmpc_version", 1) + 1
+        return out
+
+    dyn_model.fit = fit_and_bump
+    dyn_model._bcmpc_version = getattr(dyn_model, "_bcmpc_version", 1)
+    dyn_model._bcmpc_fit_hooked = True
+
+
+def extract(dyn_model) -> Tuple[MLPSpec, List[np.ndarray], int]:
+    """Return ``(spec, normalization10, version)`` for the engine."""
+    norm = normalization_of(dyn_model)
+    if hasattr(dyn_model, "mlp_spec"):                      # bc_mpc_amd.dynamics.NNDynamicsModel
+        return dyn_model.mlp_spec(), norm, int(dyn_model.version)
+    w = getattr(dyn_model, "weights", None)
+    if w is not None and hasattr(w, "kernels"):             # NumPy stand-ins
+        spec = MLPSpec([np.asarray(k) for k in w.kernels], [np.asarray(b) for b in w.biases],
+                       _act_name(getattr(w, "activation", "tanh")),
+                       getattr(w, "ln_gamma", None), getattr(w, "ln_beta", None))
+        version = getattr(dyn_model, "version", None)
+        if version is None:      # no stamp: content digest (~1 MB of weights, <1 ms)
+            d = hashlib.blake2b(digest_size=8)
+            for a in list(w.kernels) + list(w.biases) + list(getattr(w, "ln_gamma", None) or []) \
+                    + list(getattr(w, "ln_beta", None) or []):
+                d.update(np.ascontiguousarray(a, dtype=np.float32).tobytes())
+            version = int.from_bytes(d.digest(), "little") & (2**63 - 1)
+        return spec, norm, int(version)
+    if hasattr(dyn_model, "sess"):                          # reference TF1 NNDynamicsModel
+        _install_fit_hook(dyn_model)
+        return _tf_weights(dyn_model), norm, int(dyn_model._bcmpc_version)
+    raise TypeError(f"cannot read dynamics weights from {type(dyn_model).__name__}")

@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Benchmark: random-shooting MPC get_action on MI355X (libbcmpc).
+
+One "step" = one control step of MPCcontroller.get_action (controllers.py:57-88):
+fan out the state, roll K candidate action sequences H steps through the
+dynamics MLP, score them with the cheetah cost, argmin, return the first
+action to the host.  Inputs (state, [H, K, A] f64 actions) are resident in HBM
+before the timed region (synthetic HalfCheetah-dim data, random-init weights
+of the configured architecture).
+
+Multi-GPU (driver: torch.distributed.run, one rank per GPU): weak scaling --
+each rank owns K candidates of its own (global K = N*K); per step every rank
+runs its shard and the ranks agree on the global argmin through one
+all-gather (bc_mpc_amd.distributed).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# BASELINE.json configs (S=20, A=6, 2x500 tanh unless stated)
+WORKLOADS = {
+    "cfg1": dict(K=1000, H=15, hidden=500, L=2, act="tanh"),
+    "cfg2": dict(K=4096, H=20, hidden=500, L=2, act="tanh"),
+    "cfg3": dict(K=65536, H=20, hidden=500, L=2, act="tanh"),
+    "cfg4_shard": dict(K=32768, H=20, hidden=500, L=2, act="tanh"),   # 262144 / 8 per GPU
+    "ppo_defaults": dict(K=400, H=7, hidden=256, L=2, act="relu"),
+}
+S_DIM, A_DIM = 20, 6
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix, v_mfma_f32_16x16x4_f32
+HBM_PEAK_GBS = 8000.0
+
+
+def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM):
+    """Algorithmic MLP FLOPs per candidate-step: 2*[(S+A)h + (L-1)h^2 + hS]."""
+    return 2 * ((S + A) * hidden + (L - 1) * hidden * hidden + hidden * S)
+
+
+def cpu_baseline(spec_w, norm, state, H, budget_s):
+    """The oracle (NumPy restatement of the reference path, kind "port") timed on
+    the host cores over a bounded sample of the same workload."""
+    from oracle import mpc_oracle as orc
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    dyn = orc.NumpyDynamics(spec_w, norm)
+    Ks = 8192
+    rs = np.random.RandomState(0)
+    done, calls, t0 = 0, 0, time.perf_counter()
+    while True:
+        orc.get_action(dyn, state, H, Ks, -np.ones(A_DIM), np.ones(A_DIM), rng=rs)
+        done += Ks * H
+        calls += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    return dict(value=done / el, unit="candidate-steps/s", cores=int(threads), kind="port",
+                sample=f"{calls} oracle get_action calls at K={Ks} (1/8 of cfg3's K), H={H}, "
+                       f"2x500 tanh, OpenBLAS {threads} threads, {el:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
+    ap.add_argument("--actions", default="hbm", choices=["hbm", "device"],
+                    help="hbm: [H,K,A] f64 actions resident in HBM (parity mode input); device: in-kernel Philox")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from bc_mpc_amd import distributed as bdist
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    import bc_mpc_amd._lib as L_
+
+    wl = WORKLOADS[args.workload]
+    K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
+    offset = rank * K
+
+    # synthetic inputs: glorot kernels, 0.1 N biases, synthetic stats/state
+    rs = np.random.RandomState(1000)
+    dims = [S_DIM + A_DIM] + [hidden] * L + [S_DIM]
+    kernels, biases = [], []
+    for i in range(len(dims) - 1):
+        r = np.random.RandomState(1000 + i)
+        lim = np.sqrt(6.0 / (dims[i] + dims[i + 1]))
+        kernels.append(r.uniform(-lim, lim, (dims[i], dims[i + 1])).astype(np.float32))
+        biases.append((0.1 * r.standard_normal(dims[i + 1])).astype(np.float32))
+    r7 = np.random.RandomState(7)
+    mean_obs = 0.1 * r7.standard_normal(S_DIM)
+    std_obs = np.abs(r7.standard_normal(S_DIM)) * 0.5 + 0.2
+    mean_d = 0.005 * r7.standard_normal(S_DIM)
+    std_d = 0.05 * (np.abs(r7.standard_normal(S_DIM)) + 0.2)
+    norm = [mean_obs, std_obs, np.zeros(A_DIM), np.full(A_DIM, 1 / np.sqrt(3)), np.zeros(1), np.zeros(1),
+            mean_obs, std_obs, mean_d, std_d]
+    state = mean_obs + 0.5 * std_obs * np.random.RandomState(11).standard_normal(S_DIM)
+
+    eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local)
+    eng.set_weights(MLPSpec(kernels, biases, act), norm, 1)
+    d_state = torch.from_numpy(state).to(dev)
+    d_actions = None
+    if args.actions == "hbm":
+        host = np.random.RandomState(1234 + rank).uniform(-1, 1, (H, K, A_DIM))
+        d_actions = torch.from_numpy(host).to(dev)
+        del host
+    d_costs = torch.empty(K, dtype=torch.float64, device=dev)
+    d_res = torch.zeros(__import__("ctypes").sizeof(L_.Result), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i):
+        eng.rollout_async(d_state.data_ptr(), 0, d_actions.data_ptr() if d_actions is not None else None,
+                          0xB0B + i, offset, d_costs.data_ptr(), None, d_res.data_ptr(), stream.cuda_stream)
+        raw = d_res.cpu().numpy()                       # D2H of the result; syncs the stream
+        best_i = int(raw[:8].view(np.int64)[0])
+        best_c = float(raw[8:16].view(np.float64)[0])
+        first = raw[16:16 + 8 * A_DIM].view(np.float64).copy()
+        return bdist.allgather_minloc(True, best_c, best_i, first, A_DIM)
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kern_ms, step_s = [], []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ts = time.perf_counter()
+        step(args.warmup + i)
+        step_s.append(time.perf_counter() - ts)
+        kern_ms.append(eng.last_kernel_ms()[0])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_cand_steps = K * world * H * args.steps
+    value = total_cand_steps / elapsed
+    fpcs = flop_per_cand_step(hidden, L)
+    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    achieved_tflops = K * H * fpcs / kern_avg_s / 1e12
+    out = {
+        "metric": "candidate-steps/sec (K x H per get_action), HalfCheetah dims",
+        "value": value,
+        "unit": "candidate-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (HalfCheetah dims s=20,a=6; random-init 2x500 tanh dynamics MLP; "
+                f"actions {'resident in HBM as [H,K,6] f64' if args.actions == 'hbm' else 'drawn in-kernel (Philox)'})",
+        "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
+                               f"{L}x{hidden} {act}, fp32 MFMA, 1 RCCL all-gather min-loc per step",
+                   "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
+                   "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}"},
+        "p50_ms": float(np.percentile(step_s, 50) * 1e3),
+        "p90_ms": float(np.percentile(step_s, 90) * 1e3),
+        "kernel_ms_avg": kern_avg_s * 1e3,
+        "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved_tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "rollout_fp32<512>", "flop_per_launch": K * H * fpcs,
+                     "flop_per_cand_step": fpcs},
+        "cpu_baseline": None,
+    }
+    prof = os.path.join(REPO, "profiles", "traffic_per_launch.json")
+    if os.path.exists(prof):
+        try:
+            tr = json.load(open(prof)).get(args.workload)
+            if tr:
+                out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+        except Exception:
+            pass
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import mpc_oracle as orc
+        w = orc.MLPWeights(kernels, biases, act)
+        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

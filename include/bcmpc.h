@@ -1,0 +1,151 @@
+/*
+ * bcmpc.h -- C ABI of the MI355X random-shooting MPC rollout engine.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   controllers.MPCcontroller.get_action            (controllers.py:57-88)
+ *     -> H x dynamics.NNDynamicsModel.predict       (dynamics.py:106-119, MLP dynamics.py:54-71)
+ *     -> cost_functions.trajectory_cost_fn(cheetah) (cost_functions.py:9-30, :59-63)
+ *     -> np.argmin + first action                   (controllers.py:82-85)
+ * The reference binds that path in-process from Python; the host mirror
+ * (bc_mpc_amd/controllers.py) binds these symbols through ctypes.
+ *
+ * Plain C: pointers + sizes, no torch/HIP types in the signatures (streams
+ * are passed as void*).  Every entry point returns a bcmpc_status; on error
+ * bcmpc_last_error() returns a thread-local message.  One engine per device
+ * per host thread; an engine is not re-entrant.
+ */
+#ifndef BCMPC_H_
+#define BCMPC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCMPC_ABI_VERSION 1
+#define BCMPC_MAX_LAYERS 8      /* hidden layers supported (dynamics.py:66 n_layers) */
+#define BCMPC_MAX_STATE 32      /* S: observation dim (HalfCheetah: 20, cheetah_env.py:21-27) */
+#define BCMPC_MAX_INPUT 32      /* S + A (dynamics.py:26 concat) */
+#define BCMPC_MAX_ACTION 16
+
+typedef enum bcmpc_status {
+    BCMPC_OK = 0,
+    BCMPC_ERR_ARG = 1,          /* bad argument (Python: ValueError)          */
+    BCMPC_ERR_UNSUPPORTED = 2,  /* shape/mode this build does not implement    */
+    BCMPC_ERR_HIP = 3,          /* HIP runtime failure (Python: RuntimeError)  */
+    BCMPC_ERR_STATE = 4,        /* e.g. rollout before set_weights             */
+    BCMPC_ERR_EMPTY = 5         /* K == 0: np.argmin of an empty sequence      */
+} bcmpc_status;
+
+typedef enum bcmpc_activation {  /* dynamics.py:60 activation / train_mpc_ppo.py:539 */
+    BCMPC_ACT_TANH = 0,
+    BCMPC_ACT_RELU = 1
+} bcmpc_activation;
+
+typedef enum bcmpc_cost {
+    BCMPC_COST_CHEETAH = 0,     /* fused cheetah_cost_fn (cost_functions.py:10-30) */
+    BCMPC_COST_NONE = 1         /* no fused cost: caller scores the trajectory     */
+} bcmpc_cost;
+
+typedef enum bcmpc_precision {
+    BCMPC_PREC_FP32 = 0         /* f32 MLP on v_mfma_f32_16x16x4_f32 (exact f32 fma chain) */
+} bcmpc_precision;
+
+/* Replaces the constructor arguments of MPCcontroller (controllers.py:28-35)
+ * plus the NNDynamicsModel shape (dynamics.py:8-19, build_network :54-62). */
+typedef struct bcmpc_config {
+    int32_t state_dim;    /* S  (env.observation_space.shape[0], dynamics.py:23)  */
+    int32_t action_dim;   /* A  (env.action_space.shape[0], dynamics.py:24)       */
+    int32_t hidden;       /* h  (dynamics.py:59 size)                              */
+    int32_t n_layers;     /* L  (dynamics.py:58 n_layers)                          */
+    int32_t activation;   /* bcmpc_activation                                      */
+    int32_t layer_norm;   /* FLAGS.LAYER_NORM (dynamics.py:68)                     */
+    int32_t horizon;      /* H  (controllers.py:31 horizon)                        */
+    int32_t cost;         /* bcmpc_cost                                            */
+    int64_t num_paths;    /* K on this device (controllers.py:33 num_simulated_paths) */
+    int32_t precision;    /* bcmpc_precision                                       */
+    int32_t device;       /* HIP device ordinal                                    */
+    int32_t reserved[8];  /* must be zero                                          */
+} bcmpc_config;
+
+/* Replaces the state NNDynamicsModel holds: TF variables
+ * NNDynamicsModel/dense{,_1,..}/{kernel,bias} (+ LayerNorm/{gamma,beta}) and
+ * the normalization stats of dynamics.py:41.  Host pointers, copied. */
+typedef struct bcmpc_weights {
+    const float* const* kernels;   /* L+1 arrays, kernel[l] is [in, out] row-major  */
+    const float* const* biases;    /* L+1 arrays of length out                      */
+    const float* const* ln_gamma;  /* L arrays of length h, or NULL when LN is off  */
+    const float* const* ln_beta;   /* L arrays of length h, or NULL                 */
+    const double* mean_obs;        /* S */
+    const double* std_obs;         /* S */
+    const double* mean_action;     /* A */
+    const double* std_action;      /* A */
+    const double* mean_deltas;     /* S */
+    const double* std_deltas;      /* S */
+} bcmpc_weights;
+
+/* Output of one control step (controllers.py:82-85). */
+typedef struct bcmpc_result {
+    int64_t best_index;                       /* global candidate index, np.argmin semantics */
+    double best_cost;                         /* costs[best_index] (controllers.py:83)       */
+    double first_action[BCMPC_MAX_ACTION];    /* action_paths[0, best_index, :]              */
+} bcmpc_result;
+
+typedef struct bcmpc_engine bcmpc_engine;
+
+int bcmpc_abi_version(void);
+const char* bcmpc_last_error(void);
+
+/* MPCcontroller.__init__ (controllers.py:28-41) + device allocation. */
+int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out);
+int bcmpc_destroy(bcmpc_engine* eng);
+
+/* Weight re-sync hook: idempotent on `version`; a new version
+ * re-packs the dense kernels into MFMA fragment order on the device. */
+int bcmpc_set_weights(bcmpc_engine* eng, const bcmpc_weights* w, uint64_t version);
+uint64_t bcmpc_weights_version(const bcmpc_engine* eng);
+
+/* env.action_space.low / .high (controllers.py:53). Defaults: [-1, 1]^A. */
+int bcmpc_set_action_bounds(bcmpc_engine* eng, const double* low, const double* high);
+
+/* MPCcontroller.get_action (controllers.py:57-88), synchronous, host memory.
+ *   state    : S doubles (tiled K times, controllers.py:63)
+ *   actions  : [H, K, A] doubles in C order (the array np.random.uniform returns
+ *              at controllers.py:53), or NULL => draw them on the device with
+ *              Philox4x32-10 keyed by (seed, cand_offset + k, h, j)
+ *   cand_offset : global index of this device's first candidate (multi-GPU shard)
+ *   out      : best index (global) / cost / first action
+ *   costs_out: optional K doubles, per-candidate trajectory cost (cost_functions.py:59-63) */
+int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actions,
+                     uint64_t seed, int64_t cand_offset, bcmpc_result* out, double* costs_out);
+
+/* Device-memory, asynchronous form (no host sync; graph-capturable).
+ *   d_state      : device, S doubles, or [K, S] when state_stride == S (predict mode,
+ *                  dynamics.py:106 on per-candidate states)
+ *   d_actions    : device [H, K, A] doubles, or NULL => device RNG
+ *   d_costs      : device K doubles (required when cost == CHEETAH)
+ *   d_traj       : device [H+1, K, S] doubles or NULL (states_paths_all, controllers.py:65-74)
+ *   d_result     : device bcmpc_result or NULL (argmin + first action)
+ *   stream       : hipStream_t the launches are enqueued on, used verbatim (NULL is HIP's
+ *                  null stream; pass bcmpc_stream(eng) for the engine's own stream) */
+int bcmpc_rollout_async(bcmpc_engine* eng, const double* d_state, int64_t state_stride,
+                        const double* d_actions, uint64_t seed, int64_t cand_offset,
+                        double* d_costs, double* d_traj, bcmpc_result* d_result, void* stream);
+
+/* Device stream the engine launches on (hipStream_t as void*). */
+void* bcmpc_stream(bcmpc_engine* eng);
+
+/* Timing of the last rollout kernel launched through bcmpc_get_action /
+ * bcmpc_rollout_async, in milliseconds (HIP events on the launch stream);
+ * requires the launch to have completed. */
+int bcmpc_last_kernel_ms(bcmpc_engine* eng, float* rollout_ms, float* argmin_ms);
+
+/* Static shape facts for tests: padded hidden size and packed weight bytes. */
+int bcmpc_engine_info(const bcmpc_engine* eng, int32_t* hidden_padded, int64_t* packed_weight_bytes,
+                      int32_t* waves_per_block);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BCMPC_H_ */

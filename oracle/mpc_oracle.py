@@ -1,0 +1,305 @@
+"""CPU oracle for the random-shooting MPC hot path -- TEST INFRASTRUCTURE ONLY.
+
+This module is the *checker*, never the product.  Only ``tests/``,
+``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py`` may
+import it.  The shipped path (``bc_mpc_amd``) never imports anything under
+``oracle/`` and fails loudly when its HIP library is missing.
+
+It is a NumPy restatement of the reference path, function by function:
+
+* ``NumpyDynamics.predict``   <- ``dynamics.py:106-119`` (NNDynamicsModel.predict):
+  f64 normalisation, cast to f32 at the TF placeholder feed
+  (``dynamics.py:23-24``), f32 MLP, f64 de-normalisation + residual add.
+* ``NumpyDynamics.mlp``       <- ``dynamics.py:54-71`` (build_network):
+  ``tf.layers.dense`` == ``x @ W + b`` with W stored ``[in, out]``; optional
+  ``tf.contrib.layers.layer_norm`` after each hidden activation
+  (``dynamics.py:68-69``; TF1 defaults: last-axis moments, eps 1e-12,
+  ``x*inv + (beta - mean*inv)`` with ``inv = rsqrt(var+eps)*gamma``).
+* ``cheetah_cost_fn``         <- ``cost_functions.py:9-52``.
+* ``trajectory_cost_fn``      <- ``cost_functions.py:59-63``.
+* ``get_action``              <- ``controllers.py:43-88`` (MPCcontroller).
+
+Parity status: the controller / cost / RNG half is PINNED bit-exactly against
+fixtures produced by running the reference's own ``controllers.py`` +
+``cost_functions.py`` (``tests/golden/gen_golden.py``).  The MLP half lives in
+TensorFlow 1.x inside the reference, which is absent (version unpinned, no
+reference test pins it); it is restated here from ``dynamics.py:54-71`` and is
+therefore pinned only through this restatement (fp32 tolerance).
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+NORM_EPS = 1e-10          # dynamics.py:109-110 (std + 1e-10)
+LN_EPS = 1e-12            # tf.contrib.layers.layer_norm default variance_epsilon (TF1)
+HEADING_PENALTY = 10      # cost_functions.py:12
+COST_DT = 0.01            # cost_functions.py:28
+
+
+# ----------------------------------------------------------------------------
+# cost_functions.py restatement
+# ----------------------------------------------------------------------------
+def cheetah_cost_fn(state, action, next_state):
+    """Restates ``cost_functions.cheetah_cost_fn`` (cost_functions.py:9-52)."""
+    if len(state.shape) > 1:                          # batched branch :10-30
+        scores = np.zeros((state.shape[0],))
+        scores[state[:, 5] >= 0.2] += HEADING_PENALTY  # :16-18 front leg
+        scores[state[:, 6] >= 0] += HEADING_PENALTY    # :20-22 front shin
+        scores[state[:, 7] >= 0] += HEADING_PENALTY    # :24-26 front foot
+        scores -= (next_state[:, 17] - state[:, 17]) / COST_DT   # :28
+        return scores
+    score = 0                                          # scalar branch :32-52
+    if state[5] >= 0.2:
+        score += HEADING_PENALTY
+    if state[6] >= 0:
+        score += HEADING_PENALTY
+    if state[7] >= 0:
+        score += HEADING_PENALTY
+    score -= (next_state[17] - state[17]) / COST_DT
+    return score
+
+
+def trajectory_cost_fn(cost_fn, states, actions, next_states):
+    """Restates ``cost_functions.trajectory_cost_fn`` (cost_functions.py:59-63)."""
+    trajectory_cost = 0
+    for i in range(len(actions)):
+        trajectory_cost += cost_fn(states[i], actions[i], next_states[i])
+    return trajectory_cost
+
+
+# ----------------------------------------------------------------------------
+# dynamics.py restatement
+# ----------------------------------------------------------------------------
+@dataclass
+class MLPWeights:
+    """Dense stack ``26 -> h (x L) -> 20`` in TF layout (kernel ``[in, out]``)."""
+    kernels: List[np.ndarray]
+    biases: List[np.ndarray]
+    activation: str = "tanh"                     # "tanh" | "relu"
+    ln_gamma: Optional[List[np.ndarray]] = None  # one per hidden layer when LN is on
+    ln_beta: Optional[List[np.ndarray]] = None
+
+    @property
+    def n_layers(self) -> int:
+        return len(self.kernels) - 1
+
+    @property
+    def hidden(self) -> int:
+        return int(self.kernels[0].shape[1])
+
+    @property
+    def layer_norm(self) -> bool:
+        return self.ln_gamma is not None
+
+    def digest(self) -> str:
+        h = hashlib.sha256()
+        for a in list(self.kernels) + list(self.biases) + list(self.ln_gamma or []) + list(self.ln_beta or []):
+            h.update(np.ascontiguousarray(a, dtype=np.float32).tobytes())
+        h.update(self.activation.encode())
+        return h.hexdigest()
+
+
+def _act(x: np.ndarray, kind: str) -> np.ndarray:
+    if kind == "tanh":
+        return np.tanh(x)
+    if kind == "relu":
+        return np.maximum(x, np.float32(0))
+    raise ValueError(kind)
+
+
+def layer_norm_tf1(x: np.ndarray, gamma: np.ndarray, beta: np.ndarray) -> np.ndarray:
+    """tf.contrib.layers.layer_norm (TF1) over the last axis, f32.
+
+    nn.moments -> mean, mean(squared_difference(x, mean)); then
+    nn.batch_normalization: inv = rsqrt(var + eps) * gamma;
+    y = x * inv + (beta - mean * inv).
+    """
+    x = x.astype(np.float32, copy=False)
+    mean = np.mean(x, axis=-1, keepdims=True, dtype=np.float32)
+    var = np.mean(np.square(x - mean), axis=-1, keepdims=True, dtype=np.float32)
+    inv = (np.float32(1) / np.sqrt(var + np.float32(LN_EPS))) * gamma.astype(np.float32)
+    return x * inv + (beta.astype(np.float32) - mean * inv)
+
+
+class NumpyDynamics:
+    """Duck-typed stand-in for ``dynamics.NNDynamicsModel`` (dynamics.py:7-119).
+
+    Exposes the same attributes ``MPCcontroller`` and the build's weight
+    adapter read: ``mean_obs, std_obs, mean_action, std_action, mean_deltas,
+    std_deltas`` (dynamics.py:41) and ``predict`` (dynamics.py:106).
+    """
+
+    def __init__(self, weights: MLPWeights, normalization: Sequence[np.ndarray]):
+        (self.mean_obs, self.std_obs, self.mean_action, self.std_action,
+         self.mean_reward, self.std_reward, self.mean_nxt_state, self.std_nxt_state,
+         self.mean_deltas, self.std_deltas) = normalization
+        self.weights = weights
+
+    # dynamics.py:54-71
+    def mlp(self, x32: np.ndarray) -> np.ndarray:
+        w = self.weights
+        out = x32
+        for li in range(w.n_layers):
+            out = out @ w.kernels[li] + w.biases[li]          # tf.layers.dense
+            out = _act(out, w.activation)
+            if w.layer_norm:                                   # FLAGS.LAYER_NORM
+                out = layer_norm_tf1(out, w.ln_gamma[li], w.ln_beta[li])
+        out = out @ w.kernels[-1] + w.biases[-1]               # output_activation=None
+        return out.astype(np.float32, copy=False)
+
+    # dynamics.py:106-119
+    def predict(self, unnormalized_state, unnormalized_action):
+        normalized_state = (unnormalized_state - self.mean_obs) / (self.std_obs + NORM_EPS)
+        normalized_action = (unnormalized_action - self.mean_action) / (self.std_action + NORM_EPS)
+        # feed_dict into tf.float32 placeholders (dynamics.py:23-24) then tf.concat (:26)
+        x = np.concatenate([np.asarray(normalized_state).astype(np.float32),
+                            np.asarray(normalized_action).astype(np.float32)], axis=1)
+        normalized_state_delta = self.mlp(x)
+        unnormalized_state_delta = normalized_state_delta * self.std_deltas + self.mean_deltas
+        return unnormalized_state + unnormalized_state_delta
+
+
+# ----------------------------------------------------------------------------
+# controllers.py restatement (MPCcontroller, controllers.py:26-88)
+# ----------------------------------------------------------------------------
+def rollout(dyn: NumpyDynamics, state, action_paths, cost_fn=cheetah_cost_fn):
+    """Body of ``MPCcontroller.get_action`` after sampling (controllers.py:62-82).
+
+    ``state`` is ``(S,)`` (tiled K times, controllers.py:63) or ``(K, S)``.
+    Returns ``(costs[K] f64, states_paths_all[H+1, K, S] f64)``.
+    """
+    H, K, _ = action_paths.shape
+    state = np.asarray(state)
+    states = np.tile(state, [K, 1]) if state.ndim == 1 else state
+    states_paths_all = [states]
+    for i in range(H):
+        states = dyn.predict(states, action_paths[i, :, :])
+        states_paths_all.append(states)
+    states_paths_all = np.asarray(states_paths_all)
+    costs = trajectory_cost_fn(cost_fn, states_paths_all[:-1], action_paths, states_paths_all[1:])
+    return costs, states_paths_all
+
+
+def get_action(dyn: NumpyDynamics, state, horizon: int, num_simulated_paths: int,
+               low, high, cost_fn=cheetah_cost_fn, rng=None):
+    """``MPCcontroller.get_action`` (controllers.py:57-88), returning extras.
+
+    ``rng`` defaults to the global legacy ``np.random`` stream, exactly like
+    ``controllers.py:53``.  Returns ``(opt_action f64 (A,), argmin, costs)``.
+    """
+    rng = np.random if rng is None else rng
+    action_paths = rng.uniform(low=low, high=high, size=[horizon, num_simulated_paths, len(high)])
+    costs, _ = rollout(dyn, state, action_paths, cost_fn)
+    i = int(np.argmin(costs))
+    return action_paths[:, i, :][0].copy(), i, costs
+
+
+# ----------------------------------------------------------------------------
+# Philox4x32-10 restatement of the engine's device RNG ("perf" action mode)
+# ----------------------------------------------------------------------------
+_PH_M0, _PH_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_PH_W0, _PH_W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Vectorised Philox4x32-10 (Salmon et al., SC'11).  uint32 arrays in/out."""
+    c0, c1, c2, c3 = (np.asarray(c, dtype=np.uint64) & _M32 for c in (c0, c1, c2, c3))
+    k0 = np.uint64(k0) & _M32
+    k1 = np.uint64(k1) & _M32
+    for r in range(10):
+        p0 = _PH_M0 * c0
+        p1 = _PH_M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & _M32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & _M32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & _M32, lo1, (hi0 ^ c3 ^ k1) & _M32, lo0
+        if r != 9:
+            k0 = (k0 + _PH_W0) & _M32
+            k1 = (k1 + _PH_W1) & _M32
+    return [c.astype(np.uint32) for c in (c0, c1, c2, c3)]
+
+
+def device_rng_actions(seed: int, cand_offset: int, K: int, H: int, low, high) -> np.ndarray:
+    """Actions the engine draws on-device in RNG mode, as ``[H, K, A]`` f64.
+
+    Counter = (lo32(g), hi32(g), h, j) for global candidate g, step h, draw j;
+    key = (lo32(seed), hi32(seed)).  Each Philox block gives 4 u32 = two
+    53-bit doubles built like NumPy's legacy ``random_sample``
+    (``((a >> 5) * 67108864 + (b >> 6)) / 2**53``); action = low + (high-low)*u,
+    the form of ``np.random.uniform`` used at controllers.py:53.
+    """
+    low = np.asarray(low, dtype=np.float64)
+    high = np.asarray(high, dtype=np.float64)
+    A = low.shape[0]
+    ndraw = (A + 1) // 2
+    g = (np.arange(K, dtype=np.uint64) + np.uint64(cand_offset))
+    out = np.empty((H, K, A), dtype=np.float64)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for h in range(H):
+        u = np.empty((K, 2 * ndraw), dtype=np.float64)
+        for j in range(ndraw):
+            r = philox4x32_10(g & _M32, g >> np.uint64(32), np.full(K, h, np.uint64),
+                              np.full(K, j, np.uint64), k0, k1)
+            for p in range(2):
+                a = (r[2 * p].astype(np.uint64) >> np.uint64(5)).astype(np.float64)
+                b = (r[2 * p + 1].astype(np.uint64) >> np.uint64(6)).astype(np.float64)
+                u[:, 2 * j + p] = (a * 67108864.0 + b) / 9007199254740992.0
+        out[h] = low + (high - low) * u[:, :A]
+    return out
+
+
+# ----------------------------------------------------------------------------
+# Synthetic inputs
+# ----------------------------------------------------------------------------
+def synthetic_weights(state_dim=20, action_dim=6, hidden=500, n_layers=2,
+                      activation="tanh", layer_norm=False, seed_base=1000) -> MLPWeights:
+    """Glorot-uniform kernels (TF default initializer) from RandomState(1000+layer),
+    biases ~ 0.1 N(0,1); LN gamma ~ 1 + 0.1 N, beta ~ 0.1 N (when enabled)."""
+    dims = [state_dim + action_dim] + [hidden] * n_layers + [state_dim]
+    ks, bs, gs, bts = [], [], [], []
+    for li in range(len(dims) - 1):
+        rs = np.random.RandomState(seed_base + li)
+        lim = np.sqrt(6.0 / (dims[li] + dims[li + 1]))
+        ks.append(rs.uniform(-lim, lim, size=(dims[li], dims[li + 1])).astype(np.float32))
+        bs.append((0.1 * rs.standard_normal(dims[li + 1])).astype(np.float32))
+        if layer_norm and li < n_layers:
+            gs.append((1.0 + 0.1 * rs.standard_normal(dims[li + 1])).astype(np.float32))
+            bts.append((0.1 * rs.standard_normal(dims[li + 1])).astype(np.float32))
+    return MLPWeights(ks, bs, activation, gs if layer_norm else None, bts if layer_norm else None)
+
+
+def synthetic_normalization(state_dim=20, action_dim=6, seed=7):
+    """The 10-tuple of utils.compute_normalization (utils.py:132-158), synthetic."""
+    rs = np.random.RandomState(seed)
+    mean_obs = 0.1 * rs.standard_normal(state_dim)
+    std_obs = np.abs(rs.standard_normal(state_dim)) * 0.5 + 0.2
+    mean_action = np.zeros(action_dim)
+    std_action = np.full(action_dim, 1.0 / np.sqrt(3.0))
+    mean_deltas = 0.005 * rs.standard_normal(state_dim)
+    std_deltas = 0.05 * (np.abs(rs.standard_normal(state_dim)) + 0.2)
+    zeros1 = np.zeros(1)
+    return [mean_obs, std_obs, mean_action, std_action, zeros1, zeros1.copy(),
+            mean_obs.copy(), std_obs.copy(), mean_deltas, std_deltas]
+
+
+def synthetic_state(normalization, seed=11):
+    rs = np.random.RandomState(seed)
+    mean_obs, std_obs = normalization[0], normalization[1]
+    return mean_obs + 0.5 * std_obs * rs.standard_normal(mean_obs.shape[0])
+
+
+def near_threshold_mask(states_paths_all: np.ndarray, delta: float = 1e-4) -> np.ndarray:
+    """Candidates whose cost has a +-10 penalty within ``delta`` of flipping
+    (|s5-0.2|, |s6|, |s7| < delta at any of the H scored states)."""
+    s = states_paths_all[:-1]
+    m = (np.abs(s[..., 5] - 0.2) < delta) | (np.abs(s[..., 6]) < delta) | (np.abs(s[..., 7]) < delta)
+    return m.any(axis=0)
+
+
+def argmin_ref(costs: np.ndarray) -> int:
+    """np.argmin semantics the engine must reproduce (first NaN, else first min)."""
+    return int(np.argmin(costs))

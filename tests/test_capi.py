@@ -1,0 +1,80 @@
+"""C ABI checks that need no GPU: the library loads, exports every symbol the
+header declares, and ctypes struct layouts equal the C compiler's."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "bcmpc.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(bcmpc_[a-z_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(lib, n), n
+    bound = {s[0] for s in _lib.SIGNATURES}
+    assert bound == set(names), "ctypes signature table out of sync with include/bcmpc.h"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert re.search(rf"\bT {n}\b", out), n
+
+
+def test_abi_version_and_error_channel_without_gpu():
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    assert lib.bcmpc_abi_version() == _lib.ABI_VERSION
+    # argument validation runs before any HIP call
+    cfg = _lib.Config(state_dim=20, action_dim=6, hidden=500, n_layers=2, horizon=0, num_paths=16)
+    h = ctypes.c_void_p()
+    assert lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.ERR_ARG
+    assert b"horizon" in lib.bcmpc_last_error()
+    cfg.horizon, cfg.hidden = 5, 4096
+    assert lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.ERR_UNSUPPORTED
+    with pytest.raises(ValueError):
+        _lib.check(_lib.ERR_EMPTY)
+
+
+def test_struct_layouts_match_c():
+    from bc_mpc_amd import _lib
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "bcmpc.h"
+#define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("bcmpc_config %zu\nbcmpc_weights %zu\nbcmpc_result %zu\n",
+         sizeof(bcmpc_config), sizeof(bcmpc_weights), sizeof(bcmpc_result));
+  P(bcmpc_config, num_paths) P(bcmpc_config, precision) P(bcmpc_config, device) P(bcmpc_config, reserved)
+  P(bcmpc_weights, mean_obs) P(bcmpc_weights, std_deltas)
+  P(bcmpc_result, best_cost) P(bcmpc_result, first_action)
+  return 0; }
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        exe = os.path.join(d, "t")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
+        lines = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = dict(l.rsplit(" ", 1) for l in lines if l)
+    assert int(got["bcmpc_config"]) == ctypes.sizeof(_lib.Config)
+    assert int(got["bcmpc_weights"]) == ctypes.sizeof(_lib.Weights)
+    assert int(got["bcmpc_result"]) == ctypes.sizeof(_lib.Result)
+    for key, v in got.items():
+        if "." in key:
+            t, f = key.split(".")
+            cls = {"bcmpc_config": _lib.Config, "bcmpc_weights": _lib.Weights, "bcmpc_result": _lib.Result}[t]
+            assert getattr(cls, f).offset == int(v), key

@@ -1,0 +1,91 @@
+"""Host-side logic that needs no GPU: sharding, min-loc selection, cost
+recognition, weight extraction."""
+import numpy as np
+import pytest
+
+from bc_mpc_amd import cost_functions as cf
+from bc_mpc_amd import distributed as dd
+from bc_mpc_amd import weights as ww
+
+
+@pytest.mark.parametrize("K,world", [(1, 1), (7, 2), (65536, 8), (3, 8), (262144, 8), (1000, 3)])
+def test_shard_ranges_partition_k(K, world):
+    rngs = [dd.shard_range(K, r, world) for r in range(world)]
+    assert rngs[0][0] == 0 and rngs[-1][1] == K
+    for (a, b), (c, d) in zip(rngs, rngs[1:]):
+        assert b == c and b >= a
+    sizes = [b - a for a, b in rngs]
+    assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_sharded_minloc_equals_np_argmin(seed):
+    rs = np.random.RandomState(seed)
+    K = int(rs.randint(1, 200))
+    costs = np.round(rs.standard_normal(K), 1)          # many exact ties
+    if seed % 3 == 0:
+        costs[rs.randint(0, K, size=2)] = np.nan
+    if seed % 5 == 0:
+        costs[:] = 7.0
+    world = int(rs.randint(1, 9))
+    recs = []
+    for r in range(world):
+        lo, hi = dd.shard_range(K, r, world)
+        if hi == lo:
+            recs.append([0.0, np.inf, -1.0])
+            continue
+        i = int(np.argmin(costs[lo:hi]))
+        recs.append([1.0, costs[lo + i], float(lo + i)])
+    best = dd.select(np.asarray(recs))
+    assert int(best[2]) == int(np.argmin(costs))
+
+
+def test_cheetah_cost_recognition():
+    assert cf.is_cheetah_cost(cf.cheetah_cost_fn)
+
+    def cheetah_cost_fn(state, action, next_state):     # same name, different maths
+        return cf.cheetah_cost_fn(state, action, next_state) + 1e-12
+    assert not cf.is_cheetah_cost(cheetah_cost_fn)
+
+    def my_cost(state, action, next_state):
+        return cf.cheetah_cost_fn(state, action, next_state)
+    assert not cf.is_cheetah_cost(my_cost)               # unknown name -> trajectory mode
+    assert not cf.is_cheetah_cost(None)
+
+
+def test_cheetah_cost_recognises_a_faithful_copy():
+    # a verbatim-semantics implementation under the reference's function name
+    def cheetah_cost_fn(state, action, next_state):
+        scores = np.zeros((state.shape[0],))
+        scores[state[:, 5] >= 0.2] += 10
+        scores[state[:, 6] >= 0] += 10
+        scores[state[:, 7] >= 0] += 10
+        scores -= (next_state[:, 17] - state[:, 17]) / 0.01
+        return scores
+    assert cf.is_cheetah_cost(cheetah_cost_fn)
+
+
+def test_weight_extraction_from_numpy_standin():
+    from oracle import mpc_oracle as orc
+    w = orc.synthetic_weights(20, 6, 64, 2, "relu", True)
+    dyn = orc.NumpyDynamics(w, orc.synthetic_normalization())
+    spec, norm, v1 = ww.extract(dyn)
+    assert spec.activation == "relu" and spec.layer_norm and spec.n_layers == 2 and spec.hidden == 64
+    assert len(norm) == 10 and norm[0].dtype == np.float64
+    _, _, v2 = ww.extract(dyn)
+    assert v1 == v2
+    dyn.weights.kernels[1] = dyn.weights.kernels[1] * 2
+    _, _, v3 = ww.extract(dyn)
+    assert v3 != v1
+
+
+def test_tf_fit_hook_bumps_version():
+    class Fake:
+        def fit(self, data):
+            return 1.0, 0
+    f = Fake()
+    ww._install_fit_hook(f)
+    v0 = f._bcmpc_version
+    f.fit(None)
+    f.fit(None)
+    assert f._bcmpc_version == v0 + 2

@@ -1,0 +1,70 @@
+"""The CPU oracle against the fixtures produced by the reference's own code."""
+import hashlib
+
+import numpy as np
+
+from oracle import mpc_oracle as orc
+
+
+def test_oracle_reproduces_reference_costs_bitwise(golden):
+    costs, states = orc.rollout(golden.dyn(), golden.state, golden.actions())
+    assert np.array_equal(costs, golden.costs, equal_nan=True)
+    assert int(np.argmin(costs)) == golden.argmin
+    if "states" in golden.z.files:
+        assert np.array_equal(states, golden.z["states"], equal_nan=True)
+
+
+def test_regenerated_actions_match_reference_stream(golden):
+    ap = golden.actions()
+    assert hashlib.sha256(np.ascontiguousarray(ap).tobytes()).digest() == golden.z["action_digest"].tobytes()
+
+
+def test_oracle_get_action_matches_reference_and_rng_side_effect(golden):
+    if golden.meta.get("inject"):
+        return  # injected cases replace the sampled actions; covered by the rollout test
+    np.random.seed(golden.meta["seed"])
+    a, i, costs = orc.get_action(golden.dyn(), golden.state, golden.H, golden.K, golden.low, golden.high)
+    assert i == golden.argmin
+    assert np.array_equal(a, golden.opt_action)
+    assert a.dtype == np.float64 and a.shape == (golden.A,)
+    # exactly H*K*A doubles consumed from the global stream (controllers.py:53)
+    assert np.random.random() == float(golden.z["next_draw"])
+
+
+def test_philox_known_answer_vectors():
+    # Random123 kat_vectors, philox4x32_10
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for c, k, want in kat:
+        got = orc.philox4x32_10(*[np.array([v], dtype=np.uint64) for v in c], *k)
+        assert tuple(int(x[0]) for x in got) == want
+
+
+def test_device_rng_actions_in_range_and_shard_invariant():
+    a = orc.device_rng_actions(1234, 0, 64, 3, -np.ones(6), np.ones(6))
+    b = orc.device_rng_actions(1234, 32, 32, 3, -np.ones(6), np.ones(6))
+    assert np.array_equal(a[:, 32:], b)
+    assert a.min() >= -1 and a.max() < 1
+    assert abs(a.mean()) < 0.1
+
+
+def test_layer_norm_matches_float64_definition():
+    rs = np.random.RandomState(0)
+    x = rs.standard_normal((8, 96)).astype(np.float32)
+    g = rs.standard_normal(96).astype(np.float32)
+    b = rs.standard_normal(96).astype(np.float32)
+    y = orc.layer_norm_tf1(x, g, b)
+    x64 = x.astype(np.float64)
+    ref = (x64 - x64.mean(1, keepdims=True)) / np.sqrt(x64.var(1, keepdims=True) + 1e-12) * g + b
+    assert np.abs(y - ref).max() < 1e-5
+
+
+def test_cost_scalar_and_batched_branches_agree():
+    rs = np.random.RandomState(3)
+    s = rs.standard_normal((16, 20)) * 0.3
+    ns = s + rs.standard_normal((16, 20)) * 0.02
+    batched = orc.cheetah_cost_fn(s, None, ns)
+    scalar = np.array([orc.cheetah_cost_fn(s[i], None, ns[i]) for i in range(16)])
+    assert np.array_equal(batched, scalar)
