@@ -1,7 +1,7 @@
 # Builds libbcmpc.so (HIP for gfx950) in-tree.  `make -j` is safe; no cmake.
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-function
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
 OBJ      := build/rollout.o build/capi.o

@@ -19,7 +19,7 @@ try:  # single HIP runtime per process (see module docstring)
 except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbcmpc.so")
+LIB_PATH = os.environ.get("BCMPC_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbcmpc.so")
 
 MAX_LAYERS = 8
 MAX_STATE = 32

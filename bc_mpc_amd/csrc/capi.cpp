@@ -108,7 +108,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     e->T = e->HP / 16;
     // small K: one wave per block spreads candidates over more CUs
     const int64_t waves = (c.num_paths + 15) / 16;
-    e->wpb = waves >= 4 * 256 ? 4 : 1;
+    e->wpb = std::min(waves >= 4 * 256 ? 4 : 1, max_waves_per_block(e->HP, c.n_layers));
+    if (e->wpb < 1) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "layer stack does not fit in LDS"); }
     const int L = c.n_layers, T = e->T;
     size_t off = 0;
     e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;                   // [S+A -> h]
@@ -226,6 +227,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     if (d_result && c.cost != BCMPC_COST_CHEETAH) return fail(BCMPC_ERR_ARG, "argmin needs the fused cost");
     RolloutArgs a{};
     for (int l = 0; l <= c.n_layers; ++l) {
+        const size_t end = l < c.n_layers ? e->w_off[l + 1] : e->w_floats;
+        a.wbytes[l] = (int32_t)((end - e->w_off[l]) * sizeof(float));
         a.w[l] = reinterpret_cast<const float __attribute__((ext_vector_type(4)))*>(e->d_w + e->w_off[l]);
         a.b[l] = e->d_b + e->b_off[l];
     }

@@ -15,6 +15,7 @@ constexpr int kConstCols = 32;
 
 struct RolloutArgs {
     const float __attribute__((ext_vector_type(4)))* w[BCMPC_MAX_LAYERS + 1];  // packed kernels
+    int32_t wbytes[BCMPC_MAX_LAYERS + 1];    // packed bytes per layer (buffer num_records)
     const float* b[BCMPC_MAX_LAYERS + 1];    // padded biases
     const float* lng[BCMPC_MAX_LAYERS];      // padded LN gamma (0 on pad lanes)
     const float* lnb[BCMPC_MAX_LAYERS];      // padded LN beta
@@ -41,6 +42,7 @@ struct ArgminArgs {
     int32_t A;
 };
 
+int max_waves_per_block(int hidden_padded, int n_layers);
 hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 

@@ -68,46 +68,115 @@ __device__ __forceinline__ double rng_action(uint64_t seed, uint64_t g, int h, i
     return __dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u));   // low + (high-low)*u, no FMA
 }
 
-// -------------------------------------------------------------- MLP tiles ---
-// acc[j] = sum_u sum_r W[t0+j][u][r] * x[u][r] for a block of TB output tiles.
-// wblk points at the packed block [u][j][lane] (f4 per lane).
-template <int TIN, int TB>
-__device__ __forceinline__ void mm_tiles(const f4* __restrict__ wblk, const float (&x)[TIN][4],
-                                         f4 (&acc)[TB], int lane) {
-#pragma unroll
-    for (int j = 0; j < TB; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < TIN; ++u) {
-        f4 w[TB];
-#pragma unroll
-        for (int j = 0; j < TB; ++j) w[j] = wblk[(u * TB + j) * 64 + lane];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-#pragma unroll
-            for (int j = 0; j < TB; ++j)
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j][r], x[u][r], acc[j], 0, 0, 0);
-        }
-    }
+// ------------------------------------------------------------ activation ---
+// Branch-free tanh: odd Taylor polynomial below |x| = 0.4, else
+// 1 - 2/(1 + e^{2|x|}) with v_exp_f32 / v_rcp_f32 (<= ~4 ulp vs float64 tanh,
+// np.tanh itself is ~1.4 ulp; see DESIGN.md "numerics").
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float ax = fabsf(x);
+    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);   // exp(2|x|)
+    const float r = __builtin_amdgcn_rcpf(1.0f + e);
+    const float big = __builtin_copysignf(fmaf(-2.0f, r, 1.0f), x);
+    const float x2 = x * x;
+    float p = -1382.0f / 155925.0f;
+    p = fmaf(p, x2, 62.0f / 2835.0f);
+    p = fmaf(p, x2, -17.0f / 315.0f);
+    p = fmaf(p, x2, 2.0f / 15.0f);
+    p = fmaf(p, x2, -1.0f / 3.0f);
+    const float small = fmaf(x * x2, p, x);
+    return ax < 0.4f ? small : big;
 }
 
-__device__ __forceinline__ float activate(float v, int act) {
-    return act == BCMPC_ACT_RELU ? fmaxf(v, 0.f) : tanhf(v);
+template <int ACT>
+__device__ __forceinline__ float activate(float v) {
+    if constexpr (ACT == BCMPC_ACT_RELU) return fmaxf(v, 0.f);
+    else return tanh_fast(v);
 }
 
-// bias + activation of a finished 4-tile block, parked in the wave's LDS slab.
-template <int TB>
-__device__ __forceinline__ void store_block(const f4 (&acc)[TB], int t0, const float* __restrict__ bias,
-                                            int act, f4* y, int lane) {
+// bias + activation of one output tile (tf.layers.dense: BiasAdd then act)
+template <int ACT>
+__device__ __forceinline__ f4 bias_act(const f4 acc, const float* __restrict__ bias, int t, int q) {
+    const f4 bv = *reinterpret_cast<const f4*>(bias + 16 * t + 4 * q);
+    f4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = activate<ACT>(acc[r] + bv[r]);
+    return v;
+}
+
+// ---------------------------------------------------------- dense layers ---
+// Raw buffer load of one 16-B weight fragment: voffset = lane*16 (VGPR),
+// soffset = fragment position (SGPR).  Reads past the layer's num_records
+// return 0 (hardware range check), so the prefetch may run off the end.
+__device__ __forceinline__ f4 wload(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t layer_rsrc(const void* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+
+// Streaming dense layer [TIN tiles in -> TOUT = NB*TB tiles out].  The packed
+// weights [tb][u][j][lane] are ONE linear stream of 1-KiB fragments: u-step
+// (tb, u) starts at byte (tb*TIN + u) * TB KiB.  A D-deep register ring holds
+// the next D u-steps; each refill simply advances the stream position.  With
+// EPI, block tb-1's bias+activation runs inside block tb's MFMA stream (VALU
+// beside MFMA) and lands in the wave's LDS slab y (block -1 writes to a
+// scratch tile past the end, branch-free).  Biases come from LDS (lgkmcnt),
+// never through the vmcnt queue the weight ring lives on.
+template <int TIN, int TOUT, int TB, int D, int ACT, bool EPI>
+__device__ __forceinline__ void layer_stream(__amdgpu_buffer_rsrc_t rs, const float (&x)[TIN][4],
+                                             const float* bias, f4* y, f4 (&out)[TB], int lane) {
+    constexpr int NB = TOUT / TB;
+    static_assert(NB * TB == TOUT, "TOUT must be a multiple of TB");
+    // the ring slot of u-step u is u % D in EVERY block, so blocks must span whole ring turns
+    static_assert(NB == 1 || TIN % D == 0, "TIN must be a multiple of the prefetch depth D");
+    constexpr int STEPB = TB * 1024;              // bytes per u-step
     const int q = lane >> 4;
+    const int voff = lane * 16;
+    f4 ring[D][TB];
 #pragma unroll
-    for (int j = 0; j < TB; ++j) {
-        const int t = t0 + j;
-        const f4 bv = *reinterpret_cast<const f4*>(bias + 16 * t + 4 * q);
-        f4 v;
+    for (int d = 0; d < D; ++d)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = activate(acc[j][r] + bv[r], act);   // BiasAdd then act
-        y[t * 64 + lane] = v;
+        for (int j = 0; j < TB; ++j) ring[d][j] = wload(rs, voff, d * STEPB + j * 1024);
+    f4 prev[TB];
+#pragma unroll
+    for (int j = 0; j < TB; ++j) prev[j] = (f4){0.f, 0.f, 0.f, 0.f};
+    for (int tb = 0; tb < NB; ++tb) {
+        const int base = tb * TIN * STEPB;
+        const int dst = (tb == 0) ? TOUT : (tb - 1) * TB;         // scratch tile for the pseudo-block -1
+        f4 acc[TB];
+#pragma unroll
+        for (int j = 0; j < TB; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < TIN; ++u) {
+            const int slot = u % D;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < TB; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[slot][j][r], x[u][r], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TB; ++j) ring[slot][j] = wload(rs, voff, base + (u + D) * STEPB + j * 1024);
+            if constexpr (EPI) {
+                // spread the previous block's epilogue over this block's u-steps
+                constexpr int GAP = TIN >= TB ? TIN / TB : 1;
+#pragma unroll
+                for (int e = 0; e < TB; ++e)
+                    if ((TIN >= TB) ? (u == e * GAP + GAP / 2) : (u == TIN - 1)) {
+                        y[(dst + e) * 64 + lane] = bias_act<ACT>(prev[e], bias, (dst + e) & (TOUT - 1), q);
+                    }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < TB; ++j) prev[j] = acc[j];
     }
+    if constexpr (EPI) {
+        const int dst = (NB - 1) * TB;
+#pragma unroll
+        for (int e = 0; e < TB; ++e) y[(dst + e) * 64 + lane] = bias_act<ACT>(prev[e], bias, dst + e, q);
+    }
+#pragma unroll
+    for (int j = 0; j < TB; ++j) out[j] = prev[j];
 }
 
 // tf.contrib.layers.layer_norm over the true hidden width (dynamics.py:68-69).
@@ -156,13 +225,22 @@ __device__ __forceinline__ void reload(float (&x)[T][4], const f4* y, int lane) 
     }
 }
 
+// LDS carve-up of one block: [consts 2 KiB][biases L*HP + 32 floats][per-wave slabs]
+__host__ __device__ constexpr int param_bytes(int L, int HP) {
+    return ((kConstRows * kConstCols * 8 + (L * HP + 32) * 4) + 15) & ~15;
+}
+
 // ------------------------------------------------------------ the kernel ---
-template <int HP>
+#ifndef BCMPC_D
+#define BCMPC_D 2
+#endif
+template <int HP, int ACT, bool LN>
 __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
     constexpr int T = HP / 16;     // hidden tiles
-    constexpr int TB = 4;          // output tiles per block (packing granule)
+    constexpr int TB = 4;          // output tiles per streamed block (packing granule)
+    constexpr int D = BCMPC_D;     // weight prefetch depth, u-steps
     static_assert(T % TB == 0, "hidden tiles must be a multiple of 4");
-    extern __shared__ __attribute__((aligned(16))) f4 lds_y[];
+    extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -170,10 +248,17 @@ __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
     const int m = lane & 15;
     const int64_t cand = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 16 + m;
     const bool valid = cand < a.K;
-    f4* y = lds_y + (size_t)wave * T * 64;
+    const int S = a.S, A = a.A, L = a.L;
 
-    const double* __restrict__ C = a.consts;   // [8][32]
-    const int S = a.S, A = a.A;
+    // ---- stage per-block parameters in LDS: consts (f64) + all biases ----
+    double* C = reinterpret_cast<double*>(lds);                          // [8][32]
+    float* Bl = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kConstRows * kConstCols * 8);
+    for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
+    for (int l = 0; l < L; ++l)
+        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i];
+    for (int i = threadIdx.x; i < 32; i += blockDim.x) Bl[L * HP + i] = a.b[L][i];
+    __syncthreads();
+    f4* y = reinterpret_cast<f4*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP)) + (size_t)wave * (T + TB) * 64;
 
     // state of candidate `cand`, dims d = 16v + 4q + r
     double s[2][4];
@@ -196,8 +281,36 @@ __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
     double cost = 0.0;   // trajectory_cost = 0 (cost_functions.py:60)
     const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
 
+    // actions of this lane's input rows i = 16v + 4q + r in [S, S+A): fetched
+    // one step ahead so the step-start loads never stall the weight stream
+    auto fetch_action = [&](int h, int i) -> double {
+        const int j = i - S;
+        if (!valid || i < S || j >= A) return 0.0;
+        return a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
+                         : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
+    };
+    double act_next[2][4];
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act_next[v][r] = fetch_action(0, 16 * v + 4 * q + r);
+
+    const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
+    const __amdgpu_buffer_rsrc_t rsL = layer_rsrc(a.w[L], a.wbytes[L]);
+
     for (int h = 0; h < a.H; ++h) {
         // ---- predict: normalise (dynamics.py:109-110), cast to f32 (TF feed) ----
+        double act_cur[2][4];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) act_cur[v][r] = act_next[v][r];
+        if (h + 1 < a.H) {
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) act_next[v][r] = fetch_action(h + 1, 16 * v + 4 * q + r);
+        }
         float x0[2][4];
 #pragma unroll
         for (int v = 0; v < 2; ++v)
@@ -209,12 +322,7 @@ __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
                     xv = (float)__ddiv_rn(__dsub_rn(s[v][r], C[0 * 32 + i]), C[1 * 32 + i]);
                 } else if (i < S + A) {
                     const int j = i - S;
-                    double av = 0.0;
-                    if (valid) {
-                        av = a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
-                                       : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
-                    }
-                    xv = (float)__ddiv_rn(__dsub_rn(av, C[2 * 32 + j]), C[3 * 32 + j]);
+                    xv = (float)__ddiv_rn(__dsub_rn(act_cur[v][r], C[2 * 32 + j]), C[3 * 32 + j]);
                 }
                 x0[v][r] = xv;
             }
@@ -222,35 +330,27 @@ __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
         // ---- layer 0: [S+A -> h] ----
         float x[T][4];
         {
-            const f4* W = a.w[0];
-            for (int tb = 0; tb < T / TB; ++tb) {
-                f4 acc[TB];
-                mm_tiles<2, TB>(W + (size_t)tb * 2 * TB * 64, x0, acc, lane);
-                store_block<TB>(acc, tb * TB, a.b[0], a.act, y, lane);
-            }
+            f4 unused[TB];
+            layer_stream<2, T, TB, 2, ACT, true>(rs0, x0, Bl, y, unused, lane);
             reload<T>(x, y, lane);
-            if (a.ln) layer_norm<T>(x, a.lng[0], a.lnb[0], a.hidden, lane);
+            if constexpr (LN) layer_norm<T>(x, a.lng[0], a.lnb[0], a.hidden, lane);
         }
-        // ---- hidden layers 1..L-1: [h -> h] ----
-        for (int l = 1; l < a.L; ++l) {
-            const f4* W = a.w[l];
-            for (int tb = 0; tb < T / TB; ++tb) {
-                f4 acc[TB];
-                mm_tiles<T, TB>(W + (size_t)tb * T * TB * 64, x, acc, lane);
-                store_block<TB>(acc, tb * TB, a.b[l], a.act, y, lane);
-            }
+        // ---- hidden layers 1..L-1: [h -> h], streamed, parked in LDS ----
+        for (int l = 1; l < L; ++l) {
+            f4 unused[TB];
+            layer_stream<T, T, TB, D, ACT, true>(layer_rsrc(a.w[l], a.wbytes[l]), x, Bl + l * HP, y, unused, lane);
             reload<T>(x, y, lane);
-            if (a.ln) layer_norm<T>(x, a.lng[l], a.lnb[l], a.hidden, lane);
+            if constexpr (LN) layer_norm<T>(x, a.lng[l], a.lnb[l], a.hidden, lane);
         }
         // ---- output layer: [h -> S], no activation (dynamics.py:70) ----
         f4 o[2];
-        mm_tiles<T, 2>(a.w[a.L], x, o, lane);
+        layer_stream<T, 2, 2, D, ACT, false>(rsL, x, Bl, y, o, lane);
 
         // ---- de-normalise + residual (dynamics.py:113,116), f64, no FMA ----
         double sn[2][4];
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
-            const f4 bv = *reinterpret_cast<const f4*>(a.b[a.L] + 16 * v + 4 * q);
+            const f4 bv = *reinterpret_cast<const f4*>(Bl + L * HP + 16 * v + 4 * q);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int d = 16 * v + 4 * q + r;
@@ -344,28 +444,45 @@ __global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
-template <int HP>
+static size_t slab_bytes(int HP) { return (size_t)(HP / 16 + 4) * 64 * sizeof(f4); }
+
+int max_waves_per_block(int hidden_padded, int n_layers) {
+    const size_t budget = 160 * 1024;
+    for (int w : {4, 2, 1})
+        if ((size_t)param_bytes(n_layers, hidden_padded) + w * slab_bytes(hidden_padded) <= budget) return w;
+    return 0;
+}
+
+template <int HP, int ACT, bool LN>
 static hipError_t launch_hp(const RolloutArgs& a, int waves_per_block, hipStream_t st) {
-    const size_t lds = (size_t)waves_per_block * (HP / 16) * 64 * sizeof(f4);
+    const size_t lds = (size_t)param_bytes(a.L, HP) + waves_per_block * slab_bytes(HP);
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)rollout_fp32<HP>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * (HP / 16) * 64 * 16));
+        hipError_t e = hipFuncSetAttribute((const void*)rollout_fp32<HP, ACT, LN>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int64_t waves = (a.K + 15) / 16;
     const int64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
-    hipLaunchKernelGGL(rollout_fp32<HP>, dim3((unsigned)blocks), dim3(64 * waves_per_block), lds, st, a);
+    hipLaunchKernelGGL((rollout_fp32<HP, ACT, LN>), dim3((unsigned)blocks), dim3(64 * waves_per_block), lds, st, a);
     return hipGetLastError();
+}
+
+template <int HP>
+static hipError_t launch_act(const RolloutArgs& a, int wpb, hipStream_t st) {
+    if (a.ln) return a.act == BCMPC_ACT_RELU ? launch_hp<HP, BCMPC_ACT_RELU, true>(a, wpb, st)
+                                             : launch_hp<HP, BCMPC_ACT_TANH, true>(a, wpb, st);
+    return a.act == BCMPC_ACT_RELU ? launch_hp<HP, BCMPC_ACT_RELU, false>(a, wpb, st)
+                                   : launch_hp<HP, BCMPC_ACT_TANH, false>(a, wpb, st);
 }
 
 hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st) {
     switch (hidden_padded) {
-        case 64: return launch_hp<64>(a, waves_per_block, st);
-        case 128: return launch_hp<128>(a, waves_per_block, st);
-        case 256: return launch_hp<256>(a, waves_per_block, st);
-        case 512: return launch_hp<512>(a, waves_per_block, st);
+        case 64: return launch_act<64>(a, waves_per_block, st);
+        case 128: return launch_act<128>(a, waves_per_block, st);
+        case 256: return launch_act<256>(a, waves_per_block, st);
+        case 512: return launch_act<512>(a, waves_per_block, st);
         default: return hipErrorInvalidValue;
     }
 }

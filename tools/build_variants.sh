@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build A/B variants of libbcmpc.so into build/variants/ (selected at run time via BCMPC_LIB).
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p build/variants
+H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize"
+$H -x hip -c bc_mpc_amd/csrc/capi.cpp -o build/variants/capi.o
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  $H $flags -c bc_mpc_amd/csrc/rollout.hip -o build/variants/rollout_$name.o &
+done
+wait
+for spec in "$@"; do
+  name=${spec%%:*}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so build/variants/rollout_$name.o build/variants/capi.o
+done
+ls build/variants/*.so
