@@ -4,12 +4,16 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
-OBJ      := build/rollout.o build/capi.o
-HDR      := include/bcmpc.h $(SRC)/kernels.h
+OBJ      := build/rollout.o build/rollout_grp.o build/capi.o
+HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h
 
 all: $(LIB)
 
 build/rollout.o: $(SRC)/rollout.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build/rollout_grp.o: $(SRC)/rollout_grp.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -21,12 +25,14 @@ $(LIB): $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
 
 # resource usage report (VGPR/SGPR/LDS/occupancy) for the rollout kernels
-resources: $(SRC)/rollout.hip $(HDR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Spill|Occupancy|LDS" 
+resources: $(SRC)/rollout.hip $(SRC)/rollout_grp.hip $(HDR)
+	$(HIPCC) $(HIPFLAGS) -c $(SRC)/rollout.hip -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Spill|Occupancy|LDS"
+	$(HIPCC) $(HIPFLAGS) -c $(SRC)/rollout_grp.hip -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Spill|Occupancy|LDS" 
 
-asm: $(SRC)/rollout.hip $(HDR)
+asm: $(SRC)/rollout.hip $(SRC)/rollout_grp.hip $(HDR)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -S --cuda-device-only $< -o build/rollout.s
+	$(HIPCC) $(HIPFLAGS) -S --cuda-device-only $(SRC)/rollout.hip -o build/rollout.s
+	$(HIPCC) $(HIPFLAGS) -S --cuda-device-only $(SRC)/rollout_grp.hip -o build/rollout_grp.s
 
 clean:
 	rm -rf build $(LIB)

@@ -30,6 +30,7 @@ OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
 ACT_TANH, ACT_RELU = 0, 1
 COST_CHEETAH, COST_NONE = 0, 1
 PREC_FP32 = 0
+KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3}
 
 
 class Config(ctypes.Structure):
@@ -45,7 +46,8 @@ class Config(ctypes.Structure):
         ("num_paths", ctypes.c_int64),
         ("precision", ctypes.c_int32),
         ("device", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 8),
+        ("kernel", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 7),
     ]
 
 
@@ -95,7 +97,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ("bcmpc_engine_info", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
-      ctypes.POINTER(ctypes.c_int32)]),
+      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
 ]
 
 _lib = None

@@ -58,6 +58,8 @@ void pack_layer(const float* W, int in, int out, int Tin, int Tout, int TB, floa
 struct bcmpc_engine {
     bcmpc_config cfg{};
     int HP = 0, T = 0, wpb = 4;
+    int kernel = BCMPC_KERNEL_SOLO;    // resolved kernel layout
+    int pack_tb = 4;                   // output tiles per packed block of layers 0..L-1
     hipStream_t stream = nullptr;
     // device buffers
     float* d_w = nullptr;   size_t w_floats = 0;
@@ -109,7 +111,17 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     // small K: one wave per block spreads candidates over more CUs
     const int64_t waves = (c.num_paths + 15) / 16;
     e->wpb = std::min(waves >= 4 * 256 ? 4 : 1, max_waves_per_block(e->HP, c.n_layers));
-    if (e->wpb < 1) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "layer stack does not fit in LDS"); }
+    int kern = c.kernel == BCMPC_KERNEL_AUTO ? BCMPC_KERNEL_GROUP4 : c.kernel;
+    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_GROUP4) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
+    const int nw = kern == BCMPC_KERNEL_GROUP4 ? 4 : 2;
+    if (kern != BCMPC_KERNEL_SOLO &&
+        (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw) > 160 * 1024)) {
+        if (c.kernel != BCMPC_KERNEL_AUTO) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group kernel does not fit this shape"); }
+        kern = BCMPC_KERNEL_SOLO;
+    }
+    if (kern == BCMPC_KERNEL_SOLO && e->wpb < 1) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "layer stack does not fit in LDS"); }
+    e->kernel = kern;
+    e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->T / nw;
     const int L = c.n_layers, T = e->T;
     size_t off = 0;
     e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;                   // [S+A -> h]
@@ -171,8 +183,9 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         if (!w->kernels[l] || !w->biases[l]) return fail(BCMPC_ERR_ARG, "null kernel/bias pointer");
     HIP_TRY(hipSetDevice(c.device));
     std::vector<float> hw(e->w_floats, 0.f);
-    pack_layer(w->kernels[0], S + A, h, 2, T, 4, hw.data() + e->w_off[0]);
-    for (int l = 1; l < L; ++l) pack_layer(w->kernels[l], h, h, T, T, 4, hw.data() + e->w_off[l]);
+    const int tb = e->pack_tb;
+    pack_layer(w->kernels[0], S + A, h, 2, T, tb, hw.data() + e->w_off[0]);
+    for (int l = 1; l < L; ++l) pack_layer(w->kernels[l], h, h, T, T, tb, hw.data() + e->w_off[l]);
     pack_layer(w->kernels[L], h, S, T, 2, 2, hw.data() + e->w_off[L]);
     std::vector<float> hb((size_t)L * HP + 32, 0.f);
     for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
@@ -243,7 +256,11 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     a.H = c.horizon; a.S = c.state_dim; a.A = c.action_dim; a.L = c.n_layers;
     a.hidden = c.hidden; a.act = c.activation; a.ln = c.layer_norm; a.cost = c.cost;
     HIP_TRY(hipEventRecord(e->ev[0], st));
-    HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
+    if (e->kernel == BCMPC_KERNEL_SOLO) {
+        HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
+    } else {
+        HIP_TRY(launch_rollout_grp(a, e->HP, e->kernel == BCMPC_KERNEL_GROUP4 ? 4 : 2, st));
+    }
     HIP_TRY(hipEventRecord(e->ev[1], st));
     if (d_result) {
         ArgminArgs m{};
@@ -308,11 +325,13 @@ int bcmpc_last_kernel_ms(bcmpc_engine* e, float* rollout_ms, float* argmin_ms) {
 }
 
 int bcmpc_engine_info(const bcmpc_engine* e, int32_t* hidden_padded, int64_t* packed_weight_bytes,
-                      int32_t* waves_per_block) {
+                      int32_t* waves_per_block, int32_t* kernel) {
     if (!e) return fail(BCMPC_ERR_ARG, "null argument");
     if (hidden_padded) *hidden_padded = e->HP;
     if (packed_weight_bytes) *packed_weight_bytes = (int64_t)(e->w_floats * sizeof(float));
-    if (waves_per_block) *waves_per_block = e->wpb;
+    if (waves_per_block) *waves_per_block = e->kernel == BCMPC_KERNEL_SOLO ? e->wpb
+                                            : (e->kernel == BCMPC_KERNEL_GROUP4 ? 4 : 2);
+    if (kernel) *kernel = e->kernel;
     return BCMPC_OK;
 }
 

@@ -44,6 +44,8 @@ struct ArgminArgs {
 
 int max_waves_per_block(int hidden_padded, int n_layers);
 hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st);
+size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw);
+hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 
 }  // namespace bcmpc

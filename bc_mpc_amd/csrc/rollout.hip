@@ -35,85 +35,9 @@
 
 #include "../../include/bcmpc.h"
 #include "kernels.h"
+#include "device_common.h"
 
 namespace bcmpc {
-
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-// ---------------------------------------------------------------- Philox ---
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]);
-        const uint32_t lo0 = 0xD2511F53u * c[0];
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]);
-        const uint32_t lo1 = 0xCD9E8D57u * c[2];
-        const uint32_t n0 = hi1 ^ c[1] ^ k0;
-        const uint32_t n2 = hi0 ^ c[3] ^ k1;
-        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-
-// Uniform action j of global candidate g at step h (oracle.device_rng_actions).
-__device__ __forceinline__ double rng_action(uint64_t seed, uint64_t g, int h, int j,
-                                             double lo, double hi) {
-    uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)h, (uint32_t)(j >> 1)};
-    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const uint32_t a = (j & 1) ? c[2] : c[0];
-    const uint32_t b = (j & 1) ? c[3] : c[1];
-    // NumPy legacy random_sample: ((a >> 5) * 2^26 + (b >> 6)) / 2^53 (exact in f64)
-    const double u = ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
-    return __dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u));   // low + (high-low)*u, no FMA
-}
-
-// ------------------------------------------------------------ activation ---
-// Branch-free tanh: odd Taylor polynomial below |x| = 0.4, else
-// 1 - 2/(1 + e^{2|x|}) with v_exp_f32 / v_rcp_f32 (<= ~4 ulp vs float64 tanh,
-// np.tanh itself is ~1.4 ulp; see DESIGN.md "numerics").
-__device__ __forceinline__ float tanh_fast(float x) {
-    const float ax = fabsf(x);
-    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);   // exp(2|x|)
-    const float r = __builtin_amdgcn_rcpf(1.0f + e);
-    const float big = __builtin_copysignf(fmaf(-2.0f, r, 1.0f), x);
-    const float x2 = x * x;
-    float p = -1382.0f / 155925.0f;
-    p = fmaf(p, x2, 62.0f / 2835.0f);
-    p = fmaf(p, x2, -17.0f / 315.0f);
-    p = fmaf(p, x2, 2.0f / 15.0f);
-    p = fmaf(p, x2, -1.0f / 3.0f);
-    const float small = fmaf(x * x2, p, x);
-    return ax < 0.4f ? small : big;
-}
-
-template <int ACT>
-__device__ __forceinline__ float activate(float v) {
-    if constexpr (ACT == BCMPC_ACT_RELU) return fmaxf(v, 0.f);
-    else return tanh_fast(v);
-}
-
-// bias + activation of one output tile (tf.layers.dense: BiasAdd then act)
-template <int ACT>
-__device__ __forceinline__ f4 bias_act(const f4 acc, const float* __restrict__ bias, int t, int q) {
-    const f4 bv = *reinterpret_cast<const f4*>(bias + 16 * t + 4 * q);
-    f4 v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = activate<ACT>(acc[r] + bv[r]);
-    return v;
-}
-
-// ---------------------------------------------------------- dense layers ---
-// Raw buffer load of one 16-B weight fragment: voffset = lane*16 (VGPR),
-// soffset = fragment position (SGPR).  Reads past the layer's num_records
-// return 0 (hardware range check), so the prefetch may run off the end.
-__device__ __forceinline__ f4 wload(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t layer_rsrc(const void* p, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
-}
 
 // Streaming dense layer [TIN tiles in -> TOUT = NB*TB tiles out].  The packed
 // weights [tb][u][j][lane] are ONE linear stream of 1-KiB fragments: u-step
@@ -223,11 +147,6 @@ __device__ __forceinline__ void reload(float (&x)[T][4], const f4* y, int lane) 
         const f4 v = y[u * 64 + lane];
         x[u][0] = v[0]; x[u][1] = v[1]; x[u][2] = v[2]; x[u][3] = v[3];
     }
-}
-
-// LDS carve-up of one block: [consts 2 KiB][biases L*HP + 32 floats][per-wave slabs]
-__host__ __device__ constexpr int param_bytes(int L, int HP) {
-    return ((kConstRows * kConstCols * 8 + (L * HP + 32) * 4) + 15) & ~15;
 }
 
 // ------------------------------------------------------------ the kernel ---
@@ -393,20 +312,6 @@ __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ argmin -------
-struct Best {
-    double c;
-    int64_t i;
-};
-
-// np.argmin: a NaN beats every number (first NaN wins); else smaller value;
-// equal values -> lower index.
-__device__ __forceinline__ bool better(const Best& a, const Best& b) {
-    const bool an = a.c != a.c, bn = b.c != b.c;
-    if (an != bn) return an;
-    if (!an && a.c != b.c) return a.c < b.c;
-    return a.i < b.i;
-}
-
 __global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
     __shared__ double sc[16];
     __shared__ int64_t si[16];

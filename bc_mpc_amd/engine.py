@@ -6,6 +6,7 @@ the HIP kernels; this file only marshals pointers.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -68,7 +69,7 @@ class RolloutEngine:
 
     def __init__(self, state_dim: int, action_dim: int, hidden: int, n_layers: int,
                  activation: str, layer_norm: bool, horizon: int, num_paths: int,
-                 device: int = 0, cost: str = "cheetah"):
+                 device: int = 0, cost: str = "cheetah", kernel: Optional[str] = None):
         self._lib = _lib.load()
         if activation not in _ACT:
             raise ValueError(f"unsupported activation {activation!r} (tanh | relu)")
@@ -81,6 +82,10 @@ class RolloutEngine:
         cfg.num_paths = int(num_paths)
         cfg.precision = _lib.PREC_FP32
         cfg.device = int(device)
+        kernel = kernel or os.environ.get("BCMPC_KERNEL", "auto")
+        if kernel not in _lib.KERNELS:
+            raise ValueError(f"unknown kernel {kernel!r}; one of {sorted(_lib.KERNELS)}")
+        cfg.kernel = _lib.KERNELS[kernel]
         h = ctypes.c_void_p()
         _lib.check(self._lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -183,9 +188,12 @@ class RolloutEngine:
         return float(r.value), float(m.value)
 
     def info(self) -> dict:
-        hp, wb, wpb = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
-        _lib.check(self._lib.bcmpc_engine_info(self._h, ctypes.byref(hp), ctypes.byref(wb), ctypes.byref(wpb)))
-        return dict(hidden_padded=hp.value, packed_weight_bytes=wb.value, waves_per_block=wpb.value)
+        hp, wb, wpb, kn = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self._lib.bcmpc_engine_info(self._h, ctypes.byref(hp), ctypes.byref(wb), ctypes.byref(wpb),
+                                               ctypes.byref(kn)))
+        names = {v: k for k, v in _lib.KERNELS.items()}
+        return dict(hidden_padded=hp.value, packed_weight_bytes=wb.value, waves_per_block=wpb.value,
+                    kernel=names.get(kn.value, str(kn.value)))
 
     def close(self) -> None:
         if getattr(self, "_h", None):

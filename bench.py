@@ -121,6 +121,9 @@ def main():
 
     eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local)
     eng.set_weights(MLPSpec(kernels, biases, act), norm, 1)
+    info = eng.info()
+    kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>"}.get(
+        info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
     d_state = torch.from_numpy(state).to(dev)
     d_actions = None
     if args.actions == "hbm":
@@ -189,7 +192,7 @@ def main():
         "kernel_ms_avg": kern_avg_s * 1e3,
         "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "rollout_fp32<512>", "flop_per_launch": K * H * fpcs,
+                     "kernel": kernel_name, "flop_per_launch": K * H * fpcs,
                      "flop_per_cand_step": fpcs},
         "cpu_baseline": None,
     }

@@ -52,6 +52,13 @@ typedef enum bcmpc_precision {
     BCMPC_PREC_FP32 = 0         /* f32 MLP on v_mfma_f32_16x16x4_f32 (exact f32 fma chain) */
 } bcmpc_precision;
 
+typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")              */
+    BCMPC_KERNEL_AUTO = 0,
+    BCMPC_KERNEL_SOLO = 1,      /* one wave owns 16 candidates, activations in VGPRs     */
+    BCMPC_KERNEL_GROUP2 = 2,    /* 2 waves share 16 candidates through an LDS slab       */
+    BCMPC_KERNEL_GROUP4 = 3     /* 4 waves share 16 candidates                           */
+} bcmpc_kernel;
+
 /* Replaces the constructor arguments of MPCcontroller (controllers.py:28-35)
  * plus the NNDynamicsModel shape (dynamics.py:8-19, build_network :54-62). */
 typedef struct bcmpc_config {
@@ -66,7 +73,8 @@ typedef struct bcmpc_config {
     int64_t num_paths;    /* K on this device (controllers.py:33 num_simulated_paths) */
     int32_t precision;    /* bcmpc_precision                                       */
     int32_t device;       /* HIP device ordinal                                    */
-    int32_t reserved[8];  /* must be zero                                          */
+    int32_t kernel;       /* bcmpc_kernel: 0 = auto                                */
+    int32_t reserved[7];  /* must be zero                                          */
 } bcmpc_config;
 
 /* Replaces the state NNDynamicsModel holds: TF variables
@@ -143,7 +151,7 @@ int bcmpc_last_kernel_ms(bcmpc_engine* eng, float* rollout_ms, float* argmin_ms)
 
 /* Static shape facts for tests: padded hidden size and packed weight bytes. */
 int bcmpc_engine_info(const bcmpc_engine* eng, int32_t* hidden_padded, int64_t* packed_weight_bytes,
-                      int32_t* waves_per_block);
+                      int32_t* waves_per_block, int32_t* kernel);
 
 #ifdef __cplusplus
 }

@@ -22,11 +22,14 @@ pytestmark = pytest.mark.gpu
 ATOL, RTOL = 1e-4, 1e-5
 
 
-def _engine(g: Golden, K=None, H=None, cost="cheetah"):
+KERNELS = ["solo", "group2", "group4"]
+
+
+def _engine(g: Golden, K=None, H=None, cost="cheetah", kernel="auto"):
     from bc_mpc_amd.engine import MLPSpec, RolloutEngine
     w = g.weights
     eng = RolloutEngine(g.S, g.A, w.hidden, w.n_layers, w.activation, w.layer_norm,
-                        H or g.H, K if K is not None else g.K, device=0, cost=cost)
+                        H or g.H, K if K is not None else g.K, device=0, cost=cost, kernel=kernel)
     eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), g.norm, version=1)
     return eng
 
@@ -55,10 +58,12 @@ def argmin_is_decidable(g: Golden) -> bool:
     return g.top2_gap > 2 * (ATOL + RTOL * abs(best)) and not g.near[g.argmin]
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", golden_names())
-def test_engine_matches_reference_fixture(name):
+def test_engine_matches_reference_fixture(name, kernel):
     g = Golden(name)
-    eng = _engine(g)
+    eng = _engine(g, kernel=kernel)
+    assert eng.info()["kernel"] == kernel
     if g.meta.get("inject") == "philox":
         res = eng.get_action(g.state, None, seed=g.meta["rng_seed"], cand_offset=g.meta["cand_offset"],
                              return_costs=True)
@@ -66,7 +71,7 @@ def test_engine_matches_reference_fixture(name):
     else:
         res = eng.get_action(g.state, g.actions(), return_costs=True)
         offset = 0
-    assert_costs_close(res.costs, g.costs, g.near, name)
+    assert_costs_close(res.costs, g.costs, g.near, f"{name}/{kernel}")
     assert res.best_index - offset == int(np.argmin(res.costs))
     if argmin_is_decidable(g):
         assert res.best_index - offset == g.argmin
@@ -103,15 +108,16 @@ def test_mpccontroller_dropin_bitexact(name):
     assert np.random.random() == float(g.z["next_draw"])
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", ["tiny_tanh", "small_relu", "small_ln_relu", "deep3_tanh", "one_layer_tanh",
                                   "nan_candidates", "ragged_k1", "ragged_k17_h1"])
-def test_trajectory_states_match(name):
+def test_trajectory_states_match(name, kernel):
     """states_paths_all (controllers.py:65-74) from the kernel vs the reference's."""
     import torch
     g = Golden(name)
     if "states" not in g.z.files:
         pytest.skip("fixture holds no states")
-    eng = _engine(g, cost="none")
+    eng = _engine(g, cost="none", kernel=kernel)
     dev = torch.device("cuda", 0)
     st = torch.from_numpy(g.state).to(dev)
     act = torch.from_numpy(np.ascontiguousarray(g.actions())).to(dev)
@@ -182,7 +188,8 @@ def test_non_fused_cost_goes_through_trajectory_mode():
     assert ctrl.last_index == i and np.array_equal(a, want)
 
 
-def test_full_size_cfg3_properties():
+@pytest.mark.parametrize("kernel", ["auto", "solo"])
+def test_full_size_cfg3_properties(kernel):
     """K=65536, H=20, 2x500 tanh (BASELINE cfg3 dims) at full size: shard
     invariance (bitwise), argmin consistency, determinism, and a 256-candidate
     oracle sample within tolerance -- device-RNG and host-action modes."""
@@ -195,7 +202,7 @@ def test_full_size_cfg3_properties():
     spec = MLPSpec(w.kernels, w.biases, w.activation)
 
     def mk(k):
-        e = RolloutEngine(20, 6, 500, 2, "tanh", False, H, k)
+        e = RolloutEngine(20, 6, 500, 2, "tanh", False, H, k, kernel=kernel)
         e.set_weights(spec, norm, 1)
         return e
 
