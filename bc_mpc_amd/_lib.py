@@ -30,7 +30,7 @@ OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
 ACT_TANH, ACT_RELU = 0, 1
 COST_CHEETAH, COST_NONE = 0, 1
 PREC_FP32 = 0
-KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3}
+KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3, "group8": 4}
 
 
 class Config(ctypes.Structure):

@@ -30,6 +30,10 @@ int fail(int code, const std::string& msg) {
             return fail(BCMPC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
+int kern_waves(int kern) {
+    return kern == BCMPC_KERNEL_GROUP8 ? 8 : kern == BCMPC_KERNEL_GROUP4 ? 4 : kern == BCMPC_KERNEL_GROUP2 ? 2 : 1;
+}
+
 int padded_hidden(int h) {
     for (int hp : {64, 128, 256, 512})
         if (h <= hp) return hp;
@@ -111,9 +115,11 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     // small K: one wave per block spreads candidates over more CUs
     const int64_t waves = (c.num_paths + 15) / 16;
     e->wpb = std::min(waves >= 4 * 256 ? 4 : 1, max_waves_per_block(e->HP, c.n_layers));
-    int kern = c.kernel == BCMPC_KERNEL_AUTO ? BCMPC_KERNEL_GROUP4 : c.kernel;
-    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_GROUP4) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
-    const int nw = kern == BCMPC_KERNEL_GROUP4 ? 4 : 2;
+    // auto: 4-wave groups; 8-wave groups when K is too small to give every SIMD two waves
+    int kern = c.kernel != BCMPC_KERNEL_AUTO ? c.kernel
+             : ((c.num_paths + 15) / 16 < 512 && e->T % 8 == 0 ? BCMPC_KERNEL_GROUP8 : BCMPC_KERNEL_GROUP4);
+    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_GROUP8) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
+    const int nw = kern_waves(kern);
     if (kern != BCMPC_KERNEL_SOLO &&
         (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw) > 160 * 1024)) {
         if (c.kernel != BCMPC_KERNEL_AUTO) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group kernel does not fit this shape"); }
@@ -259,7 +265,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     if (e->kernel == BCMPC_KERNEL_SOLO) {
         HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
     } else {
-        HIP_TRY(launch_rollout_grp(a, e->HP, e->kernel == BCMPC_KERNEL_GROUP4 ? 4 : 2, st));
+        HIP_TRY(launch_rollout_grp(a, e->HP, kern_waves(e->kernel), st));
     }
     HIP_TRY(hipEventRecord(e->ev[1], st));
     if (d_result) {
@@ -329,8 +335,7 @@ int bcmpc_engine_info(const bcmpc_engine* e, int32_t* hidden_padded, int64_t* pa
     if (!e) return fail(BCMPC_ERR_ARG, "null argument");
     if (hidden_padded) *hidden_padded = e->HP;
     if (packed_weight_bytes) *packed_weight_bytes = (int64_t)(e->w_floats * sizeof(float));
-    if (waves_per_block) *waves_per_block = e->kernel == BCMPC_KERNEL_SOLO ? e->wpb
-                                            : (e->kernel == BCMPC_KERNEL_GROUP4 ? 4 : 2);
+    if (waves_per_block) *waves_per_block = e->kernel == BCMPC_KERNEL_SOLO ? e->wpb : kern_waves(e->kernel);
     if (kernel) *kernel = e->kernel;
     return BCMPC_OK;
 }

@@ -37,7 +37,25 @@ namespace bcmpc {
 // waves per SIMD the register allocator must allow: 2-wave groups need ~250
 // registers per wave; 4-wave groups fit 128 (4/SIMD) up to HP = 256 and
 // ~134 (3/SIMD, spill-free) at HP = 512.
-constexpr int grp_waves_per_eu(int HP, int NW) { return NW == 2 ? 2 : (HP >= 512 ? 3 : 4); }
+#ifndef GRP_WPE512
+#define GRP_WPE512 3
+#endif
+#ifndef GRP_PRIO
+#define GRP_PRIO 0
+#endif
+#ifndef GRP_STAGGER
+#define GRP_STAGGER 0
+#endif
+#ifndef GRP_DIAG_SMALLW          // timing-only diagnostic: weights from a 16 KiB window (L1-resident)
+#define GRP_DIAG_SMALLW 0
+#endif
+#ifndef GRP_DIAG_NOBAR           // timing-only diagnostic: no group barriers (results wrong)
+#define GRP_DIAG_NOBAR 0
+#endif
+#ifndef GRP_LDS_PAD
+#define GRP_LDS_PAD 0
+#endif
+constexpr int grp_waves_per_eu(int HP, int NW) { return NW == 2 ? 2 : (NW == 8 ? 4 : (HP >= 512 ? GRP_WPE512 : 4)); }
 
 // acc[j] += sum over u-steps [u0, u1) of W[tile j][u] * slab[u]
 template <int TW, int UNR>
@@ -49,6 +67,7 @@ __device__ __forceinline__ void mm_slab(__amdgpu_buffer_rsrc_t rs, int wbase, in
 #pragma unroll
     for (int j = 0; j < TW; ++j) ring[j] = wload(rs, voff, wbase + u0 * STEPB + j * 1024);
     f4 xc = slab[u0 * 64 + lane];
+    if constexpr (GRP_PRIO) __builtin_amdgcn_s_setprio(1);
     for (int u = u0; u < u1; u += UNR) {
 #pragma unroll
         for (int uu = 0; uu < UNR; ++uu) {
@@ -59,10 +78,13 @@ __device__ __forceinline__ void mm_slab(__amdgpu_buffer_rsrc_t rs, int wbase, in
                 for (int j = 0; j < TW; ++j)
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[j][r], xc[r], acc[j], 0, 0, 0);
 #pragma unroll
-            for (int j = 0; j < TW; ++j) ring[j] = wload(rs, voff, wbase + (u + uu + 1) * STEPB + j * 1024);
+            for (int j = 0; j < TW; ++j)
+                ring[j] = wload(rs, voff, GRP_DIAG_SMALLW ? (((u + uu + 1) * 4 + j) & 15) * 1024
+                                                          : wbase + (u + uu + 1) * STEPB + j * 1024);
             xc = xn;
         }
     }
+    if constexpr (GRP_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // group LayerNorm of the wave's TW activated tiles (tf.contrib.layers.layer_norm,
@@ -149,6 +171,10 @@ void rollout_grp(const RolloutArgs a) {
     f4* slab = reinterpret_cast<f4*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP));
     float* red = reinterpret_cast<float*>(slab + grp_slab_tiles(T, NW) * 64);
     for (int i = threadIdx.x; i < 64; i += blockDim.x) slab[T * 64 + i] = (f4){0.f, 0.f, 0.f, 0.f};
+    if constexpr (GRP_STAGGER > 0) {            // de-phase co-resident groups (speed only)
+        const int n = (blockIdx.x % 3) * GRP_STAGGER;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     __syncthreads();
 
     double s[2][4];
@@ -233,19 +259,19 @@ void rollout_grp(const RolloutArgs a) {
 #pragma unroll
             for (int j = 0; j < TW; ++j) v[j] = bias_act<ACT>(acc[j], Bl + l * HP, tile0 + j, q);
             if constexpr (LN) group_layer_norm<TW, NW>(v, tile0, a.lng[l], a.lnb[l], a.hidden, red, w, lane);
-            __syncthreads();                          // every wave is done reading the slab
+            if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // every wave is done reading the slab
 #pragma unroll
             for (int j = 0; j < TW; ++j) slab[(tile0 + j) * 64 + lane] = v[j];
-            __syncthreads();                          // new activations visible
+            if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // new activations visible
         }
 
         // ---- output layer: [h -> S], u split over the group ----
         f4 po[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
         mm_slab<2, (UO % 2 == 0) ? 2 : 1>(rsL, 0, w * UO, (w + 1) * UO, slab, po, lane);
-        __syncthreads();                              // done reading activations
+        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();       // done reading activations
         slab[(2 * w + 0) * 64 + lane] = po[0];
         slab[(2 * w + 1) * 64 + lane] = po[1];
-        __syncthreads();
+        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();
         f4 o[2] = {slab[0 * 64 + lane], slab[1 * 64 + lane]};
 #pragma unroll
         for (int k = 1; k < NW; ++k) {                // fixed summation order
@@ -295,7 +321,7 @@ void rollout_grp(const RolloutArgs a) {
 // ------------------------------------------------------------ launchers ----
 template <int HP, int ACT, bool LN, int NW>
 static hipError_t launch_grp_t(const RolloutArgs& a, hipStream_t st) {
-    const size_t lds = (size_t)param_bytes(a.L, HP) + grp_slab_bytes<HP, NW>();
+    const size_t lds = (size_t)param_bytes(a.L, HP) + grp_slab_bytes<HP, NW>() + GRP_LDS_PAD;
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)rollout_grp<HP, ACT, LN, NW>,
@@ -319,7 +345,9 @@ static hipError_t launch_grp_act(const RolloutArgs& a, hipStream_t st) {
 template <int NW>
 static hipError_t launch_grp_nw(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
     switch (hidden_padded) {
-        case 64: return launch_grp_act<64, NW>(a, st);
+        case 64:
+            if constexpr (NW <= 4) return launch_grp_act<64, NW>(a, st);
+            return hipErrorInvalidValue;
         case 128: return launch_grp_act<128, NW>(a, st);
         case 256: return launch_grp_act<256, NW>(a, st);
         case 512: return launch_grp_act<512, NW>(a, st);
@@ -336,6 +364,7 @@ hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, h
     switch (nw) {
         case 2: return launch_grp_nw<2>(a, hidden_padded, st);
         case 4: return launch_grp_nw<4>(a, hidden_padded, st);
+        case 8: return launch_grp_nw<8>(a, hidden_padded, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -32,6 +32,7 @@ WORKLOADS = {
     "cfg2": dict(K=4096, H=20, hidden=500, L=2, act="tanh"),
     "cfg3": dict(K=65536, H=20, hidden=500, L=2, act="tanh"),
     "cfg4_shard": dict(K=32768, H=20, hidden=500, L=2, act="tanh"),   # 262144 / 8 per GPU
+    "cfg3_relu": dict(K=65536, H=20, hidden=500, L=2, act="relu"),    # diagnostic: no tanh
     "ppo_defaults": dict(K=400, H=7, hidden=256, L=2, act="relu"),
 }
 S_DIM, A_DIM = 20, 6
@@ -87,9 +88,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (N ranks on one GPU): BCMPC_DIST_BACKEND=gloo BCMPC_BENCH_DEVICE=0
+    backend = os.environ.get("BCMPC_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("BCMPC_BENCH_DEVICE", local))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -122,7 +129,8 @@ def main():
     eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local)
     eng.set_weights(MLPSpec(kernels, biases, act), norm, 1)
     info = eng.info()
-    kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>"}.get(
+    kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
+                   "group8": "rollout_grp<NW=8>"}.get(
         info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
     d_state = torch.from_numpy(state).to(dev)
     d_actions = None
@@ -160,7 +168,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -186,7 +194,9 @@ def main():
         "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
                                f"{L}x{hidden} {act}, fp32 MFMA, 1 RCCL all-gather min-loc per step",
                    "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
-                   "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}"},
+                   "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
+                   "collective": f"{backend} all_gather min-loc, {3 + A_DIM} f64 per rank per step" if world > 1
+                   else "none (1 rank)"},
         "p50_ms": float(np.percentile(step_s, 50) * 1e3),
         "p90_ms": float(np.percentile(step_s, 90) * 1e3),
         "kernel_ms_avg": kern_avg_s * 1e3,

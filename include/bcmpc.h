@@ -56,7 +56,8 @@ typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")  
     BCMPC_KERNEL_AUTO = 0,
     BCMPC_KERNEL_SOLO = 1,      /* one wave owns 16 candidates, activations in VGPRs     */
     BCMPC_KERNEL_GROUP2 = 2,    /* 2 waves share 16 candidates through an LDS slab       */
-    BCMPC_KERNEL_GROUP4 = 3     /* 4 waves share 16 candidates                           */
+    BCMPC_KERNEL_GROUP4 = 3,    /* 4 waves share 16 candidates                           */
+    BCMPC_KERNEL_GROUP8 = 4     /* 8 waves share 16 candidates (small K)                 */
 } bcmpc_kernel;
 
 /* Replaces the constructor arguments of MPCcontroller (controllers.py:28-35)

@@ -29,3 +29,11 @@ if [ "${PROFILE:-1}" = 1 ]; then
     stop_on $? rocprof
     find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*" | head
 fi
+if [ "${REHEARSE:-1}" = 1 ]; then
+    cd "${GRAFT_REPO_ROOT:-/root/repo}"
+    BCMPC_DIST_BACKEND=gloo BCMPC_BENCH_DEVICE=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 \
+        --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench_2rank_rehearsal.log 2>&1
+    stop_on $? rehearsal
+    tail -1 gpurun_out/bench_2rank_rehearsal.log
+fi
