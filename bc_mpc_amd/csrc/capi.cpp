@@ -35,7 +35,7 @@ int kern_waves(int kern) {
 }
 
 int padded_hidden(int h) {
-    for (int hp : {64, 128, 256, 512})
+    for (int hp : {64, 128, 256, 512, 768, 1024})
         if (h <= hp) return hp;
     return -1;
 }
@@ -96,7 +96,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     if (c.action_dim < 1 || c.action_dim > BCMPC_MAX_ACTION) return fail(BCMPC_ERR_UNSUPPORTED, "action_dim must be in [1, 16]");
     if (c.state_dim + c.action_dim > BCMPC_MAX_INPUT) return fail(BCMPC_ERR_UNSUPPORTED, "state_dim + action_dim must be <= 32");
     if (c.n_layers < 1 || c.n_layers > BCMPC_MAX_LAYERS) return fail(BCMPC_ERR_UNSUPPORTED, "n_layers must be in [1, 8]");
-    if (padded_hidden(c.hidden) < 0 || c.hidden < 1) return fail(BCMPC_ERR_UNSUPPORTED, "hidden must be in [1, 512] in this build");
+    if (padded_hidden(c.hidden) < 0 || c.hidden < 1) return fail(BCMPC_ERR_UNSUPPORTED, "hidden must be in [1, 1024] in this build");
     if (c.activation != BCMPC_ACT_TANH && c.activation != BCMPC_ACT_RELU) return fail(BCMPC_ERR_UNSUPPORTED, "activation must be tanh or relu");
     if (c.horizon < 1) return fail(BCMPC_ERR_ARG, "horizon must be >= 1");
     if (c.num_paths < 0) return fail(BCMPC_ERR_ARG, "num_paths must be >= 0");
@@ -125,7 +125,11 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (c.kernel != BCMPC_KERNEL_AUTO) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group kernel does not fit this shape"); }
         kern = BCMPC_KERNEL_SOLO;
     }
-    if (kern == BCMPC_KERNEL_SOLO && e->wpb < 1) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "layer stack does not fit in LDS"); }
+    if (kern == BCMPC_KERNEL_GROUP2 && e->HP > 512) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group2 kernel supports hidden <= 512"); }
+    if (kern == BCMPC_KERNEL_SOLO && (e->wpb < 1 || e->HP > 512)) {
+        delete e;
+        return fail(BCMPC_ERR_UNSUPPORTED, "solo kernel supports hidden <= 512 and needs LDS for its slabs");
+    }
     e->kernel = kern;
     e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->T / nw;
     const int L = c.n_layers, T = e->T;

@@ -55,7 +55,11 @@ namespace bcmpc {
 #ifndef GRP_LDS_PAD
 #define GRP_LDS_PAD 0
 #endif
-constexpr int grp_waves_per_eu(int HP, int NW) { return NW == 2 ? 2 : (NW == 8 ? 4 : (HP >= 512 ? GRP_WPE512 : 4)); }
+constexpr int grp_waves_per_eu(int HP, int NW) {
+    return NW == 2 ? 2
+         : NW == 8 ? (HP >= 768 ? 3 : 4)
+         : (HP >= 768 ? 2 : HP >= 512 ? GRP_WPE512 : 4);
+}
 
 // acc[j] += sum over u-steps [u0, u1) of W[tile j][u] * slab[u]
 template <int TW, int UNR>
@@ -351,6 +355,12 @@ static hipError_t launch_grp_nw(const RolloutArgs& a, int hidden_padded, hipStre
         case 128: return launch_grp_act<128, NW>(a, st);
         case 256: return launch_grp_act<256, NW>(a, st);
         case 512: return launch_grp_act<512, NW>(a, st);
+        case 768:
+            if constexpr (NW >= 4) return launch_grp_act<768, NW>(a, st);
+            return hipErrorInvalidValue;
+        case 1024:
+            if constexpr (NW >= 4) return launch_grp_act<1024, NW>(a, st);
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }

@@ -33,6 +33,7 @@ WORKLOADS = {
     "cfg3": dict(K=65536, H=20, hidden=500, L=2, act="tanh"),
     "cfg4_shard": dict(K=32768, H=20, hidden=500, L=2, act="tanh"),   # 262144 / 8 per GPU
     "cfg3_relu": dict(K=65536, H=20, hidden=500, L=2, act="relu"),    # diagnostic: no tanh
+    "cfg5_pass": dict(K=65536, H=50, hidden=1024, L=3, act="tanh"),   # one random-shooting pass of cfg5
     "ppo_defaults": dict(K=400, H=7, hidden=256, L=2, act="relu"),
 }
 S_DIM, A_DIM = 20, 6
@@ -45,7 +46,7 @@ def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM):
     return 2 * ((S + A) * hidden + (L - 1) * hidden * hidden + hidden * S)
 
 
-def cpu_baseline(spec_w, norm, state, H, budget_s):
+def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net):
     """The oracle (NumPy restatement of the reference path, kind "port") timed on
     the host cores over a bounded sample of the same workload."""
     from oracle import mpc_oracle as orc
@@ -55,7 +56,7 @@ def cpu_baseline(spec_w, norm, state, H, budget_s):
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     dyn = orc.NumpyDynamics(spec_w, norm)
-    Ks = 8192
+    Ks = min(8192, K_full)
     rs = np.random.RandomState(0)
     done, calls, t0 = 0, 0, time.perf_counter()
     while True:
@@ -66,8 +67,8 @@ def cpu_baseline(spec_w, norm, state, H, budget_s):
             break
     el = time.perf_counter() - t0
     return dict(value=done / el, unit="candidate-steps/s", cores=int(threads), kind="port",
-                sample=f"{calls} oracle get_action calls at K={Ks} (1/8 of cfg3's K), H={H}, "
-                       f"2x500 tanh, OpenBLAS {threads} threads, {el:.1f} s")
+                sample=f"{calls} oracle get_action calls at K={Ks} (of the workload's K={K_full}), H={H}, "
+                       f"{net}, OpenBLAS {threads} threads, {el:.1f} s")
 
 
 def main():
@@ -217,7 +218,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import mpc_oracle as orc
         w = orc.MLPWeights(kernels, biases, act)
-        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds)
+        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, f"{L}x{hidden} {act}")
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -249,3 +249,23 @@ def test_errors_are_python_exceptions():
         e2.get_action(np.zeros(20))
     with pytest.raises(ValueError):
         e2.set_weights(MLPSpec(w.kernels[:2], w.biases[:2]), orc.synthetic_normalization(), 1)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "group4", "group8"])
+@pytest.mark.parametrize("hidden,L,act,ln", [(1024, 3, "tanh", False), (768, 2, "tanh", False),
+                                             (1000, 3, "relu", True), (600, 2, "tanh", False)])
+def test_large_hidden_vs_oracle(hidden, L, act, ln, kernel):
+    """cfg5-class networks (3x1024) and odd widths on the group kernels."""
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    K, H = 96, 4
+    w = orc.synthetic_weights(20, 6, hidden, L, act, ln, seed_base=77)
+    norm = orc.synthetic_normalization()
+    state = orc.synthetic_state(norm)
+    acts = np.random.RandomState(5).uniform(-1, 1, (H, K, 6))
+    eng = RolloutEngine(20, 6, hidden, L, act, ln, H, K, kernel=kernel)
+    eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), norm, 1)
+    res = eng.get_action(state, acts, return_costs=True)
+    want, states = orc.rollout(orc.NumpyDynamics(w, norm), state, acts)
+    assert_costs_close(res.costs, want, orc.near_threshold_mask(states), f"h{hidden}xL{L}/{kernel}")
+    assert res.best_index == int(np.argmin(res.costs))
