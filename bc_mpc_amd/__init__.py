@@ -5,11 +5,11 @@ path (controllers.py:57-88 -> dynamics.py:106-119 -> cost_functions.py:9-63).
 The compute path is libbcmpc.so (HIP, gfx950); see DESIGN.md.
 """
 from . import _lib
-from .controllers import Controller, MPCcontroller, RandomController
+from .controllers import Controller, MPCcontroller, MPCcontrollerPolicyNet, RandomController
 from .cost_functions import cheetah_cost_fn, trajectory_cost_fn
-from .engine import MLPSpec, RolloutEngine, StepResult
+from .engine import MLPSpec, PolicySpec, RolloutEngine, StepResult
 
-__all__ = ["Controller", "MPCcontroller", "RandomController", "cheetah_cost_fn", "trajectory_cost_fn",
+__all__ = ["Controller", "MPCcontroller", "MPCcontrollerPolicyNet", "RandomController", "PolicySpec", "cheetah_cost_fn", "trajectory_cost_fn",
            "MLPSpec", "RolloutEngine", "StepResult"]
 
 _lib.load()   # fail loudly at import when the HIP library is missing

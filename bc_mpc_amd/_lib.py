@@ -47,7 +47,10 @@ class Config(ctypes.Structure):
         ("precision", ctypes.c_int32),
         ("device", ctypes.c_int32),
         ("kernel", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("policy_hidden", ctypes.c_int32),
+        ("policy_layers", ctypes.c_int32),
+        ("policy_mode", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -70,6 +73,20 @@ class Weights(ctypes.Structure):
     ]
 
 
+class Policy(ctypes.Structure):
+    _fields_ = [
+        ("kernels", ctypes.POINTER(_FP)),
+        ("biases", ctypes.POINTER(_FP)),
+        ("ob_mean", _FP),
+        ("ob_std", _FP),
+        ("logstd", _FP),
+        ("explore", ctypes.c_double),
+    ]
+
+
+POLICY_MODES = {"explore": 0, "stochastic": 1}
+
+
 class Result(ctypes.Structure):
     _fields_ = [
         ("best_index", ctypes.c_int64),
@@ -86,6 +103,8 @@ SIGNATURES = [
     ("bcmpc_destroy", ctypes.c_int, [ctypes.c_void_p]),
     ("bcmpc_set_weights", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Weights), ctypes.c_uint64]),
     ("bcmpc_weights_version", ctypes.c_uint64, [ctypes.c_void_p]),
+    ("bcmpc_set_policy", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Policy), ctypes.c_uint64]),
+    ("bcmpc_first_actions", ctypes.c_int, [ctypes.c_void_p, _DP]),
     ("bcmpc_set_action_bounds", ctypes.c_int, [ctypes.c_void_p, _DP, _DP]),
     ("bcmpc_get_action", ctypes.c_int,
      [ctypes.c_void_p, _DP, _DP, ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(Result), _DP]),

@@ -30,6 +30,7 @@ from typing import Optional
 import numpy as np
 
 from . import distributed as _dist
+from . import policy as _policy
 from . import weights as _weights
 from .cost_functions import is_cheetah_cost, trajectory_cost_fn
 from .engine import RolloutEngine
@@ -196,3 +197,111 @@ class MPCcontroller(Controller):
                           stream.cuda_stream)
         traj = d_traj.cpu().numpy()                       # synchronises the stream
         return np.asarray(trajectory_cost_fn(self.cost_fn, traj[:-1], local_actions, traj[1:]), dtype=np.float64)
+
+
+class MPCcontrollerPolicyNet(Controller):
+    """Policy-guided MPC (controllers.py:160-237) on the MI355X rollout engine.
+
+    Each horizon step the policy net's action for every candidate is computed
+    inside the rollout kernel (fused 20->h->h->6 tanh MLP, ppo_bc_policy.py:
+    54-88), mixed with the exploration draw and fed to the dynamics MLP:
+
+    * ``self_exp=False`` (train_mpc_ppo.py default, FLAGS.SELFEXP):
+      ``(1 - explore) * mean + explore * exploration[i]`` (controllers.py:204-208)
+      -- deterministic given the global NumPy stream, bit-for-bit parity;
+    * ``self_exp=True``: ``mean + exp(logstd) * N(0, 1)`` (DiagGaussianPd.sample).
+      TF's random_normal stream cannot be reproduced outside TF; the engine
+      draws N(0,1) with Philox (seed from ``seed=`` or a private generator, so
+      the global NumPy stream is consumed exactly as the reference does).
+
+    ``sample_random_actions`` is still called once per step in both modes
+    (controllers.py:191), preserving the reference's RNG side effect.
+    """
+
+    def __init__(self,
+                 env,
+                 dyn_model,
+                 policy_net,
+                 explore=1.,
+                 self_exp=True,
+                 horizon=5,
+                 cost_fn=None,
+                 num_simulated_paths=10,
+                 *,
+                 seed: Optional[int] = None,
+                 device: Optional[int] = None,
+                 process_group=None):
+        self.env = env
+        self.dyn_model = dyn_model
+        self.policy_net = policy_net
+        self.horizon = horizon
+        self.cost_fn = cost_fn
+        self.num_simulated_paths = num_simulated_paths
+        self.self_exp = self_exp
+        self.explore = explore
+        self._seed_rng = np.random.RandomState(0x5EEDF00D if seed is None else seed)
+        self._device = device
+        self._group = process_group
+        self._engine = None
+        self._engine_key = None
+        self.last_cost = None
+        self.last_index = None
+        self.last_costs = None
+        self.keep_costs = False
+
+    # controllers.py:181-186
+    def sample_random_actions(self):
+        np_action_paths = np.random.uniform(low=self.env.action_space.low, high=self.env.action_space.high,
+                                            size=[self.horizon, self.num_simulated_paths,
+                                                  len(self.env.action_space.high)])
+        return np_action_paths
+
+    def _engine_for(self, spec, pspec, S, A, k_local) -> RolloutEngine:
+        dev = _default_device() if self._device is None else self._device
+        mode = "stochastic" if self.self_exp else "explore"
+        key = (S, A, spec.hidden, spec.n_layers, spec.activation, spec.layer_norm, int(self.horizon), int(k_local),
+               dev, pspec.hidden, pspec.n_layers, mode)
+        if self._engine is None or self._engine_key != key:
+            if self._engine is not None:
+                self._engine.close()
+            self._engine = RolloutEngine(S, A, spec.hidden, spec.n_layers, spec.activation, spec.layer_norm,
+                                         int(self.horizon), int(k_local), device=dev, cost="cheetah",
+                                         policy_hidden=pspec.hidden, policy_layers=pspec.n_layers,
+                                         policy_mode=mode)
+            self._engine.set_action_bounds(np.asarray(self.env.action_space.low, dtype=np.float64),
+                                           np.asarray(self.env.action_space.high, dtype=np.float64))
+            self._engine_key = key
+        return self._engine
+
+    # controllers.py:189-237
+    def get_action(self, state):
+        S = int(np.prod(self.env.observation_space.shape))
+        A = len(self.env.action_space.high)
+        K = int(self.num_simulated_paths)
+        if self.horizon < 1:
+            raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+        if not is_cheetah_cost(self.cost_fn, S, A):
+            raise ValueError("MPCcontrollerPolicyNet on the engine needs the fused cheetah cost_fn")
+        state = np.asarray(state, dtype=np.float64).reshape(-1)
+        rank, ws = _dist.world(self._group)
+        lo, hi = _dist.shard_range(K, rank, ws)
+        spec, norm, version = _weights.extract(self.dyn_model)
+        pspec, pversion = _policy.extract(self.policy_net)
+        exploration = self.sample_random_actions()           # every rank draws the full [H, K, A]
+        seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+        if K == 0:
+            raise ValueError("attempt to get argmin of an empty sequence")
+        valid, cost, index, first = False, float("inf"), -1, None
+        if hi > lo:
+            eng = self._engine_for(spec, pspec, S, A, hi - lo)
+            eng.set_weights(spec, norm, version)
+            eng.set_policy(pspec, float(self.explore), pversion)
+            local = np.ascontiguousarray(exploration[:, lo:hi, :])
+            res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
+            valid, cost, index, first = True, res.best_cost, res.best_index, res.first_action
+            self.last_costs = res.costs
+        cost, index, first_g = _dist.allgather_minloc(valid, cost, index, first, A, self._group)
+        self.last_cost, self.last_index = cost, index
+        return first_g                                         # copy of action_paths[0, argmin] (:233-235)
+
+    get_action_mcs = get_action                                # controllers.py:239 (identical body)

@@ -57,6 +57,20 @@ void pack_layer(const float* W, int in, int out, int Tin, int Tout, int TB, floa
     }
 }
 
+// Output layer of the policy: one 16-row output tile whose row n holds action
+// rowmap[n] (or zero): the host places action j at row S-16+j, i.e. in exactly
+// the lanes/registers where the dynamics' layer-0 input expects action j.
+void pack_out_rows(const float* W, int in, int out, int Tin, const int* rowmap, float* dst) {
+    for (int u = 0; u < Tin; ++u)
+        for (int lane = 0; lane < 64; ++lane)
+            for (int r = 0; r < 4; ++r) {
+                const int k = 16 * u + 4 * (lane >> 4) + r;
+                const int c = rowmap[lane & 15];
+                const size_t o = (((size_t)u * 64) + lane) * 4 + r;
+                dst[o] = (k < in && c >= 0 && c < out) ? W[(size_t)k * out + c] : 0.f;
+            }
+}
+
 }  // namespace
 
 struct bcmpc_engine {
@@ -81,6 +95,14 @@ struct bcmpc_engine {
     bool has_weights = false;
     hipEvent_t ev[3]{};
     bool timed = false;
+    // fused policy (MPCcontrollerPolicyNet)
+    int PHP = 0, TP = 0, PL = 0;
+    float* d_pw = nullptr;  size_t pw_floats = 0;  size_t pw_off[BCMPC_MAX_LAYERS + 1]{};
+    float* d_pb = nullptr;                          // [PL][PHP] + kPolParams
+    double* d_first = nullptr;                      // [K][A] step-0 actions
+    double explore = 0.0;
+    uint64_t pol_version = 0;
+    bool has_policy = false;
 };
 
 extern "C" {
@@ -118,10 +140,25 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     // auto: 4-wave groups; 8-wave groups when K is too small to give every SIMD two waves
     int kern = c.kernel != BCMPC_KERNEL_AUTO ? c.kernel
              : ((c.num_paths + 15) / 16 < 512 && e->T % 8 == 0 ? BCMPC_KERNEL_GROUP8 : BCMPC_KERNEL_GROUP4);
+    if (c.policy_hidden > 0) {
+        // MPCcontrollerPolicyNet: the policy MLP is fused into the 4-wave group kernel
+        if (c.policy_hidden > 128 || c.policy_layers < 1 || c.policy_layers > BCMPC_MAX_LAYERS)
+            { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy: hidden must be in [1,128], layers in [1,8]"); }
+        if (c.state_dim < 16) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines need state_dim >= 16"); }
+        if (e->HP < 128 || e->HP > 512) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines support dynamics hidden 65..512"); }
+        if (c.policy_mode != BCMPC_POLICY_EXPLORE && c.policy_mode != BCMPC_POLICY_STOCHASTIC)
+            { delete e; return fail(BCMPC_ERR_ARG, "unknown policy_mode"); }
+        if (c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4)
+            { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines run on the group4 kernel"); }
+        kern = BCMPC_KERNEL_GROUP4;
+        e->PHP = 128;
+        e->TP = 8;
+        e->PL = c.policy_layers;
+    }
     if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_GROUP8) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
     const int nw = kern_waves(kern);
     if (kern != BCMPC_KERNEL_SOLO &&
-        (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw) > 160 * 1024)) {
+        (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw, e->PHP, e->PL) > 160 * 1024)) {
         if (c.kernel != BCMPC_KERNEL_AUTO) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group kernel does not fit this shape"); }
         kern = BCMPC_KERNEL_SOLO;
     }
@@ -156,6 +193,19 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     }
     for (int i = 0; i < 3; ++i)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { g_last_error = "event create failed"; return cleanup(BCMPC_ERR_HIP); }
+    if (e->PL > 0) {
+        size_t poff = 0;
+        e->pw_off[0] = poff; poff += (size_t)e->TP * 2 * 64 * 4;                    // [S -> ph]
+        for (int l = 1; l < e->PL; ++l) { e->pw_off[l] = poff; poff += (size_t)e->TP * e->TP * 64 * 4; }
+        e->pw_off[e->PL] = poff; poff += (size_t)e->TP * 64 * 4;                  // [ph -> one 16-row tile]
+        e->pw_floats = poff;
+        if (hipMalloc(&e->d_pw, poff * sizeof(float)) != hipSuccess ||
+            hipMalloc(&e->d_pb, ((size_t)e->PL * e->PHP + kPolParams) * sizeof(float)) != hipSuccess ||
+            hipMalloc(&e->d_first, std::max<int64_t>(1, c.num_paths) * c.action_dim * sizeof(double)) != hipSuccess) {
+            g_last_error = "device allocation failed";
+            return cleanup(BCMPC_ERR_HIP);
+        }
+    }
     // default action bounds: HalfCheetah ctrlrange [-1, 1]
     for (int j = 0; j < BCMPC_MAX_ACTION && j < kConstCols; ++j) {
         e->h_consts[6 * kConstCols + j] = -1.0;
@@ -169,7 +219,8 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (!e) return BCMPC_OK;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
-                    (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result})
+                    (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
+                    (void*)e->d_first})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
     for (auto& ev : e->ev)
@@ -225,6 +276,54 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
     return BCMPC_OK;
 }
 
+int bcmpc_set_policy(bcmpc_engine* e, const bcmpc_policy* p, uint64_t version) {
+    if (!e || !p || !p->kernels || !p->biases || !p->ob_mean || !p->ob_std || !p->logstd)
+        return fail(BCMPC_ERR_ARG, "null argument");
+    if (e->PL == 0) return fail(BCMPC_ERR_STATE, "engine was created without a policy (config.policy_hidden == 0)");
+    if (e->has_policy && version == e->pol_version) { e->explore = p->explore; return BCMPC_OK; }
+    const bcmpc_config& c = e->cfg;
+    const int S = c.state_dim, A = c.action_dim, ph = c.policy_hidden, PL = e->PL, TP = e->TP, PHP = e->PHP;
+    for (int l = 0; l <= PL; ++l)
+        if (!p->kernels[l] || !p->biases[l]) return fail(BCMPC_ERR_ARG, "null policy kernel/bias pointer");
+    HIP_TRY(hipSetDevice(c.device));
+    std::vector<float> hw(e->pw_floats, 0.f);
+    const int tb = TP / 4;
+    pack_layer(p->kernels[0], S, ph, 2, TP, tb, hw.data() + e->pw_off[0]);
+    for (int l = 1; l < PL; ++l) pack_layer(p->kernels[l], ph, ph, TP, TP, tb, hw.data() + e->pw_off[l]);
+    int rowmap[16];
+    for (int n = 0; n < 16; ++n) {
+        const int j = n - (S - 16);                     // action j sits at output-tile row S-16+j
+        rowmap[n] = (j >= 0 && j < A) ? j : -1;
+    }
+    pack_out_rows(p->kernels[PL], ph, A, TP, rowmap, hw.data() + e->pw_off[PL]);
+    std::vector<float> hb((size_t)PL * PHP + kPolParams, 0.f);
+    for (int l = 0; l < PL; ++l) std::memcpy(hb.data() + (size_t)l * PHP, p->biases[l], sizeof(float) * ph);
+    float* pm = hb.data() + (size_t)PL * PHP;           // [obmean 32][obstd 32][logstd 16][outbias 16]
+    for (int d = 0; d < 32; ++d) {
+        pm[d] = d < S ? p->ob_mean[d] : 0.f;
+        pm[32 + d] = d < S ? p->ob_std[d] : 1.f;
+    }
+    for (int j = 0; j < A; ++j) {
+        pm[64 + j] = p->logstd[j];
+        pm[80 + (S - 16 + j)] = p->biases[PL][j];
+    }
+    HIP_TRY(hipMemcpyAsync(e->d_pw, hw.data(), hw.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_pb, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->explore = p->explore;
+    e->pol_version = version;
+    e->has_policy = true;
+    return BCMPC_OK;
+}
+
+int bcmpc_first_actions(bcmpc_engine* e, double* out) {
+    if (!e || !out) return fail(BCMPC_ERR_ARG, "null argument");
+    if (!e->d_first) return fail(BCMPC_ERR_STATE, "engine has no policy");
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    HIP_TRY(hipMemcpy(out, e->d_first, sizeof(double) * e->cfg.num_paths * e->cfg.action_dim, hipMemcpyDeviceToHost));
+    return BCMPC_OK;
+}
+
 int bcmpc_set_action_bounds(bcmpc_engine* e, const double* low, const double* high) {
     if (!e || !low || !high) return fail(BCMPC_ERR_ARG, "null argument");
     for (int j = 0; j < e->cfg.action_dim; ++j) {
@@ -265,6 +364,23 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     a.seed = seed; a.cand_offset = cand_offset; a.K = c.num_paths;
     a.H = c.horizon; a.S = c.state_dim; a.A = c.action_dim; a.L = c.n_layers;
     a.hidden = c.hidden; a.act = c.activation; a.ln = c.layer_norm; a.cost = c.cost;
+    if (e->PL > 0) {
+        if (!e->has_policy) return fail(BCMPC_ERR_STATE, "bcmpc_set_policy has not been called");
+        if (c.cost != BCMPC_COST_CHEETAH) return fail(BCMPC_ERR_UNSUPPORTED, "policy engines need the fused cost");
+        for (int l = 0; l <= e->PL; ++l) {
+            const size_t end = l < e->PL ? e->pw_off[l + 1] : e->pw_floats;
+            a.pwbytes[l] = (int32_t)((end - e->pw_off[l]) * sizeof(float));
+            a.pw[l] = reinterpret_cast<const float __attribute__((ext_vector_type(4)))*>(e->d_pw + e->pw_off[l]);
+        }
+        for (int l = 0; l < e->PL; ++l) a.pb[l] = e->d_pb + (size_t)l * e->PHP;
+        a.pparams = e->d_pb + (size_t)e->PL * e->PHP;
+        a.pL = e->PL;
+        a.phidden_padded = e->PHP;
+        a.pol_mode = c.policy_mode;
+        a.explore = e->explore;
+        a.act_out = e->d_first;
+        a.act_out_steps = 1;
+    }
     HIP_TRY(hipEventRecord(e->ev[0], st));
     if (e->kernel == BCMPC_KERNEL_SOLO) {
         HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
@@ -275,6 +391,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     if (d_result) {
         ArgminArgs m{};
         m.costs = d_costs; m.actions = d_actions; m.consts = e->d_consts; m.out = d_result;
+        m.act_out = e->PL > 0 ? e->d_first : nullptr;
         m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
         HIP_TRY(launch_argmin(m, st));
     }

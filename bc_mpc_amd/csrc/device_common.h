@@ -86,6 +86,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t layer_rsrc(const void* p, int 
 }
 
 // LDS carve-up of one block: [consts 2 KiB][biases L*HP + 32 floats][per-wave slabs]
+__host__ __device__ constexpr int pol_param_bytes(int PL, int PHP) {
+    return PHP == 0 ? 0 : (((PL * PHP + kPolParams) * 4) + 15) & ~15;
+}
+
 __host__ __device__ constexpr int param_bytes(int L, int HP) {
     return ((kConstRows * kConstCols * 8 + (L * HP + 32) * 4) + 15) & ~15;
 }

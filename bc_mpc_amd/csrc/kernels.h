@@ -29,10 +29,21 @@ struct RolloutArgs {
     int64_t cand_offset;
     int64_t K;
     int32_t H, S, A, L, hidden, act, ln, cost;
+    // fused policy (MPCcontrollerPolicyNet, controllers.py:189-237); pL == 0: none
+    const float __attribute__((ext_vector_type(4)))* pw[BCMPC_MAX_LAYERS + 1];
+    int32_t pwbytes[BCMPC_MAX_LAYERS + 1];
+    const float* pb[BCMPC_MAX_LAYERS];       // padded hidden biases
+    const float* pparams;                    // kPolParams floats: obmean[32] obstd[32] logstd[16] outbias[16]
+    int32_t pL, phidden_padded, pol_mode;
+    double explore;
+    double* act_out;                         // [act_out_steps][K][A] f64 actions actually rolled out, or nullptr
+    int32_t act_out_steps;
 };
+constexpr int kPolParams = 96;
 
 struct ArgminArgs {
     const double* costs;
+    const double* act_out;   // [.][K][A] actions written by the rollout (policy mode) or nullptr
     const double* actions;   // [H][K][A] or nullptr
     const double* consts;
     bcmpc_result* out;
@@ -44,7 +55,7 @@ struct ArgminArgs {
 
 int max_waves_per_block(int hidden_padded, int n_layers);
 hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st);
-size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw);
+size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_padded, int policy_layers);
 hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 

@@ -340,7 +340,8 @@ __global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
         if (best.i < a.K) {
             for (int j = 0; j < a.A; ++j) {
                 out->first_action[j] =
-                    a.actions ? a.actions[best.i * a.A + j]     // action_paths[0, i*, :] (controllers.py:84-85)
+                    a.act_out ? a.act_out[best.i * a.A + j]     // policy-mixed actions (controllers.py:233-235)
+                    : a.actions ? a.actions[best.i * a.A + j]   // action_paths[0, i*, :] (controllers.py:84-85)
                               : rng_action(a.seed, (uint64_t)(a.cand_offset + best.i), 0, j,
                                            a.consts[6 * 32 + j], a.consts[7 * 32 + j]);
             }

@@ -55,8 +55,9 @@ namespace bcmpc {
 #ifndef GRP_LDS_PAD
 #define GRP_LDS_PAD 0
 #endif
-constexpr int grp_waves_per_eu(int HP, int NW) {
-    return NW == 2 ? 2
+constexpr int grp_waves_per_eu(int HP, int NW, int PHP = 0) {
+    return PHP > 0 ? (HP >= 512 ? 2 : 3)              // fused policy: more live state per wave
+         : NW == 2 ? 2
          : NW == 8 ? (HP >= 768 ? 3 : 4)
          : (HP >= 768 ? 2 : HP >= 512 ? GRP_WPE512 : 4);
 }
@@ -148,13 +149,110 @@ __host__ __device__ constexpr int grp_slab_bytes() {
     return grp_slab_tiles(HP / 16, NW) * 64 * 16 + 2 * NW * 16 * 4;   // tiles + LN reduction area
 }
 
-template <int HP, int ACT, bool LN, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(grp_waves_per_eu(HP, NW), 8)))
-void rollout_grp(const RolloutArgs a) {
-    constexpr int T = HP / 16;          // hidden tiles
+// One dense stack of the block, all layers fp32 MFMA.  Layer 0 reads its two
+// input tiles from registers (x0); hidden layers read the shared slab; each
+// wave owns TW = T/NW output tiles; the output layer (NOUT tiles) is K-split
+// over the group and its partial tiles are summed in fixed wave order.
+// Returns the pre-bias output tiles in every wave (tf.layers.dense adds the
+// bias after the matmul; the caller does that in its own precision).
+struct StackView {
+    const f4* const* w;         // packed layers 0..L (global)
+    const int32_t* wbytes;
+    const float* bias;          // LDS: [L][HPAD] hidden biases (output bias handled by the caller)
+    const float* const* lng;    // LN params (global, per hidden layer)
+    const float* const* lnb;
+    int L;
+    int hidden;                 // true width (LN statistics)
+};
+
+template <int T, int NW, int NOUT, int ACT, bool LN>
+__device__ __forceinline__ void group_mlp(const StackView& sv, f4 (&ring)[T / NW], const float (&x0)[2][4],
+                                          f4 (&o)[NOUT], f4* slab, float* red, int w, int lane) {
     constexpr int TW = T / NW;          // output tiles per wave
     constexpr int UO = T / NW;          // output-layer u-steps per wave
-    static_assert(T % NW == 0, "hidden tiles must split evenly over the group");
+    const int q = lane >> 4;
+    const int voff = lane * 16;
+    const int tile0 = w * TW;
+    // ---- layer 0 from registers: ring holds u-step 0 (prefetched by the caller) ----
+    const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(sv.w[0], sv.wbytes[0]);
+    f4 acc[TW];
+#pragma unroll
+    for (int j = 0; j < TW; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[j][r], x0[u][r], acc[j], 0, 0, 0);
+        if (u == 0) {
+#pragma unroll
+            for (int j = 0; j < TW; ++j) ring[j] = wload(rs0, voff, (w * 2 + 1) * TW * 1024 + j * 1024);
+        }
+    }
+    for (int l = 0; l < sv.L; ++l) {
+        if (l > 0) {
+            // ---- hidden layer l: [h -> h] from the slab ----
+#pragma unroll
+            for (int j = 0; j < TW; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
+            mm_slab<TW, (TW >= 16 ? 1 : 2)>(layer_rsrc(sv.w[l], sv.wbytes[l]), w * T * TW * 1024, 0, T, slab, acc,
+                                           lane);
+        }
+        // bias + activation (+ LN) in registers, then hand over through the slab
+        f4 v[TW];
+#pragma unroll
+        for (int j = 0; j < TW; ++j) v[j] = bias_act<ACT>(acc[j], sv.bias + l * T * 16, tile0 + j, q);
+        if constexpr (LN) group_layer_norm<TW, NW>(v, tile0, sv.lng[l], sv.lnb[l], sv.hidden, red, w, lane);
+        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // every wave is done reading the slab
+#pragma unroll
+        for (int j = 0; j < TW; ++j) slab[(tile0 + j) * 64 + lane] = v[j];
+        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // new activations visible
+    }
+    // ---- output layer: [h -> NOUT tiles], u split over the group ----
+    f4 po[NOUT];
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) po[k] = (f4){0.f, 0.f, 0.f, 0.f};
+    mm_slab<NOUT, (UO % 2 == 0) ? 2 : 1>(layer_rsrc(sv.w[sv.L], sv.wbytes[sv.L]), 0, w * UO, (w + 1) * UO, slab, po,
+                                         lane);
+    if constexpr (!GRP_DIAG_NOBAR) __syncthreads();       // done reading activations
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) slab[(NOUT * w + k) * 64 + lane] = po[k];
+    if constexpr (!GRP_DIAG_NOBAR) __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) o[k] = slab[k * 64 + lane];
+#pragma unroll
+    for (int g = 1; g < NW; ++g)                        // fixed summation order
+#pragma unroll
+        for (int k = 0; k < NOUT; ++k) o[k] += slab[(NOUT * g + k) * 64 + lane];
+}
+
+template <int T, int NW>
+__device__ __forceinline__ void prefetch_layer0(f4 (&ring)[T / NW], const f4* w0, int32_t bytes, int w, int lane) {
+    constexpr int TW = T / NW;
+    const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(w0, bytes);
+#pragma unroll
+    for (int j = 0; j < TW; ++j) ring[j] = wload(rs0, lane * 16, (w * 2 + 0) * TW * 1024 + j * 1024);
+}
+
+// Standard normal from two Philox uniforms (Box-Muller, f32): the stochastic
+// policy branch (DiagGaussianPd.sample = mean + std * N(0,1), ppo_bc_policy.py:85)
+__device__ __forceinline__ float rng_normal(uint64_t seed, uint64_t g, int h, int j) {
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)h, 0x80000000u | (uint32_t)j};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float u1 = ((float)(c[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
+    return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
+template <int HP, int ACT, bool LN, int NW, int PHP>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(grp_waves_per_eu(HP, NW, PHP), 8)))
+void rollout_grp(const RolloutArgs a) {
+    constexpr int T = HP / 16;          // hidden tiles of the dynamics MLP
+    constexpr int TW = T / NW;
+    constexpr int TP = PHP / 16;        // hidden tiles of the fused policy MLP (0: none)
+    constexpr int TPW = (TP > 0 ? TP : NW) / NW;
+    constexpr int TMAX = T > TP ? T : TP;
+    static_assert(T % NW == 0 && (TP == 0 || TP % NW == 0), "hidden tiles must split evenly over the group");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
@@ -165,16 +263,23 @@ void rollout_grp(const RolloutArgs a) {
     const bool valid = cand < a.K;
     const int S = a.S, A = a.A, L = a.L;
 
-    // ---- per-block parameters in LDS: consts (f64) + all biases ----
+    // ---- per-block parameters in LDS: consts (f64), biases, policy params ----
     double* C = reinterpret_cast<double*>(lds);
     float* Bl = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kConstRows * kConstCols * 8);
     for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
     for (int l = 0; l < L; ++l)
         for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i];
     for (int i = threadIdx.x; i < 32; i += blockDim.x) Bl[L * HP + i] = a.b[L][i];
-    f4* slab = reinterpret_cast<f4*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP));
-    float* red = reinterpret_cast<float*>(slab + grp_slab_tiles(T, NW) * 64);
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) slab[T * 64 + i] = (f4){0.f, 0.f, 0.f, 0.f};
+    float* Pb = Bl + L * HP + 32;                       // policy: [PL][PHP] hidden biases, then params
+    const int PL = a.pL;
+    if constexpr (TP > 0) {
+        for (int l = 0; l < PL; ++l)
+            for (int i = threadIdx.x; i < PHP; i += blockDim.x) Pb[l * PHP + i] = a.pb[l][i];
+        for (int i = threadIdx.x; i < kPolParams; i += blockDim.x) Pb[PL * PHP + i] = a.pparams[i];
+    }
+    f4* slab = reinterpret_cast<f4*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP) + pol_param_bytes(PL, PHP));
+    float* red = reinterpret_cast<float*>(slab + grp_slab_tiles(TMAX, NW) * 64);
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) slab[TMAX * 64 + i] = (f4){0.f, 0.f, 0.f, 0.f};
     if constexpr (GRP_STAGGER > 0) {            // de-phase co-resident groups (speed only)
         const int n = (blockIdx.x % 3) * GRP_STAGGER;
         for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
@@ -201,23 +306,68 @@ void rollout_grp(const RolloutArgs a) {
     }
     double cost = 0.0;   // trajectory_cost = 0 (cost_functions.py:60)
     const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
-    auto fetch_action = [&](int h, int i) -> double {
-        const int j = i - S;
-        if (!valid || i < S || j >= A) return 0.0;
+    // uniform draw j of step h: the caller's [H,K,A] array (np.random.uniform, controllers.py:53/191) or Philox
+    auto fetch_uniform = [&](int h, int j) -> double {
+        if (!valid) return 0.0;
         return a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
                          : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
     };
-    const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
-    const __amdgpu_buffer_rsrc_t rsL = layer_rsrc(a.w[L], a.wbytes[L]);
-    const int voff = lane * 16;
-    const int tile0 = w * TW;
+    const StackView dyn{a.w, a.wbytes, Bl, a.lng, a.lnb, L, a.hidden};
+    const StackView pol{a.pw, a.pwbytes, Pb, nullptr, nullptr, PL, PHP};
 
     for (int h = 0; h < a.H; ++h) {
-        // ---- layer-0 weights of u-step 0 first: they do not depend on the state ----
-        f4 ring[TW];
+        double pact[4];                                     // policy actions of rows 16+4q+r (tile 1)
 #pragma unroll
-        for (int j = 0; j < TW; ++j) ring[j] = wload(rs0, voff, (w * 2 + 0) * TW * 1024 + j * 1024);
+        for (int r = 0; r < 4; ++r) pact[r] = 0.0;
+        if constexpr (TP > 0) {
+            // ---- fused policy (ppo_bc_policy.py:54-88): obz = clip((f32(ob) - mean)/std, -5, 5) ----
+            f4 pring[TPW];
+            prefetch_layer0<TP, NW>(pring, a.pw[0], a.pwbytes[0], w, lane);
+            const float* pm = Pb + PL * PHP;                // [obmean 32][obstd 32][logstd 16][out bias 16]
+            float z0[2][4];
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int d = 16 * v + 4 * q + r;
+                    float z = 0.f;
+                    if (d < S) {
+                        z = ((float)s[v][r] - pm[d]) / pm[32 + d];
+                        z = fminf(fmaxf(z, -5.0f), 5.0f);
+                    }
+                    z0[v][r] = z;
+                }
+            f4 po[1];
+            group_mlp<TP, NW, 1, BCMPC_ACT_TANH, false>(pol, pring, z0, po, slab, red, w, lane);
+            // action rows i = S + j sit in tile 1 (host permutes the policy output rows there)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 + 4 * q + r;
+                const int j = i - S;
+                if (j >= 0 && j < A) {
+                    const float mean = po[0][r] + pm[80 + (i - 16)];          // dense bias (f32)
+                    if (a.pol_mode == BCMPC_POLICY_STOCHASTIC) {
+                        const float sd = expf(pm[64 + j]);
+                        pact[r] = (double)(mean + sd * rng_normal(a.seed ^ 0x9E3779B97F4A7C15ull, gcand, h, j));
+                    } else {
+                        // (1 - explore) * mean in f32 (NumPy keeps the f32 dtype), + explore * U in f64
+                        const float t1 = (float)(1.0 - a.explore) * mean;
+                        pact[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, fetch_uniform(h, j)));
+                    }
+                }
+            }
+            if (a.act_out && h < a.act_out_steps && valid && w == 0) {   // action_paths (controllers.py:213)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 + 4 * q + r - S;
+                    if (j >= 0 && j < A) a.act_out[((int64_t)h * a.K + cand) * A + j] = pact[r];
+                }
+            }
+        }
 
+        // ---- dynamics: layer-0 weights first (independent of the state) ----
+        f4 ring[TW];
+        prefetch_layer0<T, NW>(ring, a.w[0], a.wbytes[0], w, lane);
         // ---- normalise (dynamics.py:109-110), cast to f32 (TF feed) ----
         float x0[2][4];
 #pragma unroll
@@ -230,58 +380,13 @@ void rollout_grp(const RolloutArgs a) {
                     xv = (float)__ddiv_rn(__dsub_rn(s[v][r], C[0 * 32 + i]), C[1 * 32 + i]);
                 } else if (i < S + A) {
                     const int j = i - S;
-                    xv = (float)__ddiv_rn(__dsub_rn(fetch_action(h, i), C[2 * 32 + j]), C[3 * 32 + j]);
+                    const double av = (TP > 0 && v == 1) ? pact[r] : fetch_uniform(h, j);
+                    xv = (float)__ddiv_rn(__dsub_rn(av, C[2 * 32 + j]), C[3 * 32 + j]);
                 }
                 x0[v][r] = xv;
             }
-
-        // ---- layer 0: [S+A -> h], my TW tiles, two u-steps through the ring ----
-        f4 acc[TW];
-#pragma unroll
-        for (int j = 0; j < TW; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int j = 0; j < TW; ++j)
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[j][r], x0[u][r], acc[j], 0, 0, 0);
-            if (u == 0) {
-#pragma unroll
-                for (int j = 0; j < TW; ++j) ring[j] = wload(rs0, voff, (w * 2 + 1) * TW * 1024 + j * 1024);
-            }
-        }
-        for (int l = 0; l < L; ++l) {
-            if (l > 0) {
-                // ---- hidden layer l: [h -> h] from the slab ----
-#pragma unroll
-                for (int j = 0; j < TW; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
-                mm_slab<TW, (TW >= 16 ? 1 : 2)>(layer_rsrc(a.w[l], a.wbytes[l]), w * T * TW * 1024, 0, T, slab, acc, lane);
-            }
-            // bias + activation (+ LN) in registers, then hand over through the slab
-            f4 v[TW];
-#pragma unroll
-            for (int j = 0; j < TW; ++j) v[j] = bias_act<ACT>(acc[j], Bl + l * HP, tile0 + j, q);
-            if constexpr (LN) group_layer_norm<TW, NW>(v, tile0, a.lng[l], a.lnb[l], a.hidden, red, w, lane);
-            if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // every wave is done reading the slab
-#pragma unroll
-            for (int j = 0; j < TW; ++j) slab[(tile0 + j) * 64 + lane] = v[j];
-            if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // new activations visible
-        }
-
-        // ---- output layer: [h -> S], u split over the group ----
-        f4 po[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
-        mm_slab<2, (UO % 2 == 0) ? 2 : 1>(rsL, 0, w * UO, (w + 1) * UO, slab, po, lane);
-        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();       // done reading activations
-        slab[(2 * w + 0) * 64 + lane] = po[0];
-        slab[(2 * w + 1) * 64 + lane] = po[1];
-        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();
-        f4 o[2] = {slab[0 * 64 + lane], slab[1 * 64 + lane]};
-#pragma unroll
-        for (int k = 1; k < NW; ++k) {                // fixed summation order
-            o[0] += slab[(2 * k + 0) * 64 + lane];
-            o[1] += slab[(2 * k + 1) * 64 + lane];
-        }
+        f4 o[2];
+        group_mlp<T, NW, 2, ACT, LN>(dyn, ring, x0, o, slab, red, w, lane);
 
         // ---- cheetah penalties on the current state (cost_functions.py:16-26) ----
         double pen = 0.0;
@@ -323,51 +428,66 @@ void rollout_grp(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
-template <int HP, int ACT, bool LN, int NW>
+template <int HP, int ACT, bool LN, int NW, int PHP>
 static hipError_t launch_grp_t(const RolloutArgs& a, hipStream_t st) {
-    const size_t lds = (size_t)param_bytes(a.L, HP) + grp_slab_bytes<HP, NW>() + GRP_LDS_PAD;
+    constexpr int TMAX = (HP > PHP ? HP : PHP) / 16;
+    const size_t lds = (size_t)param_bytes(a.L, HP) + pol_param_bytes(a.pL, PHP) +
+                       (size_t)grp_slab_tiles(TMAX, NW) * 64 * 16 + 2 * NW * 16 * 4 + GRP_LDS_PAD;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)rollout_grp<HP, ACT, LN, NW>,
+        hipError_t e = hipFuncSetAttribute((const void*)rollout_grp<HP, ACT, LN, NW, PHP>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int64_t blocks = (a.K + 15) / 16;
-    hipLaunchKernelGGL((rollout_grp<HP, ACT, LN, NW>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
+    hipLaunchKernelGGL((rollout_grp<HP, ACT, LN, NW, PHP>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
     return hipGetLastError();
 }
 
-template <int HP, int NW>
+template <int HP, int NW, int PHP>
 static hipError_t launch_grp_act(const RolloutArgs& a, hipStream_t st) {
-    if (a.ln) return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, true, NW>(a, st)
-                                             : launch_grp_t<HP, BCMPC_ACT_TANH, true, NW>(a, st);
-    return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, false, NW>(a, st)
-                                   : launch_grp_t<HP, BCMPC_ACT_TANH, false, NW>(a, st);
+    if (a.ln) return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, true, NW, PHP>(a, st)
+                                             : launch_grp_t<HP, BCMPC_ACT_TANH, true, NW, PHP>(a, st);
+    return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, false, NW, PHP>(a, st)
+                                   : launch_grp_t<HP, BCMPC_ACT_TANH, false, NW, PHP>(a, st);
 }
 
 template <int NW>
 static hipError_t launch_grp_nw(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+    if (a.pL > 0) {   // fused policy: NW = 4 only, policy hidden padded to 128
+        if constexpr (NW == 4) {
+            if (a.phidden_padded != 128) return hipErrorInvalidValue;
+            switch (hidden_padded) {
+                case 128: return launch_grp_act<128, 4, 128>(a, st);
+                case 256: return launch_grp_act<256, 4, 128>(a, st);
+                case 512: return launch_grp_act<512, 4, 128>(a, st);
+                default: return hipErrorInvalidValue;
+            }
+        }
+        return hipErrorInvalidValue;
+    }
     switch (hidden_padded) {
         case 64:
-            if constexpr (NW <= 4) return launch_grp_act<64, NW>(a, st);
+            if constexpr (NW <= 4) return launch_grp_act<64, NW, 0>(a, st);
             return hipErrorInvalidValue;
-        case 128: return launch_grp_act<128, NW>(a, st);
-        case 256: return launch_grp_act<256, NW>(a, st);
-        case 512: return launch_grp_act<512, NW>(a, st);
+        case 128: return launch_grp_act<128, NW, 0>(a, st);
+        case 256: return launch_grp_act<256, NW, 0>(a, st);
+        case 512: return launch_grp_act<512, NW, 0>(a, st);
         case 768:
-            if constexpr (NW >= 4) return launch_grp_act<768, NW>(a, st);
+            if constexpr (NW >= 4) return launch_grp_act<768, NW, 0>(a, st);
             return hipErrorInvalidValue;
         case 1024:
-            if constexpr (NW >= 4) return launch_grp_act<1024, NW>(a, st);
+            if constexpr (NW >= 4) return launch_grp_act<1024, NW, 0>(a, st);
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }
 
-size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw) {
-    const int T = hidden_padded / 16;
-    return (size_t)param_bytes(n_layers, hidden_padded) + (size_t)grp_slab_tiles(T, nw) * 64 * 16 + 2 * nw * 16 * 4;
+size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_padded, int policy_layers) {
+    const int tmax = (hidden_padded > policy_hidden_padded ? hidden_padded : policy_hidden_padded) / 16;
+    return (size_t)param_bytes(n_layers, hidden_padded) + pol_param_bytes(policy_layers, policy_hidden_padded) +
+           (size_t)grp_slab_tiles(tmax, nw) * 64 * 16 + 2 * nw * 16 * 4;
 }
 
 hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st) {

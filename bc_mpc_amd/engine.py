@@ -41,6 +41,26 @@ class MLPSpec:
 
 
 @dataclass
+class PolicySpec:
+    """MlpPolicy 'pi/pol' stack (ppo_bc_policy.py:66-80): tanh dense layers then
+    'final' (no activation), TF layout [in, out]; the obfilter's f32 mean/std
+    (RunningMeanStd, ppo_bc_policy.py:57-60) and the DiagGaussian logstd (:79)."""
+    kernels: List[np.ndarray]
+    biases: List[np.ndarray]
+    ob_mean: np.ndarray
+    ob_std: np.ndarray
+    logstd: np.ndarray
+
+    @property
+    def n_layers(self) -> int:
+        return len(self.kernels) - 1
+
+    @property
+    def hidden(self) -> int:
+        return int(np.shape(self.kernels[0])[1])
+
+
+@dataclass
 class StepResult:
     best_index: int            # global candidate index (np.argmin semantics)
     best_cost: float
@@ -69,7 +89,8 @@ class RolloutEngine:
 
     def __init__(self, state_dim: int, action_dim: int, hidden: int, n_layers: int,
                  activation: str, layer_norm: bool, horizon: int, num_paths: int,
-                 device: int = 0, cost: str = "cheetah", kernel: Optional[str] = None):
+                 device: int = 0, cost: str = "cheetah", kernel: Optional[str] = None,
+                 policy_hidden: int = 0, policy_layers: int = 0, policy_mode: str = "explore"):
         self._lib = _lib.load()
         if activation not in _ACT:
             raise ValueError(f"unsupported activation {activation!r} (tanh | relu)")
@@ -86,6 +107,10 @@ class RolloutEngine:
         if kernel not in _lib.KERNELS:
             raise ValueError(f"unknown kernel {kernel!r}; one of {sorted(_lib.KERNELS)}")
         cfg.kernel = _lib.KERNELS[kernel]
+        if policy_mode not in _lib.POLICY_MODES:
+            raise ValueError(f"unknown policy_mode {policy_mode!r}")
+        cfg.policy_hidden, cfg.policy_layers = int(policy_hidden), int(policy_layers)
+        cfg.policy_mode = _lib.POLICY_MODES[policy_mode]
         h = ctypes.c_void_p()
         _lib.check(self._lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -93,6 +118,7 @@ class RolloutEngine:
         self.hidden, self.n_layers, self.activation = hidden, n_layers, activation
         self.layer_norm, self.horizon, self.num_paths = bool(layer_norm), horizon, num_paths
         self.device, self.cost = device, cost
+        self.policy_hidden, self.policy_layers, self.policy_mode = policy_hidden, policy_layers, policy_mode
         self._keep = []
 
     # ------------------------------------------------------------------ weights
@@ -131,6 +157,33 @@ class RolloutEngine:
         (w.mean_obs, w.std_obs, w.mean_action, w.std_action, w.mean_deltas, w.std_deltas) = [_dp(x) for x in stats]
         keep.append(stats)
         _lib.check(self._lib.bcmpc_set_weights(self._h, ctypes.byref(w), ctypes.c_uint64(version)))
+
+    def set_policy(self, spec: PolicySpec, explore: float, version: int) -> None:
+        """Policy weights of MPCcontrollerPolicyNet (controllers.py:160-178)."""
+        if spec.n_layers != self.policy_layers or spec.hidden != self.policy_hidden:
+            raise ValueError("policy shapes do not match the engine configuration")
+        S, A, ph = self.state_dim, self.action_dim, self.policy_hidden
+        ks = [_f32(k) for k in spec.kernels]
+        bs = [_f32(b) for b in spec.biases]
+        exp = [(S, ph)] + [(ph, ph)] * (self.policy_layers - 1) + [(ph, A)]
+        for k, b, e in zip(ks, bs, exp):
+            if k.shape != e or b.shape != (e[1],):
+                raise ValueError(f"policy kernel {k.shape}/bias {b.shape} != expected {e}")
+        vecs = [_f32(spec.ob_mean).reshape(-1), _f32(spec.ob_std).reshape(-1), _f32(spec.logstd).reshape(-1)]
+        if vecs[0].shape != (S,) or vecs[1].shape != (S,) or vecs[2].shape != (A,):
+            raise ValueError("policy ob_mean/ob_std must be (S,), logstd (A,)")
+        FP = ctypes.POINTER(ctypes.c_float)
+        karr = (FP * len(ks))(*[k.ctypes.data_as(FP) for k in ks])
+        barr = (FP * len(bs))(*[b.ctypes.data_as(FP) for b in bs])
+        p = _lib.Policy(karr, barr, vecs[0].ctypes.data_as(FP), vecs[1].ctypes.data_as(FP),
+                        vecs[2].ctypes.data_as(FP), float(explore))
+        _lib.check(self._lib.bcmpc_set_policy(self._h, ctypes.byref(p), ctypes.c_uint64(version)))
+
+    def first_actions(self) -> np.ndarray:
+        """Step-0 actions of every candidate of the last rollout (policy engines), [K, A] f64."""
+        out = np.empty((self.num_paths, self.action_dim), dtype=np.float64)
+        _lib.check(self._lib.bcmpc_first_actions(self._h, _dp(out)))
+        return out
 
     @property
     def weights_version(self) -> int:

@@ -34,6 +34,9 @@ WORKLOADS = {
     "cfg4_shard": dict(K=32768, H=20, hidden=500, L=2, act="tanh"),   # 262144 / 8 per GPU
     "cfg3_relu": dict(K=65536, H=20, hidden=500, L=2, act="relu"),    # diagnostic: no tanh
     "cfg5_pass": dict(K=65536, H=50, hidden=1024, L=3, act="tanh"),   # one random-shooting pass of cfg5
+    # MPCcontrollerPolicyNet (controllers.py:160-237) at cfg3 dims: 20->128->128->6 tanh policy fused per step,
+    # self_exp=False, explore=0.5 (train_mpc_ppo.py:36-37,178 defaults)
+    "cfg3_policy": dict(K=65536, H=20, hidden=500, L=2, act="tanh", policy=(128, 2), explore=0.5),
     "ppo_defaults": dict(K=400, H=7, hidden=256, L=2, act="relu"),
 }
 S_DIM, A_DIM = 20, 6
@@ -41,12 +44,17 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix, v_mfma_f32
 HBM_PEAK_GBS = 8000.0
 
 
-def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM):
-    """Algorithmic MLP FLOPs per candidate-step: 2*[(S+A)h + (L-1)h^2 + hS]."""
-    return 2 * ((S + A) * hidden + (L - 1) * hidden * hidden + hidden * S)
+def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None):
+    """Algorithmic MLP FLOPs per candidate-step: 2*[(S+A)h + (L-1)h^2 + hS]
+    (+ the policy stack 2*[S*ph + (PL-1)ph^2 + ph*A] when fused)."""
+    f = 2 * ((S + A) * hidden + (L - 1) * hidden * hidden + hidden * S)
+    if policy:
+        ph, pl = policy
+        f += 2 * (S * ph + (pl - 1) * ph * ph + ph * A)
+    return f
 
 
-def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net):
+def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5):
     """The oracle (NumPy restatement of the reference path, kind "port") timed on
     the host cores over a bounded sample of the same workload."""
     from oracle import mpc_oracle as orc
@@ -60,7 +68,11 @@ def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net):
     rs = np.random.RandomState(0)
     done, calls, t0 = 0, 0, time.perf_counter()
     while True:
-        orc.get_action(dyn, state, H, Ks, -np.ones(A_DIM), np.ones(A_DIM), rng=rs)
+        if pol is None:
+            orc.get_action(dyn, state, H, Ks, -np.ones(A_DIM), np.ones(A_DIM), rng=rs)
+        else:
+            orc.policy_get_action(dyn, orc.NumpyPolicy(orc.PolicyWeights(*pol)), state, H, Ks, -np.ones(A_DIM),
+                                  np.ones(A_DIM), explore, rng=rs)
         done += Ks * H
         calls += 1
         if time.perf_counter() - t0 >= budget_s:
@@ -102,7 +114,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from bc_mpc_amd import distributed as bdist
-    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
     import bc_mpc_amd._lib as L_
 
     wl = WORKLOADS[args.workload]
@@ -127,7 +139,25 @@ def main():
             mean_obs, std_obs, mean_d, std_d]
     state = mean_obs + 0.5 * std_obs * np.random.RandomState(11).standard_normal(S_DIM)
 
-    eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local)
+    policy = wl.get("policy")
+    pol_arrays = None
+    if policy:
+        ph, pl = policy
+        rp = np.random.RandomState(2024)
+        pdims = [S_DIM] + [ph] * pl + [A_DIM]
+        pks, pbs = [], []
+        for i in range(len(pdims) - 1):
+            k = rp.standard_normal((pdims[i], pdims[i + 1]))
+            k *= (1.0 if i < pl else 0.5) / np.sqrt(np.square(k).sum(axis=0, keepdims=True))   # normc init
+            pks.append(k.astype(np.float32))
+            pbs.append((0.05 * rp.standard_normal(pdims[i + 1])).astype(np.float32))
+        pol_arrays = (pks, pbs, mean_obs.astype(np.float32), (std_obs + 0.05).astype(np.float32),
+                      np.full(A_DIM, -0.5, np.float32))
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, policy_hidden=ph,
+                            policy_layers=pl, policy_mode="explore")
+        eng.set_policy(PolicySpec(*pol_arrays), wl["explore"], 1)
+    else:
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local)
     eng.set_weights(MLPSpec(kernels, biases, act), norm, 1)
     info = eng.info()
     kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
@@ -175,7 +205,7 @@ def main():
 
     total_cand_steps = K * world * H * args.steps
     value = total_cand_steps / elapsed
-    fpcs = flop_per_cand_step(hidden, L)
+    fpcs = flop_per_cand_step(hidden, L, policy=policy)
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
     achieved_tflops = K * H * fpcs / kern_avg_s / 1e12
     out = {
@@ -193,7 +223,8 @@ def main():
         "data": "synthetic (HalfCheetah dims s=20,a=6; random-init 2x500 tanh dynamics MLP; "
                 f"actions {'resident in HBM as [H,K,6] f64' if args.actions == 'hbm' else 'drawn in-kernel (Philox)'})",
         "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
-                               f"{L}x{hidden} {act}, fp32 MFMA, 1 RCCL all-gather min-loc per step",
+                               f"{L}x{hidden} {act}" + (f" + fused policy {policy[1]}x{policy[0]} tanh" if policy else "")
+                               + ", fp32 MFMA, 1 RCCL all-gather min-loc per step",
                    "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
                    "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
                    "collective": f"{backend} all_gather min-loc, {3 + A_DIM} f64 per rank per step" if world > 1
@@ -218,7 +249,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import mpc_oracle as orc
         w = orc.MLPWeights(kernels, biases, act)
-        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, f"{L}x{hidden} {act}")
+        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K,
+                                           f"{L}x{hidden} {act}" + (f" + policy {policy}" if policy else ""),
+                                           pol_arrays, wl.get("explore", 0.5))
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -60,6 +60,11 @@ typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")  
     BCMPC_KERNEL_GROUP8 = 4     /* 8 waves share 16 candidates (small K)                 */
 } bcmpc_kernel;
 
+typedef enum bcmpc_policy_mode {   /* MPCcontrollerPolicyNet.self_exp (controllers.py:201-208) */
+    BCMPC_POLICY_EXPLORE = 0,      /* self_exp=False: (1-explore)*mean + explore*U(low,high)   */
+    BCMPC_POLICY_STOCHASTIC = 1    /* self_exp=True: mean + exp(logstd)*N(0,1) (device Philox)  */
+} bcmpc_policy_mode;
+
 /* Replaces the constructor arguments of MPCcontroller (controllers.py:28-35)
  * plus the NNDynamicsModel shape (dynamics.py:8-19, build_network :54-62). */
 typedef struct bcmpc_config {
@@ -75,7 +80,10 @@ typedef struct bcmpc_config {
     int32_t precision;    /* bcmpc_precision                                       */
     int32_t device;       /* HIP device ordinal                                    */
     int32_t kernel;       /* bcmpc_kernel: 0 = auto                                */
-    int32_t reserved[7];  /* must be zero                                          */
+    int32_t policy_hidden;  /* 0: MPCcontroller; >0: MPCcontrollerPolicyNet policy width (hid_size) */
+    int32_t policy_layers;  /* policy hidden layers (num_hid_layers, train_mpc_ppo.py:178)         */
+    int32_t policy_mode;    /* bcmpc_policy_mode                                                   */
+    int32_t reserved[4];  /* must be zero                                          */
 } bcmpc_config;
 
 /* Replaces the state NNDynamicsModel holds: TF variables
@@ -101,6 +109,18 @@ typedef struct bcmpc_result {
     double first_action[BCMPC_MAX_ACTION];    /* action_paths[0, best_index, :]              */
 } bcmpc_result;
 
+/* Replaces the policy net MPCcontrollerPolicyNet consults each step
+ * (ppo_bc_policy.py:54-88): obz = clip((ob - ob_mean)/ob_std, -5, 5);
+ * tanh dense x policy_layers; mean = dense(., A); logstd.  Host pointers, copied. */
+typedef struct bcmpc_policy {
+    const float* const* kernels;   /* policy_layers+1 arrays [in,out] (pi/pol/fc1.., final) */
+    const float* const* biases;
+    const float* ob_mean;          /* S (RunningMeanStd.mean, f32)   */
+    const float* ob_std;           /* S (RunningMeanStd.std, f32)    */
+    const float* logstd;           /* A                              */
+    double explore;                /* MPCcontrollerPolicyNet.explore */
+} bcmpc_policy;
+
 typedef struct bcmpc_engine bcmpc_engine;
 
 int bcmpc_abi_version(void);
@@ -115,6 +135,9 @@ int bcmpc_destroy(bcmpc_engine* eng);
 int bcmpc_set_weights(bcmpc_engine* eng, const bcmpc_weights* w, uint64_t version);
 uint64_t bcmpc_weights_version(const bcmpc_engine* eng);
 
+/* Policy weights for MPCcontrollerPolicyNet engines (config.policy_hidden > 0). */
+int bcmpc_set_policy(bcmpc_engine* eng, const bcmpc_policy* p, uint64_t version);
+
 /* env.action_space.low / .high (controllers.py:53). Defaults: [-1, 1]^A. */
 int bcmpc_set_action_bounds(bcmpc_engine* eng, const double* low, const double* high);
 
@@ -128,6 +151,10 @@ int bcmpc_set_action_bounds(bcmpc_engine* eng, const double* low, const double* 
  *   costs_out: optional K doubles, per-candidate trajectory cost (cost_functions.py:59-63) */
 int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actions,
                      uint64_t seed, int64_t cand_offset, bcmpc_result* out, double* costs_out);
+
+/* Actions the last rollout actually used for step 0 (policy engines:
+ * action_paths[0] of controllers.py:233), copied to host K x A doubles. */
+int bcmpc_first_actions(bcmpc_engine* eng, double* out);
 
 /* Device-memory, asynchronous form (no host sync; graph-capturable).
  *   d_state      : device, S doubles, or [K, S] when state_stride == S (predict mode,

@@ -199,6 +199,96 @@ def get_action(dyn: NumpyDynamics, state, horizon: int, num_simulated_paths: int
 
 
 # ----------------------------------------------------------------------------
+# Policy-guided MPC (controllers.py:160-237) + the policy net (ppo_bc_policy.py)
+# ----------------------------------------------------------------------------
+@dataclass
+class PolicyWeights:
+    """MlpPolicy 'pi/pol' stack (ppo_bc_policy.py:66-80) + its obfilter.
+
+    kernels/biases: fc1..fcL (tanh) then 'final' (no activation), TF layout
+    [in, out]; ob_mean / ob_std: baselines RunningMeanStd.mean / .std as f32
+    (mean = f32(sum/count); std = sqrt(max(f32(sumsq/count) - mean^2, 1e-2)));
+    logstd: the DiagGaussian log-std variable (ppo_bc_policy.py:79)."""
+    kernels: List[np.ndarray]
+    biases: List[np.ndarray]
+    ob_mean: np.ndarray
+    ob_std: np.ndarray
+    logstd: np.ndarray
+
+    @property
+    def n_layers(self) -> int:
+        return len(self.kernels) - 1
+
+    @property
+    def hidden(self) -> int:
+        return int(self.kernels[0].shape[1])
+
+
+class NumpyPolicy:
+    """Duck-typed stand-in for ppo_bc_policy.MlpPolicy.act (ppo_bc_policy.py:174-185),
+    deterministic branch (``stochastic=False`` -> ``pd.mode()`` = the mean)."""
+
+    def __init__(self, w: PolicyWeights):
+        self.w = w
+
+    def mean(self, ob) -> np.ndarray:
+        ob = np.asarray(ob)
+        if ob.ndim == 1:
+            ob = ob[None]
+        x = ob.astype(np.float32)                                   # tf.float32 placeholder 'ob' (:28)
+        obz = np.clip((x - self.w.ob_mean) / self.w.ob_std, np.float32(-5.0), np.float32(5.0))   # :60
+        last = obz
+        for k, b in zip(self.w.kernels[:-1], self.w.biases[:-1]):  # :70-71
+            last = np.tanh(last @ k + b)
+        return (last @ self.w.kernels[-1] + self.w.biases[-1]).astype(np.float32)   # :72
+
+    def act(self, ob, stochastic=True):
+        if stochastic:
+            raise NotImplementedError("TF's random_normal stream is not reproducible outside TF")
+        return self.mean(ob), None
+
+
+def policy_get_action(dyn: NumpyDynamics, policy, state, horizon: int, num_simulated_paths: int,
+                      low, high, explore: float, cost_fn=cheetah_cost_fn, rng=None):
+    """MPCcontrollerPolicyNet.get_action with self_exp=False (controllers.py:189-237).
+    Returns ``(opt_action, argmin, costs)``."""
+    rng = np.random if rng is None else rng
+    exploration = rng.uniform(low=low, high=high, size=[horizon, num_simulated_paths, len(high)])   # :185
+    states = np.tile(state, [num_simulated_paths, 1])
+    states_paths_all, action_paths = [states], []
+    for i in range(horizon):
+        actions, _ = policy.act(states, stochastic=False)
+        actions = (1 - explore) * actions + explore * exploration[i, :, :]                             # :208
+        states = dyn.predict(states, actions)
+        states_paths_all.append(states)
+        action_paths.append(actions)
+    states_paths_all = np.asarray(states_paths_all)
+    action_paths = np.asarray(action_paths)
+    costs = trajectory_cost_fn(cost_fn, states_paths_all[:-1], action_paths, states_paths_all[1:])
+    i = int(np.argmin(costs))
+    return action_paths[:, i, :][0].copy(), i, costs
+
+
+def synthetic_policy(state_dim=20, action_dim=6, hidden=128, n_layers=2, seed=2024) -> PolicyWeights:
+    """MlpPolicy-shaped weights (normc-like init, ppo_bc_policy.py:63-72) and an obfilter."""
+    rs = np.random.RandomState(seed)
+    dims = [state_dim] + [hidden] * n_layers + [action_dim]
+    ks, bs = [], []
+    for i in range(len(dims) - 1):
+        k = rs.standard_normal((dims[i], dims[i + 1]))
+        k *= (1.0 if i < n_layers else 0.5) / np.sqrt(np.square(k).sum(axis=0, keepdims=True))
+        ks.append(k.astype(np.float32))
+        bs.append((0.05 * rs.standard_normal(dims[i + 1])).astype(np.float32))
+    count = 1000.0
+    mean64 = 0.1 * rs.standard_normal(state_dim)
+    sumsq = (np.square(mean64) + np.square(np.abs(rs.standard_normal(state_dim)) * 0.5 + 0.2)) * count
+    mean = (mean64 * count / count).astype(np.float32)
+    std = np.sqrt(np.maximum((sumsq / count).astype(np.float32) - np.square(mean), np.float32(1e-2)))
+    logstd = (-0.5 + 0.1 * rs.standard_normal(action_dim)).astype(np.float32)
+    return PolicyWeights(ks, bs, mean, std.astype(np.float32), logstd)
+
+
+# ----------------------------------------------------------------------------
 # Philox4x32-10 restatement of the engine's device RNG ("perf" action mode)
 # ----------------------------------------------------------------------------
 _PH_M0, _PH_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)

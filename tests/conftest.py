@@ -16,8 +16,10 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box with -m gpu)")
 
 
-def golden_names():
-    return sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+def golden_names(kind: str = "mpc"):
+    """Fixture names; kind "mpc" = MPCcontroller cases, "policy" = MPCcontrollerPolicyNet cases."""
+    names = sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+    return [n for n in names if n.startswith("policy_") == (kind == "policy")]
 
 
 class Golden:
@@ -47,6 +49,13 @@ class Golden:
         self.top2_gap = float(z["top2_gap"])
         self.low = -np.ones(self.A, dtype=np.float32)
         self.high = np.ones(self.A, dtype=np.float32)
+        self.policy = None
+        if m.get("policy"):
+            L = m["pl"]
+            self.policy = orc.PolicyWeights([z[f"PW{i}"] for i in range(L + 1)], [z[f"PB{i}"] for i in range(L + 1)],
+                                            z["P_ob_mean"], z["P_ob_std"], z["P_logstd"])
+            ref = orc.synthetic_policy(self.S, self.A, m["ph"], L, seed=m["policy_seed"])
+            assert all(np.array_equal(a, b) for a, b in zip(ref.kernels, self.policy.kernels))
 
     def actions(self):
         """The [H, K, A] action tensor the reference consumed (regenerated, then re-injected)."""
@@ -71,6 +80,11 @@ class Golden:
         return orc.NumpyDynamics(self.weights, self.norm)
 
 
-@pytest.fixture(params=golden_names())
+@pytest.fixture(params=golden_names("mpc"))
 def golden(request):
+    return Golden(request.param)
+
+
+@pytest.fixture(params=golden_names("policy"))
+def golden_policy(request):
     return Golden(request.param)

@@ -189,6 +189,73 @@ def run_case(c):
     return out
 
 
+POLICY_CASES = [
+    dict(name="policy_explore05_relu_ln", K=256, H=6, hidden=256, L=2, act="relu", ln=True, seed=21, explore=0.5,
+         ph=128, pl=2),
+    dict(name="policy_explore03_tanh", K=128, H=5, hidden=500, L=2, act="tanh", ln=False, seed=22, explore=0.3,
+         ph=128, pl=2),
+    dict(name="policy_explore0_pure", K=64, H=4, hidden=128, L=2, act="relu", ln=False, seed=23, explore=0.0,
+         ph=64, pl=1),
+    dict(name="policy_explore1_pure_expl", K=96, H=4, hidden=256, L=2, act="tanh", ln=False, seed=24, explore=1.0,
+         ph=128, pl=2),
+]
+
+
+def run_policy_case(c):
+    """controllers.MPCcontrollerPolicyNet (controllers.py:160-237), self_exp=False."""
+    S, A = 20, 6
+    w = orc.synthetic_weights(S, A, c["hidden"], c["L"], c["act"], c["ln"], seed_base=1000 + 17 * c["seed"])
+    norm = orc.synthetic_normalization(S, A, seed=7 + c["seed"])
+    state = orc.synthetic_state(norm, seed=11 + c["seed"])
+    pw = orc.synthetic_policy(S, A, c["ph"], c["pl"], seed=500 + c["seed"])
+    dyn, pol = orc.NumpyDynamics(w, norm), orc.NumpyPolicy(pw)
+    env = FakeEnv(S, A)
+    ctrl = ref_controllers.MPCcontrollerPolicyNet(env=env, dyn_model=dyn, policy_net=pol, explore=c["explore"],
+                                                  self_exp=False, horizon=c["H"], cost_fn=ref_costs.cheetah_cost_fn,
+                                                  num_simulated_paths=c["K"])
+    captured = {}
+    orig_traj = ref_controllers.trajectory_cost_fn
+
+    def traj_wrapper(cost_fn, states, actions, next_states):
+        out = orig_traj(cost_fn, states, actions, next_states)
+        captured["costs"] = np.array(out, dtype=np.float64, copy=True)
+        captured["states"] = np.concatenate([states, next_states[-1:]], axis=0)
+        captured["actions"] = np.array(actions, copy=True)
+        return out
+
+    ref_controllers.trajectory_cost_fn = traj_wrapper
+    try:
+        np.random.seed(c["seed"])
+        opt_action = ctrl.get_action(state)
+        next_draw = np.random.random()
+    finally:
+        ref_controllers.trajectory_cost_fn = orig_traj
+    costs = captured["costs"]
+    order = np.sort(costs[~np.isnan(costs)])
+    np.random.seed(c["seed"])
+    a2, i2, c2 = orc.policy_get_action(dyn, pol, state, c["H"], c["K"], env.action_space.low,
+                                       env.action_space.high, c["explore"])
+    assert np.array_equal(c2, costs) and np.array_equal(a2, opt_action), c["name"]   # restatement is exact
+    out = dict(
+        meta=json.dumps(dict(c, S=S, A=A, weight_digest=w.digest(), weight_seed_base=1000 + 17 * c["seed"],
+                             norm_seed=7 + c["seed"], state_seed=11 + c["seed"], policy_seed=500 + c["seed"],
+                             policy=True)),
+        state=state, mean_obs=norm[0], std_obs=norm[1], mean_action=norm[2], std_action=norm[3],
+        mean_deltas=norm[8], std_deltas=norm[9],
+        costs=costs, argmin=np.int64(np.argmin(costs)), opt_action=np.asarray(opt_action, dtype=np.float64),
+        top2_gap=np.float64(order[1] - order[0]), near_threshold=orc.near_threshold_mask(captured["states"]),
+        next_draw=np.float64(next_draw),
+        first_actions=captured["actions"][0],
+        action_digest=np.frombuffer(
+            __import__("hashlib").sha256(np.ascontiguousarray(captured["actions"]).tobytes()).digest(), dtype=np.uint8),
+    )
+    for i, k in enumerate(pw.kernels):
+        out[f"PW{i}"] = k
+        out[f"PB{i}"] = pw.biases[i]
+    out["P_ob_mean"], out["P_ob_std"], out["P_logstd"] = pw.ob_mean, pw.ob_std, pw.logstd
+    return out
+
+
 def main():
     note = try_trained_weights()
     print("vars.pkl:", note)
@@ -197,7 +264,15 @@ def main():
                        reference_files=["controllers.py", "cost_functions.py"],
                        dynamics="oracle.NumpyDynamics (TF1 absent; restatement of dynamics.py:54-71,106-119)",
                        numpy=np.__version__, trained_weights=note,
-                       cases=[c["name"] for c in CASES]), f, indent=1)
+                       cases=[c["name"] for c in CASES] + [c["name"] for c in POLICY_CASES],
+                       policy_cases="controllers.MPCcontrollerPolicyNet with oracle.NumpyPolicy (MlpPolicy.act "
+                                    "deterministic branch, ppo_bc_policy.py:54-88,174-185; TF/baselines absent)"),
+                  f, indent=1)
+    for c in POLICY_CASES:
+        out = run_policy_case(c)
+        np.savez_compressed(os.path.join(HERE, f"{c['name']}.npz"), **out)
+        print(f"{c['name']:32s} K={c['K']:5d} H={c['H']:3d} argmin={int(out['argmin']):5d} "
+              f"gap={float(out['top2_gap']):.4g} near={int(out['near_threshold'].sum())}")
     for c in CASES:
         out = run_case(c)
         np.savez_compressed(os.path.join(HERE, f"{c['name']}.npz"), **out)

@@ -59,7 +59,7 @@ def argmin_is_decidable(g: Golden) -> bool:
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("name", golden_names("mpc"))
 def test_engine_matches_reference_fixture(name, kernel):
     g = Golden(name)
     if kernel == "group8" and g.meta["hidden"] <= 64:
@@ -269,3 +269,88 @@ def test_large_hidden_vs_oracle(hidden, L, act, ln, kernel):
     want, states = orc.rollout(orc.NumpyDynamics(w, norm), state, acts)
     assert_costs_close(res.costs, want, orc.near_threshold_mask(states), f"h{hidden}xL{L}/{kernel}")
     assert res.best_index == int(np.argmin(res.costs))
+
+
+def _policy_env(g):
+    class Box:
+        low, high = g.low, g.high
+        shape = (g.A,)
+
+    class Env:
+        action_space = Box()
+
+        class observation_space:
+            shape = (g.S,)
+    return Env()
+
+
+@pytest.mark.parametrize("name", golden_names("policy"))
+def test_policy_engine_matches_reference_fixture(name):
+    """MPCcontrollerPolicyNet (self_exp=False) fused into the group kernel vs the reference run."""
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    g = Golden(name)
+    w, p = g.weights, g.policy
+    eng = RolloutEngine(g.S, g.A, w.hidden, w.n_layers, w.activation, w.layer_norm, g.H, g.K,
+                        policy_hidden=p.hidden, policy_layers=p.n_layers, policy_mode="explore")
+    eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), g.norm, 1)
+    eng.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), g.meta["explore"], 1)
+    rs = np.random.RandomState(g.meta["seed"])
+    expl = rs.uniform(g.low, g.high, size=[g.H, g.K, g.A])
+    res = eng.get_action(g.state, expl, return_costs=True)
+    assert_costs_close(res.costs, g.costs, g.near, f"{name}")
+    fa = eng.first_actions()
+    err = np.abs(fa - g.z["first_actions"])
+    print(f"[{name}] max|dfirst_action|={err.max():.3e}")
+    assert (err <= 1e-6).all()
+    assert res.best_index == int(np.argmin(res.costs))
+    if argmin_is_decidable(g):
+        assert res.best_index == g.argmin
+        assert np.allclose(res.first_action, g.opt_action, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", golden_names("policy"))
+def test_policy_controller_dropin(name):
+    from bc_mpc_amd import MPCcontrollerPolicyNet, cheetah_cost_fn
+    from oracle import mpc_oracle as orc
+    g = Golden(name)
+    ctrl = MPCcontrollerPolicyNet(_policy_env(g), g.dyn(), orc.NumpyPolicy(g.policy), explore=g.meta["explore"],
+                                  self_exp=False, horizon=g.H, cost_fn=cheetah_cost_fn, num_simulated_paths=g.K)
+    np.random.seed(g.meta["seed"])
+    a = ctrl.get_action(g.state)
+    assert a.dtype == np.float64 and a.shape == (g.A,)
+    if argmin_is_decidable(g):
+        assert np.allclose(a, g.opt_action, rtol=0, atol=1e-6)
+    assert np.random.random() == float(g.z["next_draw"])        # same RNG side effect as the reference
+
+
+def test_policy_stochastic_mode_is_deterministic_and_shard_invariant():
+    """self_exp=True: mean + exp(logstd) N(0,1) with device Philox normals."""
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    K, H = 512, 6
+    w = orc.synthetic_weights(20, 6, 256, 2, "relu", False)
+    p = orc.synthetic_policy(20, 6, 128, 2)
+    norm = orc.synthetic_normalization()
+    state = orc.synthetic_state(norm)
+    expl = np.random.RandomState(0).uniform(-1, 1, (H, K, 6))
+
+    def mk(k):
+        e = RolloutEngine(20, 6, 256, 2, "relu", False, H, k, policy_hidden=128, policy_layers=2,
+                          policy_mode="stochastic")
+        e.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+        e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.5, 1)
+        return e
+    full = mk(K)
+    r1 = full.get_action(state, expl, seed=42, return_costs=True)
+    a1 = full.first_actions()
+    r2 = full.get_action(state, expl, seed=42, return_costs=True)
+    assert np.array_equal(r1.costs, r2.costs)
+    half = mk(K // 2)
+    ra = half.get_action(state, np.ascontiguousarray(expl[:, :K // 2]), seed=42, cand_offset=0, return_costs=True)
+    rb = half.get_action(state, np.ascontiguousarray(expl[:, K // 2:]), seed=42, cand_offset=K // 2,
+                         return_costs=True)
+    assert np.array_equal(np.concatenate([ra.costs, rb.costs]), r1.costs)
+    # step-0 actions are mean + std * z with z ~ N(0,1): standardised residuals look normal
+    mean = orc.NumpyPolicy(p).mean(np.tile(state, [K, 1])).astype(np.float64)
+    z = (a1 - mean) / np.exp(p.logstd.astype(np.float64))
+    assert abs(z.mean()) < 0.1 and abs(z.std() - 1.0) < 0.1

@@ -68,3 +68,14 @@ def test_cost_scalar_and_batched_branches_agree():
     batched = orc.cheetah_cost_fn(s, None, ns)
     scalar = np.array([orc.cheetah_cost_fn(s[i], None, ns[i]) for i in range(16)])
     assert np.array_equal(batched, scalar)
+
+
+def test_oracle_policy_controller_reproduces_reference(golden_policy):
+    """MPCcontrollerPolicyNet (controllers.py:189-237) restated, vs the reference run."""
+    g = golden_policy
+    np.random.seed(g.meta["seed"])
+    a, i, costs = orc.policy_get_action(g.dyn(), orc.NumpyPolicy(g.policy), g.state, g.H, g.K, g.low, g.high,
+                                        g.meta["explore"])
+    assert np.array_equal(costs, g.costs)
+    assert i == g.argmin and np.array_equal(a, g.opt_action)
+    assert np.random.random() == float(g.z["next_draw"])
