@@ -18,6 +18,10 @@ It is a NumPy restatement of the reference path, function by function:
 * ``cheetah_cost_fn``         <- ``cost_functions.py:9-52``.
 * ``trajectory_cost_fn``      <- ``cost_functions.py:59-63``.
 * ``get_action``              <- ``controllers.py:43-88`` (MPCcontroller).
+* ``policy_get_action``       <- ``controllers.py:160-237`` (MPCcontrollerPolicyNet, self_exp=False).
+* ``NumpyRewardDynamics``     <- ``dynamics.py:121-238`` (NNDynamicsRewardModel two-head net).
+* ``reward_get_action``       <- ``controllers.py:90-158`` (MPCcontrollerReward, argmax).
+* ``policy_reward_get_action``<- ``controllers.py:289-363`` (MPCcontrollerPolicyNetReward).
 
 Parity status: the controller / cost / RNG half is PINNED bit-exactly against
 fixtures produced by running the reference's own ``controllers.py`` +
@@ -289,6 +293,152 @@ def synthetic_policy(state_dim=20, action_dim=6, hidden=128, n_layers=2, seed=20
 
 
 # ----------------------------------------------------------------------------
+# Learned-reward MPC: NNDynamicsRewardModel (dynamics.py:121-238) +
+# MPCcontrollerReward (controllers.py:90-158) / MPCcontrollerPolicyNetReward
+# (controllers.py:289-363)
+# ----------------------------------------------------------------------------
+@dataclass
+class RewardMLPWeights:
+    """Two-head net of ``NNDynamicsRewardModel.build_network`` (dynamics.py:150-177),
+    in TF variable-creation order:
+
+    kernels/biases: ``dense`` (shared trunk, [S+A, h]), ``dense_1`` (delta hidden,
+    [h, h]), ``dense_2`` (delta out, [h, S]), ``dense_3`` (reward hidden, [h, h]),
+    ``dense_4`` (reward out, [h, 1]); tanh on every hidden layer (the default
+    ``activation=tf.tanh``, dynamics.py:150).  ln_gamma/ln_beta (FLAGS.LAYER_NORM):
+    ``LayerNorm`` (trunk), ``LayerNorm_1`` (delta head), ``LayerNorm_2`` (reward head).
+    """
+    kernels: List[np.ndarray]
+    biases: List[np.ndarray]
+    ln_gamma: Optional[List[np.ndarray]] = None
+    ln_beta: Optional[List[np.ndarray]] = None
+    activation: str = "tanh"
+
+    @property
+    def hidden(self) -> int:
+        return int(self.kernels[0].shape[1])
+
+    @property
+    def layer_norm(self) -> bool:
+        return self.ln_gamma is not None
+
+    def digest(self) -> str:
+        h = hashlib.sha256()
+        for a in list(self.kernels) + list(self.biases) + list(self.ln_gamma or []) + list(self.ln_beta or []):
+            h.update(np.ascontiguousarray(a, dtype=np.float32).tobytes())
+        h.update(b"reward")
+        return h.hexdigest()
+
+
+class NumpyRewardDynamics(NumpyDynamics):
+    """Duck-typed stand-in for ``dynamics.NNDynamicsRewardModel`` (dynamics.py:121-238):
+    ``predict(s, a) -> (next_state [K,S] f64, reward [K,1] f64)``."""
+
+    def __init__(self, weights: RewardMLPWeights, normalization: Sequence[np.ndarray]):
+        super().__init__(weights, normalization)   # same 10-tuple order (dynamics.py:143)
+
+    # dynamics.py:150-177 (LAYER_NORM branch :153-166, plain branch :167-174)
+    def mlp(self, x32: np.ndarray):
+        w = self.weights
+        ln = w.layer_norm
+
+        def dense_act(x, i, ln_i):
+            y = np.tanh(x @ w.kernels[i] + w.biases[i])
+            return layer_norm_tf1(y, w.ln_gamma[ln_i], w.ln_beta[ln_i]) if ln else y
+
+        share = dense_act(x32, 0, 0)
+        d = dense_act(share, 1, 1)
+        d = (d @ w.kernels[2] + w.biases[2]).astype(np.float32, copy=False)
+        r = dense_act(share, 3, 2)
+        r = (r @ w.kernels[4] + w.biases[4]).astype(np.float32, copy=False)
+        return d, r
+
+    # dynamics.py:225-238
+    def predict(self, unnormalized_state, unnormalized_action):
+        normalized_state = (unnormalized_state - self.mean_obs) / (self.std_obs + NORM_EPS)
+        normalized_action = (unnormalized_action - self.mean_action) / (self.std_action + NORM_EPS)
+        x = np.concatenate([np.asarray(normalized_state).astype(np.float32),
+                            np.asarray(normalized_action).astype(np.float32)], axis=1)
+        normalized_state_delta, normalized_reward = self.mlp(x)
+        unnormalized_state_delta = (normalized_state_delta * self.std_deltas) + self.mean_deltas   # denomalize :78
+        unnormalized_nxt_state = unnormalized_state + unnormalized_state_delta
+        unnormalized_reward = (normalized_reward * self.std_reward) + self.mean_reward
+        return unnormalized_nxt_state, unnormalized_reward
+
+
+def reward_rollout(dyn: NumpyRewardDynamics, state, action_paths, gamma: float = 1.0):
+    """Body of ``MPCcontrollerReward.get_action`` after sampling (controllers.py:131-152).
+    Returns ``(rewards[K] f64, states_paths_all[H+1, K, S])``; the sum over steps is
+    NumPy's axis-0 reduction (sequential in h)."""
+    H, K, _ = action_paths.shape
+    states = np.tile(state, [K, 1])
+    paths, rewards_all = [states], []
+    for i in range(H):
+        states, reward = dyn.predict(states, action_paths[i, :, :])
+        paths.append(states)
+        rewards_all.append(reward * gamma ** i)
+    rewards_all = np.sum(np.asarray(rewards_all), axis=0).reshape([-1])
+    return rewards_all, np.asarray(paths)
+
+
+def env_sample_actions(sample, horizon: int, num_simulated_paths: int) -> np.ndarray:
+    """``MPCcontrollerReward.sample_random_actions`` (controllers.py:108-119): K*H calls
+    of ``env.action_space.sample()`` (n-major), reshaped to ``[H, K, A]``."""
+    actions = [sample() for _ in range(num_simulated_paths) for _ in range(horizon)]
+    return np.reshape(np.asarray(actions), [horizon, num_simulated_paths, -1])
+
+
+def reward_get_action(dyn: NumpyRewardDynamics, sample, state, horizon: int, num_simulated_paths: int,
+                      gamma: float = 1.0):
+    """``MPCcontrollerReward.get_action`` (controllers.py:121-158): argmax of the
+    discounted predicted reward.  Returns ``(opt_action, argmax, rewards, action_paths)``."""
+    action_paths = env_sample_actions(sample, horizon, num_simulated_paths)
+    rewards, _ = reward_rollout(dyn, state, action_paths, gamma)
+    i = int(np.argmax(rewards))
+    return action_paths[:, i, :][0].copy(), i, rewards, action_paths
+
+
+def policy_reward_get_action(dyn: NumpyRewardDynamics, policy, state, horizon: int, num_simulated_paths: int,
+                             low, high, explore: float, rng=None):
+    """``MPCcontrollerPolicyNetReward.get_action`` with self_exp=False (controllers.py:318-363):
+    undiscounted reward sum, argmax.  Returns ``(opt_action, argmax, rewards, action_paths)``."""
+    rng = np.random if rng is None else rng
+    exploration = rng.uniform(low=low, high=high, size=[horizon, num_simulated_paths, len(high)])   # :314
+    states = np.tile(state, [num_simulated_paths, 1])
+    rewards_all, action_paths = [], []
+    for i in range(horizon):
+        actions, _ = policy.act(states, stochastic=False)
+        actions = (1 - explore) * actions + explore * exploration[i, :, :]                             # :338
+        states, reward = dyn.predict(states, actions)
+        action_paths.append(actions)
+        rewards_all.append(reward)
+    action_paths = np.asarray(action_paths)
+    rewards = np.sum(np.asarray(rewards_all), axis=0).reshape([-1])
+    i = int(np.argmax(rewards))
+    return action_paths[:, i, :][0].copy(), i, rewards, action_paths
+
+
+def synthetic_reward_weights(state_dim=20, action_dim=6, hidden=500, layer_norm=False,
+                             seed_base=3000) -> RewardMLPWeights:
+    """Glorot-uniform kernels of the two-head net (TF default initializer), biases
+    ~ 0.1 N(0,1); LN gamma ~ 1 + 0.1 N, beta ~ 0.1 N."""
+    S, A, h = state_dim, action_dim, hidden
+    dims = [(S + A, h), (h, h), (h, S), (h, h), (h, 1)]
+    ks, bs = [], []
+    for i, (fi, fo) in enumerate(dims):
+        rs = np.random.RandomState(seed_base + i)
+        lim = np.sqrt(6.0 / (fi + fo))
+        ks.append(rs.uniform(-lim, lim, size=(fi, fo)).astype(np.float32))
+        bs.append((0.1 * rs.standard_normal(fo)).astype(np.float32))
+    gs = bts = None
+    if layer_norm:
+        rs = np.random.RandomState(seed_base + 99)
+        gs = [(1.0 + 0.1 * rs.standard_normal(h)).astype(np.float32) for _ in range(3)]
+        bts = [(0.1 * rs.standard_normal(h)).astype(np.float32) for _ in range(3)]
+    return RewardMLPWeights(ks, bs, gs, bts)
+
+
+# ----------------------------------------------------------------------------
 # Philox4x32-10 restatement of the engine's device RNG ("perf" action mode)
 # ----------------------------------------------------------------------------
 _PH_M0, _PH_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
@@ -362,8 +512,9 @@ def synthetic_weights(state_dim=20, action_dim=6, hidden=500, n_layers=2,
     return MLPWeights(ks, bs, activation, gs if layer_norm else None, bts if layer_norm else None)
 
 
-def synthetic_normalization(state_dim=20, action_dim=6, seed=7):
-    """The 10-tuple of utils.compute_normalization (utils.py:132-158), synthetic."""
+def synthetic_normalization(state_dim=20, action_dim=6, seed=7, reward=False):
+    """The 10-tuple of utils.compute_normalization (utils.py:132-158), synthetic.
+    ``reward=True`` also fills mean_reward / std_reward (shape (1,), utils.py:145,153)."""
     rs = np.random.RandomState(seed)
     mean_obs = 0.1 * rs.standard_normal(state_dim)
     std_obs = np.abs(rs.standard_normal(state_dim)) * 0.5 + 0.2
@@ -371,8 +522,11 @@ def synthetic_normalization(state_dim=20, action_dim=6, seed=7):
     std_action = np.full(action_dim, 1.0 / np.sqrt(3.0))
     mean_deltas = 0.005 * rs.standard_normal(state_dim)
     std_deltas = 0.05 * (np.abs(rs.standard_normal(state_dim)) + 0.2)
-    zeros1 = np.zeros(1)
-    return [mean_obs, std_obs, mean_action, std_action, zeros1, zeros1.copy(),
+    mean_reward, std_reward = np.zeros(1), np.zeros(1)
+    if reward:
+        mean_reward = 0.3 * rs.standard_normal(1)
+        std_reward = np.abs(rs.standard_normal(1)) + 0.5
+    return [mean_obs, std_obs, mean_action, std_action, mean_reward, std_reward,
             mean_obs.copy(), std_obs.copy(), mean_deltas, std_deltas]
 
 

@@ -16,10 +16,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box with -m gpu)")
 
 
+_KIND_PREFIX = {"policy": ("policy_",), "reward": ("reward_", "polrew_")}
+
+
 def golden_names(kind: str = "mpc"):
-    """Fixture names; kind "mpc" = MPCcontroller cases, "policy" = MPCcontrollerPolicyNet cases."""
+    """Fixture names; kind "mpc" = MPCcontroller cases, "policy" = MPCcontrollerPolicyNet cases,
+    "reward" = MPCcontrollerReward (reward_*) + MPCcontrollerPolicyNetReward (polrew_*) cases."""
     names = sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
-    return [n for n in names if n.startswith("policy_") == (kind == "policy")]
+    if kind == "mpc":
+        special = tuple(p for v in _KIND_PREFIX.values() for p in v)
+        return [n for n in names if not n.startswith(special)]
+    return [n for n in names if n.startswith(_KIND_PREFIX[kind])]
 
 
 class Golden:
@@ -78,6 +85,66 @@ class Golden:
     def dyn(self):
         from oracle import mpc_oracle as orc
         return orc.NumpyDynamics(self.weights, self.norm)
+
+
+class RewardGolden:
+    """A learned-reward fixture (tests/golden/gen_golden.py REWARD_CASES / POLICY_REWARD_CASES)."""
+
+    def __init__(self, name):
+        from oracle import mpc_oracle as orc
+        self.name = name
+        z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+        self.z = z
+        self.meta = m = json.loads(str(z["meta"]))
+        self.K, self.H, self.S, self.A = m["K"], m["H"], m["S"], m["A"]
+        self.weights = orc.synthetic_reward_weights(self.S, self.A, m["hidden"], m["ln"],
+                                                    seed_base=m["weight_seed_base"])
+        assert self.weights.digest() == m["weight_digest"], "synthetic reward-net generator drifted"
+        if "W0" in z.files:
+            for i, k in enumerate(self.weights.kernels):
+                assert np.array_equal(z[f"W{i}"], k)
+        self.norm = orc.synthetic_normalization(self.S, self.A, seed=m["norm_seed"], reward=True)
+        assert np.array_equal(self.norm[4], z["mean_reward"]) and np.array_equal(self.norm[5], z["std_reward"])
+        self.state = z["state"]
+        self.rewards = z["rewards"]
+        self.argmax = int(z["argmax"])
+        self.opt_action = z["opt_action"]
+        self.top2_gap = float(z["top2_gap"])
+        self.gamma = float(m.get("gamma", 1.0))
+        self.explore = m.get("explore")
+        self.low = -np.ones(self.A, dtype=np.float32)
+        self.high = np.ones(self.A, dtype=np.float32)
+        self.policy = None
+        if m.get("policy"):
+            L = m["pl"]
+            self.policy = orc.PolicyWeights([z[f"PW{i}"] for i in range(L + 1)], [z[f"PB{i}"] for i in range(L + 1)],
+                                            z["P_ob_mean"], z["P_ob_std"], z["P_logstd"])
+
+    def env_actions(self):
+        """The [H, K, A] actions the reference's env.action_space.sample() calls produced (float32 Box)."""
+        from oracle import mpc_oracle as orc
+        m = self.meta
+        if m.get("inject") == "philox":
+            return orc.device_rng_actions(m["rng_seed"], m["cand_offset"], self.K, self.H, self.low, self.high)
+        ap = np.random.RandomState(m["seed"]).uniform(-1, 1, size=(self.K * self.H, self.A)).astype(np.float32)
+        ap = ap.reshape(self.H, self.K, self.A)
+        if m.get("inject") == "tie":
+            lo, best = (int(x) for x in self.z["tie_pair"])
+            ap[:, lo, :] = ap[:, best, :]
+            ap[:, min(self.K - 1, best + 5), :] = ap[:, best, :]
+        elif m.get("inject") == "nan":
+            ap[1, 21, 2] = np.nan
+            ap[0, 40, 5] = np.nan
+        return ap
+
+    def dyn(self):
+        from oracle import mpc_oracle as orc
+        return orc.NumpyRewardDynamics(self.weights, self.norm)
+
+
+@pytest.fixture(params=golden_names("reward"))
+def golden_reward(request):
+    return RewardGolden(request.param)
 
 
 @pytest.fixture(params=golden_names("mpc"))

@@ -55,6 +55,12 @@ class _Box:
         self.low = np.asarray(low, dtype=np.float32)
         self.high = np.asarray(high, dtype=np.float32)
         self.shape = self.low.shape
+        self.np_random = np.random.RandomState(0)
+
+    def sample(self):
+        """gym.spaces.Box.sample (float32 Box): uniform(low, high) from the space's
+        own RandomState, cast to the space dtype."""
+        return self.np_random.uniform(low=self.low, high=self.high, size=self.shape).astype(np.float32)
 
 
 class FakeEnv:
@@ -256,6 +262,162 @@ def run_policy_case(c):
     return out
 
 
+REWARD_CASES = [
+    # MPCcontrollerReward (controllers.py:90-158) on NNDynamicsRewardModel (dynamics.py:121-238)
+    dict(name="reward_tiny_g1", K=16, H=3, hidden=64, ln=False, seed=41, gamma=1.0),
+    dict(name="reward_small_ln_g09", K=128, H=5, hidden=128, ln=True, seed=42, gamma=0.9),
+    dict(name="reward_500_g099", K=512, H=10, hidden=500, ln=False, seed=43, gamma=0.99),
+    dict(name="reward_500_ln", K=256, H=6, hidden=500, ln=True, seed=44, gamma=1.0),
+    dict(name="reward_tie_lower_index", K=96, H=4, hidden=64, ln=False, seed=45, gamma=0.95, inject="tie"),
+    dict(name="reward_nan_candidates", K=64, H=3, hidden=64, ln=False, seed=46, gamma=1.0, inject="nan"),
+    dict(name="reward_ragged_k1", K=1, H=2, hidden=64, ln=True, seed=47, gamma=0.5),
+    dict(name="reward_device_rng", K=300, H=7, hidden=500, ln=False, seed=48, gamma=0.97, inject="philox",
+         rng_seed=0xBEEF_0042, cand_offset=77),
+]
+
+POLICY_REWARD_CASES = [
+    # MPCcontrollerPolicyNetReward (controllers.py:289-363), self_exp=False
+    dict(name="polrew_explore05_ln", K=256, H=6, hidden=500, ln=True, seed=51, explore=0.5, ph=128, pl=2),
+    dict(name="polrew_explore0_pure", K=64, H=4, hidden=128, ln=False, seed=52, explore=0.0, ph=64, pl=1),
+    dict(name="polrew_explore1_pure_expl", K=96, H=5, hidden=256, ln=False, seed=53, explore=1.0, ph=128, pl=2),
+]
+
+
+class _NpProxy:
+    """Stands in for the ``np`` module inside the reference's controllers.py while a
+    controller runs, recording the arrays it reduces (argmax input = the reference's
+    own reward vector) and the action paths it stacks."""
+
+    def __init__(self):
+        self.argmax_in = None
+        self.stacked = []
+
+    def __getattr__(self, name):
+        return getattr(np, name)
+
+    def argmax(self, a, *args, **kwargs):
+        self.argmax_in = np.array(a, copy=True)
+        return np.argmax(a, *args, **kwargs)
+
+    def asarray(self, a, *args, **kwargs):
+        out = np.asarray(a, *args, **kwargs)
+        self.stacked.append(np.array(out, copy=True))
+        return out
+
+
+def _run_with_proxy(fn):
+    import contextlib
+    import io
+    proxy = _NpProxy()
+    ref_controllers.np = proxy
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):    # MPCcontrollerPolicyNetReward prints shapes (:351)
+            out = fn()
+    finally:
+        ref_controllers.np = np
+    return out, proxy
+
+
+def _reward_common(c, S, A, w, norm, state, rewards, opt_action, actions, extra):
+    order = np.sort(rewards[~np.isnan(rewards)])[::-1]
+    meta = dict(c, S=S, A=A, weight_digest=w.digest(), weight_seed_base=3000 + 19 * c["seed"],
+                norm_seed=7 + c["seed"], state_seed=11 + c["seed"], reward=True, **extra)
+    out = dict(
+        meta=json.dumps(meta), state=state,
+        mean_obs=norm[0], std_obs=norm[1], mean_action=norm[2], std_action=norm[3],
+        mean_reward=norm[4], std_reward=norm[5], mean_deltas=norm[8], std_deltas=norm[9],
+        rewards=rewards, argmax=np.int64(np.argmax(rewards)),
+        opt_action=np.asarray(opt_action, dtype=np.float64),
+        top2_gap=np.float64(order[0] - order[1]) if order.size > 1 else np.float64(np.inf),
+        first_actions=np.asarray(actions[0], dtype=np.float64),
+        action_digest=np.frombuffer(
+            __import__("hashlib").sha256(np.ascontiguousarray(actions).tobytes()).digest(), dtype=np.uint8),
+    )
+    if c["hidden"] <= STORE_WEIGHTS_MAX_HIDDEN:
+        for i, k in enumerate(w.kernels):
+            out[f"W{i}"] = k
+            out[f"b{i}"] = w.biases[i]
+    return out
+
+
+def run_reward_case(c):
+    S, A = 20, 6
+    w = orc.synthetic_reward_weights(S, A, c["hidden"], c["ln"], seed_base=3000 + 19 * c["seed"])
+    norm = orc.synthetic_normalization(S, A, seed=7 + c["seed"], reward=True)
+    state = orc.synthetic_state(norm, seed=11 + c["seed"])
+    dyn = orc.NumpyRewardDynamics(w, norm)
+    env = FakeEnv(S, A)
+    env.action_space.np_random = np.random.RandomState(c["seed"])
+    ctrl = ref_controllers.MPCcontrollerReward(env=env, dyn_model=dyn, horizon=c["H"], cost_fn=None,
+                                               num_simulated_paths=c["K"], gamma=c["gamma"])
+    captured = {}
+    inject = c.get("inject")
+    orig_sample = ctrl.sample_random_actions
+
+    def sample_wrapper():
+        ap = orig_sample()                     # K*H env.action_space.sample() calls, as the reference does
+        regen = np.random.RandomState(c["seed"]).uniform(-1, 1, size=(c["K"] * c["H"], A)).astype(np.float32)
+        assert np.array_equal(ap, regen.reshape(c["H"], c["K"], A)), "action regeneration recipe drifted"
+        if inject == "tie":
+            r0, _ = orc.reward_rollout(dyn, state, ap, c["gamma"])
+            best = int(np.argmax(r0))
+            lo = max(0, best // 2)
+            ap[:, lo, :] = ap[:, best, :]
+            ap[:, min(c["K"] - 1, best + 5), :] = ap[:, best, :]
+            captured["tie_pair"] = (lo, best)
+        elif inject == "nan":
+            ap[1, 21, 2] = np.nan
+            ap[0, 40, 5] = np.nan
+        elif inject == "philox":
+            ap = orc.device_rng_actions(c["rng_seed"], c["cand_offset"], c["K"], c["H"],
+                                        env.action_space.low, env.action_space.high)
+        captured["actions"] = ap
+        return ap
+
+    ctrl.sample_random_actions = sample_wrapper
+    opt_action, proxy = _run_with_proxy(lambda: ctrl.get_action(state))
+    rewards = proxy.argmax_in
+    ap = captured["actions"]
+    r2, _ = orc.reward_rollout(dyn, state, ap, c["gamma"])
+    assert np.array_equal(r2, rewards, equal_nan=True), c["name"]       # restatement is exact
+    i = int(np.argmax(rewards))
+    assert np.array_equal(ap[0, i], opt_action, equal_nan=True)
+    out = _reward_common(c, S, A, w, norm, state, rewards, opt_action, ap, {})
+    if "tie_pair" in captured:
+        out["tie_pair"] = np.asarray(captured["tie_pair"], dtype=np.int64)
+    return out
+
+
+def run_policy_reward_case(c):
+    S, A = 20, 6
+    w = orc.synthetic_reward_weights(S, A, c["hidden"], c["ln"], seed_base=3000 + 19 * c["seed"])
+    norm = orc.synthetic_normalization(S, A, seed=7 + c["seed"], reward=True)
+    state = orc.synthetic_state(norm, seed=11 + c["seed"])
+    pw = orc.synthetic_policy(S, A, c["ph"], c["pl"], seed=500 + c["seed"])
+    dyn, pol = orc.NumpyRewardDynamics(w, norm), orc.NumpyPolicy(pw)
+    env = FakeEnv(S, A)
+    ctrl = ref_controllers.MPCcontrollerPolicyNetReward(env=env, dyn_model=dyn, policy_net=pol,
+                                                        explore=c["explore"], self_exp=False, horizon=c["H"],
+                                                        num_simulated_paths=c["K"])
+    np.random.seed(c["seed"])
+    opt_action, proxy = _run_with_proxy(lambda: ctrl.get_action(state))
+    next_draw = np.random.random()
+    rewards = proxy.argmax_in
+    actions = next(a for a in proxy.stacked if a.ndim == 3 and a.shape[-1] == A)
+    np.random.seed(c["seed"])
+    a2, i2, r2, ap2 = orc.policy_reward_get_action(dyn, pol, state, c["H"], c["K"], env.action_space.low,
+                                                   env.action_space.high, c["explore"])
+    assert np.array_equal(r2, rewards) and np.array_equal(a2, opt_action) and np.array_equal(ap2, actions), c["name"]
+    out = _reward_common(c, S, A, w, norm, state, rewards, opt_action, actions,
+                         dict(policy_seed=500 + c["seed"], policy=True))
+    out["next_draw"] = np.float64(next_draw)
+    for i, k in enumerate(pw.kernels):
+        out[f"PW{i}"] = k
+        out[f"PB{i}"] = pw.biases[i]
+    out["P_ob_mean"], out["P_ob_std"], out["P_logstd"] = pw.ob_mean, pw.ob_std, pw.logstd
+    return out
+
+
 def main():
     note = try_trained_weights()
     print("vars.pkl:", note)
@@ -264,10 +426,20 @@ def main():
                        reference_files=["controllers.py", "cost_functions.py"],
                        dynamics="oracle.NumpyDynamics (TF1 absent; restatement of dynamics.py:54-71,106-119)",
                        numpy=np.__version__, trained_weights=note,
-                       cases=[c["name"] for c in CASES] + [c["name"] for c in POLICY_CASES],
+                       cases=[c["name"] for c in CASES + POLICY_CASES + REWARD_CASES + POLICY_REWARD_CASES],
+                       reward_cases="controllers.MPCcontrollerReward / MPCcontrollerPolicyNetReward with "
+                                    "oracle.NumpyRewardDynamics (restatement of dynamics.py:121-238); the "
+                                    "reward vector is the argument the reference passes to np.argmax",
                        policy_cases="controllers.MPCcontrollerPolicyNet with oracle.NumpyPolicy (MlpPolicy.act "
                                     "deterministic branch, ppo_bc_policy.py:54-88,174-185; TF/baselines absent)"),
                   f, indent=1)
+    for c in REWARD_CASES + POLICY_REWARD_CASES:
+        out = (run_policy_reward_case if c.get("explore") is not None else run_reward_case)(c)
+        np.savez_compressed(os.path.join(HERE, f"{c['name']}.npz"), **out)
+        print(f"{c['name']:32s} K={c['K']:5d} H={c['H']:3d} argmax={int(out['argmax']):5d} "
+              f"gap={float(out['top2_gap']):.4g}")
+    if os.environ.get("GEN_REWARD_ONLY"):
+        return
     for c in POLICY_CASES:
         out = run_policy_case(c)
         np.savez_compressed(os.path.join(HERE, f"{c['name']}.npz"), **out)

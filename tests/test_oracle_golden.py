@@ -79,3 +79,35 @@ def test_oracle_policy_controller_reproduces_reference(golden_policy):
     assert np.array_equal(costs, g.costs)
     assert i == g.argmin and np.array_equal(a, g.opt_action)
     assert np.random.random() == float(g.z["next_draw"])
+
+
+def test_oracle_reward_controllers_reproduce_reference(golden_reward):
+    """MPCcontrollerReward (controllers.py:90-158) / MPCcontrollerPolicyNetReward
+    (controllers.py:289-363) on the NNDynamicsRewardModel restatement, vs the reference run."""
+    g = golden_reward
+    dyn = g.dyn()
+    if g.policy is None:
+        ap = g.env_actions()
+        assert hashlib.sha256(np.ascontiguousarray(ap).tobytes()).digest() == g.z["action_digest"].tobytes()
+        rewards, _ = orc.reward_rollout(dyn, g.state, ap, g.gamma)
+        i = int(np.argmax(rewards))
+        a = ap[0, i]
+    else:
+        np.random.seed(g.meta["seed"])
+        a, i, rewards, ap = orc.policy_reward_get_action(dyn, orc.NumpyPolicy(g.policy), g.state, g.H, g.K,
+                                                         g.low, g.high, g.explore)
+        assert np.random.random() == float(g.z["next_draw"])
+        assert np.array_equal(ap[0], g.z["first_actions"])
+    assert np.array_equal(rewards, g.rewards, equal_nan=True)
+    assert i == g.argmax and np.array_equal(np.asarray(a, dtype=np.float64), g.opt_action, equal_nan=True)
+
+
+def test_reward_sum_is_sequential_in_h():
+    """np.sum(axis=0) over [H, K, 1] (controllers.py:150) adds steps in order; the
+    kernel's running sum relies on that."""
+    rs = np.random.RandomState(5)
+    a = rs.standard_normal((23, 300, 1)) * np.exp(3 * rs.standard_normal((23, 300, 1)))
+    seq = a[0].copy()
+    for i in range(1, 23):
+        seq = seq + a[i]
+    assert np.array_equal(np.sum(a, axis=0), seq)
