@@ -24,11 +24,12 @@ LIB_PATH = os.environ.get("BCMPC_LIB") or os.path.join(os.path.dirname(os.path.a
 MAX_LAYERS = 8
 MAX_STATE = 32
 MAX_ACTION = 16
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
 ACT_TANH, ACT_RELU = 0, 1
-COST_CHEETAH, COST_NONE = 0, 1
+COST_CHEETAH, COST_NONE, COST_REWARD = 0, 1, 2
+MODEL_DELTA, MODEL_REWARD = 0, 1
 PREC_FP32 = 0
 KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3, "group8": 4}
 
@@ -50,7 +51,8 @@ class Config(ctypes.Structure):
         ("policy_hidden", ctypes.c_int32),
         ("policy_layers", ctypes.c_int32),
         ("policy_mode", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 4),
+        ("model", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
     ]
 
 
@@ -70,6 +72,8 @@ class Weights(ctypes.Structure):
         ("std_action", _DP),
         ("mean_deltas", _DP),
         ("std_deltas", _DP),
+        ("mean_reward", _DP),
+        ("std_reward", _DP),
     ]
 
 
@@ -105,6 +109,7 @@ SIGNATURES = [
     ("bcmpc_weights_version", ctypes.c_uint64, [ctypes.c_void_p]),
     ("bcmpc_set_policy", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Policy), ctypes.c_uint64]),
     ("bcmpc_first_actions", ctypes.c_int, [ctypes.c_void_p, _DP]),
+    ("bcmpc_set_discount", ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
     ("bcmpc_set_action_bounds", ctypes.c_int, [ctypes.c_void_p, _DP, _DP]),
     ("bcmpc_get_action", ctypes.c_int,
      [ctypes.c_void_p, _DP, _DP, ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(Result), _DP]),

@@ -21,9 +21,19 @@ Action source (``rng=``):
 Multi-GPU: when torch.distributed is initialised each rank owns a contiguous
 slice of the K candidates (``distributed.shard_range``) and the ranks agree on
 the argmin through one all-gather of (3 + A) doubles per step.
+
+The siblings run on the same engine:
+
+* ``MPCcontrollerPolicyNet`` (controllers.py:160-239): policy MLP fused into
+  the rollout kernel;
+* ``MPCcontrollerReward`` (controllers.py:90-158) and
+  ``MPCcontrollerPolicyNetReward`` (controllers.py:289-363): the two-head
+  ``NNDynamicsRewardModel`` net (dynamics.py:121-238) in the kernel, objective =
+  argmax of the (discounted) predicted reward sum.
 """
 from __future__ import annotations
 
+import copy
 import os
 from typing import Optional
 
@@ -147,6 +157,9 @@ class MPCcontroller(Controller):
         rank, ws = _dist.world(self._group)
         lo, hi = _dist.shard_range(K, rank, ws)
         spec, norm, version = _weights.extract(self.dyn_model)
+        if spec.model != "delta":
+            raise TypeError("MPCcontroller needs an NNDynamicsModel: NNDynamicsRewardModel.predict returns "
+                            "(next_state, reward) (dynamics.py:238); use MPCcontrollerReward")
         fused = is_cheetah_cost(self.cost_fn, S, A)
         if not fused and self.rng != "numpy":
             raise ValueError("a non-cheetah cost_fn needs rng='numpy' (actions must exist on the host)")
@@ -259,19 +272,23 @@ class MPCcontrollerPolicyNet(Controller):
     def _engine_for(self, spec, pspec, S, A, k_local) -> RolloutEngine:
         dev = _default_device() if self._device is None else self._device
         mode = "stochastic" if self.self_exp else "explore"
-        key = (S, A, spec.hidden, spec.n_layers, spec.activation, spec.layer_norm, int(self.horizon), int(k_local),
-               dev, pspec.hidden, pspec.n_layers, mode)
+        key = (S, A, spec.model, spec.hidden, spec.n_layers, spec.activation, spec.layer_norm, int(self.horizon),
+               int(k_local), dev, pspec.hidden, pspec.n_layers, mode)
         if self._engine is None or self._engine_key != key:
             if self._engine is not None:
                 self._engine.close()
+            reward = spec.model == "reward"
             self._engine = RolloutEngine(S, A, spec.hidden, spec.n_layers, spec.activation, spec.layer_norm,
-                                         int(self.horizon), int(k_local), device=dev, cost="cheetah",
+                                         int(self.horizon), int(k_local), device=dev,
+                                         cost="reward" if reward else "cheetah", model=spec.model,
                                          policy_hidden=pspec.hidden, policy_layers=pspec.n_layers,
                                          policy_mode=mode)
             self._engine.set_action_bounds(np.asarray(self.env.action_space.low, dtype=np.float64),
                                            np.asarray(self.env.action_space.high, dtype=np.float64))
             self._engine_key = key
         return self._engine
+
+    _MODEL = "delta"     # NNDynamicsModel + cheetah cost, argmin
 
     # controllers.py:189-237
     def get_action(self, state):
@@ -280,17 +297,19 @@ class MPCcontrollerPolicyNet(Controller):
         K = int(self.num_simulated_paths)
         if self.horizon < 1:
             raise IndexError("index 0 is out of bounds for axis 0 with size 0")
-        if not is_cheetah_cost(self.cost_fn, S, A):
+        reward = self._MODEL == "reward"
+        if not reward and not is_cheetah_cost(self.cost_fn, S, A):
             raise ValueError("MPCcontrollerPolicyNet on the engine needs the fused cheetah cost_fn")
         state = np.asarray(state, dtype=np.float64).reshape(-1)
         rank, ws = _dist.world(self._group)
         lo, hi = _dist.shard_range(K, rank, ws)
         spec, norm, version = _weights.extract(self.dyn_model)
+        _check_model(spec, self._MODEL, type(self).__name__)
         pspec, pversion = _policy.extract(self.policy_net)
         exploration = self.sample_random_actions()           # every rank draws the full [H, K, A]
         seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
         if K == 0:
-            raise ValueError("attempt to get argmin of an empty sequence")
+            raise ValueError(f"attempt to get {'argmax' if reward else 'argmin'} of an empty sequence")
         valid, cost, index, first = False, float("inf"), -1, None
         if hi > lo:
             eng = self._engine_for(spec, pspec, S, A, hi - lo)
@@ -300,8 +319,163 @@ class MPCcontrollerPolicyNet(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, cost, index, first = True, res.best_cost, res.best_index, res.first_action
             self.last_costs = res.costs
-        cost, index, first_g = _dist.allgather_minloc(valid, cost, index, first, A, self._group)
-        self.last_cost, self.last_index = cost, index
+        sign = -1.0 if reward else 1.0                         # argmax(r) == argmin(-r), ties and NaN alike
+        cost, index, first_g = _dist.allgather_minloc(valid, sign * cost, index, first, A, self._group)
+        self.last_cost, self.last_index = sign * cost, index
         return first_g                                         # copy of action_paths[0, argmin] (:233-235)
 
     get_action_mcs = get_action                                # controllers.py:239 (identical body)
+
+
+def _check_model(spec, want: str, who: str) -> None:
+    if spec.model != want:
+        need = "NNDynamicsRewardModel (dynamics.py:121)" if want == "reward" else "NNDynamicsModel (dynamics.py:7)"
+        raise TypeError(f"{who} needs an {need}; got a {spec.model!r} dynamics net")
+
+
+class MPCcontrollerReward(Controller):
+    """Learned-reward random-shooting MPC (controllers.py:90-158) on the engine.
+
+    ``dyn_model`` is an ``NNDynamicsRewardModel`` (dynamics.py:121-238): the
+    kernel runs its two-head net each step and accumulates
+    ``sum_h reward_h * gamma**h`` (controllers.py:139,150); the controller
+    returns the first action of the ARGMAX path (controllers.py:152-156).
+
+    Action source (``rng=``):
+
+    * ``"env"`` (default, parity mode): ``sample_random_actions`` makes K*H
+      ``env.action_space.sample()`` calls and reshapes them to ``[H, K, A]``
+      exactly as controllers.py:108-119 (same env-RNG side effect, same dtype --
+      a float32 Box gives float32 actions, widened exactly to f64 for the engine);
+    * ``"device"`` (perf mode): Philox draws in the kernel, one 64-bit seed per
+      call from a private generator (``seed=``), env RNG untouched.
+    """
+
+    def __init__(self,
+                 env,
+                 dyn_model,
+                 horizon=5,
+                 cost_fn=None,
+                 num_simulated_paths=10,
+                 gamma=1.,
+                 *,
+                 rng: str = "env",
+                 seed: Optional[int] = None,
+                 device: Optional[int] = None,
+                 process_group=None):
+        self.env = env
+        self.dyn_model = dyn_model
+        self.horizon = horizon
+        self.cost_fn = cost_fn                  # stored, unused (as in the reference)
+        self.num_simulated_paths = num_simulated_paths
+        self.gamma = gamma
+        if rng not in ("env", "device"):
+            raise ValueError("rng must be 'env' or 'device'")
+        self.rng = rng
+        self._seed_rng = np.random.RandomState(0x5EED0BAD if seed is None else seed)
+        self._device = device
+        self._group = process_group
+        self._engine: Optional[RolloutEngine] = None
+        self._engine_key = None
+        self._gamma_set = None
+        self.last_reward = None
+        self.last_index = None
+        self.last_rewards = None
+        self.keep_costs = False
+
+    # controllers.py:108-119
+    def sample_random_actions(self):
+        actions = []
+        for n in range(self.num_simulated_paths):
+            for h in range(self.horizon):
+                actions.append(self.env.action_space.sample())
+        np_action_paths = np.asarray(actions)
+        np_action_paths = np.reshape(np_action_paths, [self.horizon, self.num_simulated_paths, -1])
+        return np_action_paths
+
+    def _engine_for(self, spec, S, A, k_local) -> RolloutEngine:
+        dev = _default_device() if self._device is None else self._device
+        key = (S, A, spec.hidden, spec.layer_norm, int(self.horizon), int(k_local), dev)
+        if self._engine is None or self._engine_key != key:
+            if self._engine is not None:
+                self._engine.close()
+            self._engine = RolloutEngine(S, A, spec.hidden, 2, "tanh", spec.layer_norm, int(self.horizon),
+                                         int(k_local), device=dev, cost="reward", model="reward")
+            self._engine.set_action_bounds(np.asarray(self.env.action_space.low, dtype=np.float64),
+                                           np.asarray(self.env.action_space.high, dtype=np.float64))
+            self._engine_key = key
+            self._gamma_set = None
+        if self._gamma_set != float(self.gamma):
+            self._engine.set_discount(float(self.gamma))
+            self._gamma_set = float(self.gamma)
+        return self._engine
+
+    # controllers.py:121-158
+    def get_action(self, state):
+        S = int(np.prod(self.env.observation_space.shape))
+        A = len(self.env.action_space.high)
+        K = int(self.num_simulated_paths)
+        if self.horizon < 1:
+            raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+        state = np.asarray(state, dtype=np.float64).reshape(-1)
+        rank, ws = _dist.world(self._group)
+        lo, hi = _dist.shard_range(K, rank, ws)
+        spec, norm, version = _weights.extract(self.dyn_model)
+        _check_model(spec, "reward", type(self).__name__)
+        action_paths, seed = None, 0
+        if self.rng == "env":
+            action_paths = self.sample_random_actions()      # every rank draws the full [H, K, A]
+        else:
+            seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+        if K == 0:
+            raise ValueError("attempt to get argmax of an empty sequence")
+        valid, neg, index, first = False, float("inf"), -1, None
+        if hi > lo:
+            eng = self._engine_for(spec, S, A, hi - lo)
+            eng.set_weights(spec, norm, version)
+            local = None if action_paths is None else np.ascontiguousarray(action_paths[:, lo:hi, :],
+                                                                           dtype=np.float64)
+            res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
+            valid, neg, index, first = True, -res.best_cost, res.best_index, res.first_action
+            self.last_rewards = res.costs
+        neg, index, first_g = _dist.allgather_minloc(valid, neg, index, first, A, self._group)
+        self.last_reward, self.last_index = -neg, index
+        if action_paths is not None:
+            return copy.copy(action_paths[:, index, :][0])    # controllers.py:154-156
+        return first_g
+
+
+class MPCcontrollerPolicyNetReward(MPCcontrollerPolicyNet):
+    """Policy-guided learned-reward MPC (controllers.py:289-363) on the engine:
+    the fused policy of ``MPCcontrollerPolicyNet`` plus the two-head reward net;
+    argmax of the UNdiscounted reward sum (``gamma`` is stored but unused,
+    controllers.py:345).  The reference's debug print of the reward-vector
+    shape (controllers.py:351) is not reproduced."""
+
+    _MODEL = "reward"
+
+    def __init__(self,
+                 env,
+                 dyn_model,
+                 policy_net,
+                 explore=1.,
+                 self_exp=True,
+                 horizon=5,
+                 cost_fn=None,
+                 num_simulated_paths=10,
+                 gamma=1.,
+                 *,
+                 seed: Optional[int] = None,
+                 device: Optional[int] = None,
+                 process_group=None):
+        super().__init__(env, dyn_model, policy_net, explore=explore, self_exp=self_exp, horizon=horizon,
+                         cost_fn=cost_fn, num_simulated_paths=num_simulated_paths, seed=seed, device=device,
+                         process_group=process_group)
+        self.gamma = gamma
+
+    # controllers.py:310-316
+    def sample_random_actions(self):
+        np_action_paths = np.random.uniform(low=self.env.action_space.low, high=self.env.action_space.high,
+                                            size=[self.horizon, self.num_simulated_paths,
+                                                  len(self.env.action_space.high)])
+        return np_action_paths

@@ -77,7 +77,9 @@ struct bcmpc_engine {
     bcmpc_config cfg{};
     int HP = 0, T = 0, wpb = 4;
     int kernel = BCMPC_KERNEL_SOLO;    // resolved kernel layout
+    int nw = 1;                        // waves per group (group kernels)
     int pack_tb = 4;                   // output tiles per packed block of layers 0..L-1
+    bool reward = false;               // BCMPC_MODEL_REWARD (NNDynamicsRewardModel)
     hipStream_t stream = nullptr;
     // device buffers
     float* d_w = nullptr;   size_t w_floats = 0;
@@ -100,6 +102,9 @@ struct bcmpc_engine {
     float* d_pw = nullptr;  size_t pw_floats = 0;  size_t pw_off[BCMPC_MAX_LAYERS + 1]{};
     float* d_pb = nullptr;                          // [PL][PHP] + kPolParams
     double* d_first = nullptr;                      // [K][A] step-0 actions
+    // learned reward (NNDynamicsRewardModel)
+    double* d_gpow = nullptr;                       // [H] gamma**h
+    double mean_reward = 0.0, std_reward = 0.0;
     double explore = 0.0;
     uint64_t pol_version = 0;
     bool has_policy = false;
@@ -122,7 +127,19 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     if (c.activation != BCMPC_ACT_TANH && c.activation != BCMPC_ACT_RELU) return fail(BCMPC_ERR_UNSUPPORTED, "activation must be tanh or relu");
     if (c.horizon < 1) return fail(BCMPC_ERR_ARG, "horizon must be >= 1");
     if (c.num_paths < 0) return fail(BCMPC_ERR_ARG, "num_paths must be >= 0");
-    if (c.cost != BCMPC_COST_CHEETAH && c.cost != BCMPC_COST_NONE) return fail(BCMPC_ERR_UNSUPPORTED, "unknown cost");
+    if (c.cost != BCMPC_COST_CHEETAH && c.cost != BCMPC_COST_NONE && c.cost != BCMPC_COST_REWARD)
+        return fail(BCMPC_ERR_UNSUPPORTED, "unknown cost");
+    if (c.model != BCMPC_MODEL_DELTA && c.model != BCMPC_MODEL_REWARD) return fail(BCMPC_ERR_ARG, "unknown model");
+    const bool reward = c.model == BCMPC_MODEL_REWARD;
+    if ((c.cost == BCMPC_COST_REWARD) != reward)
+        return fail(BCMPC_ERR_ARG, "the learned-reward objective and BCMPC_MODEL_REWARD go together "
+                                   "(MPCcontrollerReward needs NNDynamicsRewardModel, controllers.py:137)");
+    if (reward) {
+        if (c.n_layers != 2) return fail(BCMPC_ERR_ARG, "reward model: n_layers must be 2 (trunk + head, dynamics.py:167-174)");
+        if (c.activation != BCMPC_ACT_TANH) return fail(BCMPC_ERR_UNSUPPORTED, "reward model is tanh (dynamics.py:150)");
+        if (c.hidden > 512) return fail(BCMPC_ERR_UNSUPPORTED, "reward model: hidden must be <= 512 in this build");
+        if (c.state_dim > 31) return fail(BCMPC_ERR_UNSUPPORTED, "reward model: state_dim must be <= 31");
+    }
     if (c.cost == BCMPC_COST_CHEETAH && c.state_dim < 18) return fail(BCMPC_ERR_UNSUPPORTED, "cheetah cost needs state_dim >= 18");
     if (c.precision != BCMPC_PREC_FP32) return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32");
     int ndev = 0;
@@ -132,7 +149,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
 
     bcmpc_engine* e = new bcmpc_engine();
     e->cfg = c;
-    e->HP = padded_hidden(c.hidden);
+    e->reward = reward;
+    e->HP = reward ? std::max(128, padded_hidden(c.hidden)) : padded_hidden(c.hidden);
     e->T = e->HP / 16;
     // small K: one wave per block spreads candidates over more CUs
     const int64_t waves = (c.num_paths + 15) / 16;
@@ -140,6 +158,13 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     // auto: 4-wave groups; 8-wave groups when K is too small to give every SIMD two waves
     int kern = c.kernel != BCMPC_KERNEL_AUTO ? c.kernel
              : ((c.num_paths + 15) / 16 < 512 && e->T % 8 == 0 ? BCMPC_KERNEL_GROUP8 : BCMPC_KERNEL_GROUP4);
+    if (reward) {
+        // two-head net: 4-wave groups (16 head tiles per wave, spill-free at 2 waves/SIMD; the
+        // 8-wave layout needs ~135 registers and spills at 4 waves/SIMD -- measured 2.5% slower)
+        if (c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4 && c.kernel != BCMPC_KERNEL_GROUP8)
+            { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "reward engines run on the group4 / group8 kernels"); }
+        if (c.kernel == BCMPC_KERNEL_AUTO) kern = BCMPC_KERNEL_GROUP4;
+    }
     if (c.policy_hidden > 0) {
         // MPCcontrollerPolicyNet: the policy MLP is fused into the 4-wave group kernel
         if (c.policy_hidden > 128 || c.policy_layers < 1 || c.policy_layers > BCMPC_MAX_LAYERS)
@@ -148,9 +173,9 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (e->HP < 128 || e->HP > 512) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines support dynamics hidden 65..512"); }
         if (c.policy_mode != BCMPC_POLICY_EXPLORE && c.policy_mode != BCMPC_POLICY_STOCHASTIC)
             { delete e; return fail(BCMPC_ERR_ARG, "unknown policy_mode"); }
-        if (c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4)
-            { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines run on the group4 kernel"); }
-        kern = BCMPC_KERNEL_GROUP4;
+        if (c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4 && c.kernel != BCMPC_KERNEL_GROUP8)
+            { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines run on the group4 / group8 kernels"); }
+        if (c.kernel == BCMPC_KERNEL_AUTO) kern = BCMPC_KERNEL_GROUP4;
         e->PHP = 128;
         e->TP = 8;
         e->PL = c.policy_layers;
@@ -158,7 +183,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_GROUP8) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
     const int nw = kern_waves(kern);
     if (kern != BCMPC_KERNEL_SOLO &&
-        (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw, e->PHP, e->PL) > 160 * 1024)) {
+        (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw, e->PHP, e->PL, c.model) > 160 * 1024)) {
         if (c.kernel != BCMPC_KERNEL_AUTO) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group kernel does not fit this shape"); }
         kern = BCMPC_KERNEL_SOLO;
     }
@@ -168,21 +193,30 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         return fail(BCMPC_ERR_UNSUPPORTED, "solo kernel supports hidden <= 512 and needs LDS for its slabs");
     }
     e->kernel = kern;
+    e->nw = nw;
     e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->T / nw;
     const int L = c.n_layers, T = e->T;
-    size_t off = 0;
-    e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;                   // [S+A -> h]
-    for (int l = 1; l < L; ++l) { e->w_off[l] = off; off += (size_t)T * T * 64 * 4; }
-    e->w_off[L] = off; off += (size_t)2 * T * 64 * 4;                   // [h -> S]
+    size_t off = 0, boff = 0;
+    if (reward) {
+        // [S+A -> h] trunk, [h -> 2h] both heads' hidden layers, [2h -> S+1] block-diagonal output
+        e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;
+        e->w_off[1] = off; off += (size_t)2 * T * T * 64 * 4;
+        e->w_off[2] = off; off += (size_t)2 * 2 * T * 64 * 4;
+        e->b_off[0] = 0; e->b_off[1] = e->HP; e->b_off[2] = 3 * e->HP; boff = 3 * e->HP + 32;
+    } else {
+        e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;                   // [S+A -> h]
+        for (int l = 1; l < L; ++l) { e->w_off[l] = off; off += (size_t)T * T * 64 * 4; }
+        e->w_off[L] = off; off += (size_t)2 * T * 64 * 4;                   // [h -> S]
+        for (int l = 0; l < L; ++l) { e->b_off[l] = boff; boff += e->HP; }
+        e->b_off[L] = boff; boff += 32;
+    }
     e->w_floats = off;
-    size_t boff = 0;
-    for (int l = 0; l < L; ++l) { e->b_off[l] = boff; boff += e->HP; }
-    e->b_off[L] = boff; boff += 32;
+    const size_t ln_floats = 2 * (size_t)(reward ? 3 : L) * e->HP;
     auto cleanup = [&](int code) { bcmpc_destroy(e); return code; };
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&e->d_w, e->w_floats * sizeof(float)) != hipSuccess ||
         hipMalloc(&e->d_b, boff * sizeof(float)) != hipSuccess ||
-        hipMalloc(&e->d_ln, 2 * (size_t)L * e->HP * sizeof(float)) != hipSuccess ||
+        hipMalloc(&e->d_ln, ln_floats * sizeof(float)) != hipSuccess ||
         hipMalloc(&e->d_consts, sizeof(e->h_consts)) != hipSuccess ||
         hipMalloc(&e->d_state, BCMPC_MAX_STATE * sizeof(double)) != hipSuccess ||
         hipMalloc(&e->d_costs, std::max<int64_t>(1, c.num_paths) * sizeof(double)) != hipSuccess ||
@@ -206,6 +240,17 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
             return cleanup(BCMPC_ERR_HIP);
         }
     }
+    if (reward) {
+        if (hipMalloc(&e->d_gpow, (size_t)c.horizon * sizeof(double)) != hipSuccess) {
+            g_last_error = "device allocation failed";
+            return cleanup(BCMPC_ERR_HIP);
+        }
+        std::vector<double> ones((size_t)c.horizon, 1.0);
+        if (hipMemcpy(e->d_gpow, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+            g_last_error = "gamma upload failed";
+            return cleanup(BCMPC_ERR_HIP);
+        }
+    }
     // default action bounds: HalfCheetah ctrlrange [-1, 1]
     for (int j = 0; j < BCMPC_MAX_ACTION && j < kConstCols; ++j) {
         e->h_consts[6 * kConstCols + j] = -1.0;
@@ -220,7 +265,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
-                    (void*)e->d_first})
+                    (void*)e->d_first, (void*)e->d_gpow})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
     for (auto& ev : e->ev)
@@ -240,23 +285,59 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
     if (c.layer_norm && (!w->ln_gamma || !w->ln_beta)) return fail(BCMPC_ERR_ARG, "layer_norm enabled but LN params missing");
     if (!w->mean_obs || !w->std_obs || !w->mean_action || !w->std_action || !w->mean_deltas || !w->std_deltas)
         return fail(BCMPC_ERR_ARG, "normalization stats missing");
-    for (int l = 0; l <= L; ++l)
+    const bool rw = e->reward;
+    if (rw && (!w->mean_reward || !w->std_reward)) return fail(BCMPC_ERR_ARG, "reward model: mean_reward / std_reward missing");
+    const int NK = rw ? 5 : L + 1, NLN = rw ? 3 : L;      // kernels, LayerNorms
+    for (int l = 0; l < NK; ++l)
         if (!w->kernels[l] || !w->biases[l]) return fail(BCMPC_ERR_ARG, "null kernel/bias pointer");
+    if (c.layer_norm)
+        for (int l = 0; l < NLN; ++l)
+            if (!w->ln_gamma[l] || !w->ln_beta[l]) return fail(BCMPC_ERR_ARG, "null LayerNorm pointer");
     HIP_TRY(hipSetDevice(c.device));
     std::vector<float> hw(e->w_floats, 0.f);
     const int tb = e->pack_tb;
+    std::vector<float> hb(rw ? 3 * (size_t)HP + 32 : (size_t)L * HP + 32, 0.f);
+    std::vector<float> hln(2 * (size_t)NLN * HP, 0.f);
     pack_layer(w->kernels[0], S + A, h, 2, T, tb, hw.data() + e->w_off[0]);
-    for (int l = 1; l < L; ++l) pack_layer(w->kernels[l], h, h, T, T, tb, hw.data() + e->w_off[l]);
-    pack_layer(w->kernels[L], h, S, T, 2, 2, hw.data() + e->w_off[L]);
-    std::vector<float> hb((size_t)L * HP + 32, 0.f);
-    for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
-    std::memcpy(hb.data() + e->b_off[L], w->biases[L], sizeof(float) * S);
-    std::vector<float> hln(2 * (size_t)L * HP, 0.f);
-    if (c.layer_norm)
-        for (int l = 0; l < L; ++l) {
-            std::memcpy(hln.data() + (size_t)l * HP, w->ln_gamma[l], sizeof(float) * h);
-            std::memcpy(hln.data() + (size_t)(L + l) * HP, w->ln_beta[l], sizeof(float) * h);
+    if (rw) {
+        // heads' hidden layers side by side: W1c[k][n] = dense_1 (n < HP) | dense_3 (n >= HP)
+        std::vector<float> w1((size_t)h * 2 * HP, 0.f), wo((size_t)2 * HP * 32, 0.f);
+        for (int k = 0; k < h; ++k)
+            for (int n = 0; n < h; ++n) {
+                w1[(size_t)k * 2 * HP + n] = w->kernels[1][(size_t)k * h + n];
+                w1[(size_t)k * 2 * HP + HP + n] = w->kernels[3][(size_t)k * h + n];
+            }
+        // block-diagonal output: rows [0,h) x cols [0,S) = dense_2; rows [HP,HP+h) x col S = dense_4
+        for (int k = 0; k < h; ++k) {
+            for (int n = 0; n < S; ++n) wo[(size_t)k * 32 + n] = w->kernels[2][(size_t)k * S + n];
+            wo[(size_t)(HP + k) * 32 + S] = w->kernels[4][k];
         }
+        pack_layer(w1.data(), h, 2 * HP, T, 2 * T, 2 * T / e->nw, hw.data() + e->w_off[1]);
+        pack_layer(wo.data(), 2 * HP, 32, 2 * T, 2, 2, hw.data() + e->w_off[2]);
+        std::memcpy(hb.data(), w->biases[0], sizeof(float) * h);
+        std::memcpy(hb.data() + HP, w->biases[1], sizeof(float) * h);
+        std::memcpy(hb.data() + 2 * HP, w->biases[3], sizeof(float) * h);
+        std::memcpy(hb.data() + 3 * HP, w->biases[2], sizeof(float) * S);
+        hb[3 * HP + S] = w->biases[4][0];
+        // LN: [gamma trunk HP | delta HP | reward HP][beta ...], i.e. the heads' params side by side
+        if (c.layer_norm)
+            for (int l = 0; l < 3; ++l) {
+                std::memcpy(hln.data() + (size_t)l * HP, w->ln_gamma[l], sizeof(float) * h);
+                std::memcpy(hln.data() + (size_t)(3 + l) * HP, w->ln_beta[l], sizeof(float) * h);
+            }
+        e->mean_reward = w->mean_reward[0];
+        e->std_reward = w->std_reward[0];
+    } else {
+        for (int l = 1; l < L; ++l) pack_layer(w->kernels[l], h, h, T, T, tb, hw.data() + e->w_off[l]);
+        pack_layer(w->kernels[L], h, S, T, 2, 2, hw.data() + e->w_off[L]);
+        for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
+        std::memcpy(hb.data() + e->b_off[L], w->biases[L], sizeof(float) * S);
+        if (c.layer_norm)
+            for (int l = 0; l < L; ++l) {
+                std::memcpy(hln.data() + (size_t)l * HP, w->ln_gamma[l], sizeof(float) * h);
+                std::memcpy(hln.data() + (size_t)(L + l) * HP, w->ln_beta[l], sizeof(float) * h);
+            }
+    }
     double* C = e->h_consts;
     for (int i = 0; i < kConstCols; ++i) {
         C[0 * 32 + i] = i < S ? w->mean_obs[i] : 0.0;
@@ -287,7 +368,7 @@ int bcmpc_set_policy(bcmpc_engine* e, const bcmpc_policy* p, uint64_t version) {
         if (!p->kernels[l] || !p->biases[l]) return fail(BCMPC_ERR_ARG, "null policy kernel/bias pointer");
     HIP_TRY(hipSetDevice(c.device));
     std::vector<float> hw(e->pw_floats, 0.f);
-    const int tb = TP / 4;
+    const int tb = TP / e->nw;
     pack_layer(p->kernels[0], S, ph, 2, TP, tb, hw.data() + e->pw_off[0]);
     for (int l = 1; l < PL; ++l) pack_layer(p->kernels[l], ph, ph, TP, TP, tb, hw.data() + e->pw_off[l]);
     int rowmap[16];
@@ -336,6 +417,17 @@ int bcmpc_set_action_bounds(bcmpc_engine* e, const double* low, const double* hi
     return BCMPC_OK;
 }
 
+int bcmpc_set_discount(bcmpc_engine* e, double gamma) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    if (!e->reward) return fail(BCMPC_ERR_STATE, "discount applies to reward engines (config.model == BCMPC_MODEL_REWARD)");
+    std::vector<double> g((size_t)e->cfg.horizon);
+    for (int i = 0; i < e->cfg.horizon; ++i) g[i] = std::pow(gamma, (double)i);   // Python float ** int
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    HIP_TRY(hipMemcpyAsync(e->d_gpow, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return BCMPC_OK;
+}
+
 void* bcmpc_stream(bcmpc_engine* e) { return e ? (void*)e->stream : nullptr; }
 
 static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, const double* d_actions,
@@ -345,8 +437,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     if (!e->has_weights) return fail(BCMPC_ERR_STATE, "bcmpc_set_weights has not been called");
     if (c.num_paths == 0) return fail(BCMPC_ERR_EMPTY, "attempt to get argmin of an empty sequence");
     if (stride != 0 && stride != c.state_dim) return fail(BCMPC_ERR_ARG, "state_stride must be 0 or state_dim");
-    if (c.cost == BCMPC_COST_CHEETAH && !d_costs) return fail(BCMPC_ERR_ARG, "cheetah cost needs a costs buffer");
-    if (d_result && c.cost != BCMPC_COST_CHEETAH) return fail(BCMPC_ERR_ARG, "argmin needs the fused cost");
+    if (c.cost != BCMPC_COST_NONE && !d_costs) return fail(BCMPC_ERR_ARG, "the fused objective needs a costs buffer");
+    if (d_result && c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "argmin needs the fused cost");
     RolloutArgs a{};
     for (int l = 0; l <= c.n_layers; ++l) {
         const size_t end = l < c.n_layers ? e->w_off[l + 1] : e->w_floats;
@@ -354,9 +446,18 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.w[l] = reinterpret_cast<const float __attribute__((ext_vector_type(4)))*>(e->d_w + e->w_off[l]);
         a.b[l] = e->d_b + e->b_off[l];
     }
-    for (int l = 0; l < c.n_layers; ++l) {
-        a.lng[l] = e->d_ln + (size_t)l * e->HP;
-        a.lnb[l] = e->d_ln + (size_t)(c.n_layers + l) * e->HP;
+    if (e->reward) {   // trunk LN, then the two heads' LN params side by side (2*HP)
+        a.lng[0] = e->d_ln;               a.lng[1] = e->d_ln + e->HP;
+        a.lnb[0] = e->d_ln + 3 * e->HP;   a.lnb[1] = e->d_ln + 4 * e->HP;
+        a.model = BCMPC_MODEL_REWARD;
+        a.mean_reward = e->mean_reward;
+        a.std_reward = e->std_reward;
+        a.gpow = e->d_gpow;
+    } else {
+        for (int l = 0; l < c.n_layers; ++l) {
+            a.lng[l] = e->d_ln + (size_t)l * e->HP;
+            a.lnb[l] = e->d_ln + (size_t)(c.n_layers + l) * e->HP;
+        }
     }
     a.consts = e->d_consts;
     a.state = d_state; a.state_stride = stride;
@@ -366,7 +467,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     a.hidden = c.hidden; a.act = c.activation; a.ln = c.layer_norm; a.cost = c.cost;
     if (e->PL > 0) {
         if (!e->has_policy) return fail(BCMPC_ERR_STATE, "bcmpc_set_policy has not been called");
-        if (c.cost != BCMPC_COST_CHEETAH) return fail(BCMPC_ERR_UNSUPPORTED, "policy engines need the fused cost");
+        if (c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_UNSUPPORTED, "policy engines need the fused cost");
         for (int l = 0; l <= e->PL; ++l) {
             const size_t end = l < e->PL ? e->pw_off[l + 1] : e->pw_floats;
             a.pwbytes[l] = (int32_t)((end - e->pw_off[l]) * sizeof(float));
@@ -393,6 +494,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         m.costs = d_costs; m.actions = d_actions; m.consts = e->d_consts; m.out = d_result;
         m.act_out = e->PL > 0 ? e->d_first : nullptr;
         m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
+        m.maximize = c.cost == BCMPC_COST_REWARD;
         HIP_TRY(launch_argmin(m, st));
     }
     HIP_TRY(hipEventRecord(e->ev[2], st));
@@ -414,7 +516,7 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
                      int64_t cand_offset, bcmpc_result* out, double* costs_out) {
     if (!e || !state || !out) return fail(BCMPC_ERR_ARG, "null argument");
     const bcmpc_config& c = e->cfg;
-    if (c.cost != BCMPC_COST_CHEETAH) return fail(BCMPC_ERR_ARG, "get_action needs the fused cheetah cost");
+    if (c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "get_action needs a fused objective (cheetah cost or learned reward)");
     HIP_TRY(hipSetDevice(c.device));
     HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
     const double* d_act = nullptr;

@@ -38,6 +38,10 @@ struct RolloutArgs {
     double explore;
     double* act_out;                         // [act_out_steps][K][A] f64 actions actually rolled out, or nullptr
     int32_t act_out_steps;
+    // learned-reward net (NNDynamicsRewardModel, dynamics.py:121-238); model == BCMPC_MODEL_REWARD
+    int32_t model;
+    double mean_reward, std_reward;          // dynamics.py:236 denomalize
+    const double* gpow;                      // [H] gamma**h (controllers.py:139)
 };
 constexpr int kPolParams = 96;
 
@@ -51,11 +55,12 @@ struct ArgminArgs {
     int64_t cand_offset;
     int64_t K;
     int32_t A;
+    int32_t maximize;        // np.argmax (learned reward, controllers.py:152) instead of np.argmin
 };
 
 int max_waves_per_block(int hidden_padded, int n_layers);
 hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st);
-size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_padded, int policy_layers);
+size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_padded, int policy_layers, int model);
 hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 

@@ -317,7 +317,8 @@ __global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
     __shared__ int64_t si[16];
     Best best{__builtin_inf(), INT64_MAX};
     for (int64_t i = threadIdx.x; i < a.K; i += blockDim.x) {
-        const Best c{a.costs[i], i};
+        const double v = a.costs[i];
+        const Best c{a.maximize ? -v : v, i};      // argmax(x) == argmin(-x), NaN-first and ties alike
         if (better(c, best)) best = c;
     }
 #pragma unroll
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
         }
         bcmpc_result* out = a.out;
         out->best_index = a.cand_offset + best.i;
-        out->best_cost = best.c;
+        out->best_cost = a.maximize ? -best.c : best.c;
         for (int j = 0; j < BCMPC_MAX_ACTION; ++j) out->first_action[j] = 0.0;
         if (best.i < a.K) {
             for (int j = 0; j < a.A; ++j) {

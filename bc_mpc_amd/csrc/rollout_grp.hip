@@ -55,8 +55,9 @@ namespace bcmpc {
 #ifndef GRP_LDS_PAD
 #define GRP_LDS_PAD 0
 #endif
-constexpr int grp_waves_per_eu(int HP, int NW, int PHP = 0) {
-    return PHP > 0 ? (HP >= 512 ? 2 : 3)              // fused policy: more live state per wave
+constexpr int grp_waves_per_eu(int HP, int NW, int PHP = 0, bool RW = false) {
+    return RW ? (NW == 8 ? 4 : 2)                      // reward net: 2 groups/CU (LDS), all resident
+         : PHP > 0 ? (NW == 8 ? 4 : HP >= 512 ? 2 : 3)  // fused policy: more live state per wave
          : NW == 2 ? 2
          : NW == 8 ? (HP >= 768 ? 3 : 4)
          : (HP >= 768 ? 2 : HP >= 512 ? GRP_WPE512 : 4);
@@ -93,12 +94,17 @@ __device__ __forceinline__ void mm_slab(__amdgpu_buffer_rsrc_t rs, int wbase, in
 }
 
 // group LayerNorm of the wave's TW activated tiles (tf.contrib.layers.layer_norm,
-// dynamics.py:68-69): mean / variance over the true hidden width, across waves.
-template <int TW, int NW>
-__device__ __forceinline__ void group_layer_norm(f4 (&v)[TW], int tile0, const float* __restrict__ g,
+// dynamics.py:68-69): mean / variance over the true hidden width, across the
+// SEGW waves of the wave's LN segment (SEGW = NW: one LayerNorm over the whole
+// layer; SEGW = NW/2: the reward net's two heads, each normalised on its own,
+// dynamics.py:160,165).  tile0 indexes gamma/beta, ltile0 is the tile index
+// inside the segment (pad mask).
+template <int TW, int NW, int SEGW = NW>
+__device__ __forceinline__ void group_layer_norm(f4 (&v)[TW], int tile0, int ltile0, const float* __restrict__ g,
                                                  const float* __restrict__ bta, int hidden, float* red,
                                                  int w, int lane) {
     const int q = lane >> 4, m = lane & 15;
+    const int seg0 = (w / SEGW) * SEGW;
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < TW; ++j)
@@ -110,7 +116,7 @@ __device__ __forceinline__ void group_layer_norm(f4 (&v)[TW], int tile0, const f
     __syncthreads();
     float tot = 0.f;
 #pragma unroll
-    for (int k = 0; k < NW; ++k) tot += red[k * 16 + m];
+    for (int k = 0; k < SEGW; ++k) tot += red[(seg0 + k) * 16 + m];
     const float mean = tot / (float)hidden;
     float ss = 0.f;
 #pragma unroll
@@ -118,7 +124,7 @@ __device__ __forceinline__ void group_layer_norm(f4 (&v)[TW], int tile0, const f
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float d = v[j][r] - mean;
-            ss += (16 * (tile0 + j) + 4 * q + r < hidden) ? d * d : 0.f;
+            ss += (16 * (ltile0 + j) + 4 * q + r < hidden) ? d * d : 0.f;
         }
     ss += __shfl_xor(ss, 16);
     ss += __shfl_xor(ss, 32);
@@ -126,7 +132,7 @@ __device__ __forceinline__ void group_layer_norm(f4 (&v)[TW], int tile0, const f
     __syncthreads();
     float vs = 0.f;
 #pragma unroll
-    for (int k = 0; k < NW; ++k) vs += red[(NW + k) * 16 + m];
+    for (int k = 0; k < SEGW; ++k) vs += red[(NW + seg0 + k) * 16 + m];
     const float rs = 1.0f / sqrtf(vs / (float)hidden + 1e-12f);
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
@@ -149,6 +155,73 @@ __host__ __device__ constexpr int grp_slab_bytes() {
     return grp_slab_tiles(HP / 16, NW) * 64 * 16 + 2 * NW * 16 * 4;   // tiles + LN reduction area
 }
 
+// Layer 0 [S+A -> TW tiles] from registers: x0 holds the two input tiles
+// (rows 16v+4q+r); ring holds u-step 0's fragments (prefetched by the caller).
+template <int TW>
+__device__ __forceinline__ void layer0_mfma(__amdgpu_buffer_rsrc_t rs0, f4 (&ring)[TW], const float (&x0)[2][4],
+                                            f4 (&acc)[TW], int w, int lane) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[j][r], x0[u][r], acc[j], 0, 0, 0);
+        if (u == 0) {
+#pragma unroll
+            for (int j = 0; j < TW; ++j) ring[j] = wload(rs0, lane * 16, (w * 2 + 1) * TW * 1024 + j * 1024);
+        }
+    }
+}
+
+// Output layer [last hidden -> NOUT tiles], u (K) split over the group.  The
+// K-split gives wave w exactly the u-steps of the hidden tiles it produced
+// itself ([w*TW, (w+1)*TW)), so its B operands are its own activation
+// registers x[] -- the last hidden layer never goes through the slab.  The NW
+// partial tiles are then added in fixed wave order through the slab
+// (deterministic), leaving the pre-bias result in every wave.  `ring` holds the
+// first u-step's fragments (out_prefetch), issued before the epilogue.
+template <int NOUT>
+__device__ __forceinline__ void out_prefetch(__amdgpu_buffer_rsrc_t rs, f4 (&ring)[NOUT], int u0, int lane) {
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) ring[k] = wload(rs, lane * 16, (u0 * NOUT + k) * 1024);
+}
+
+template <int TW, int NW, int NOUT>
+__device__ __forceinline__ void group_out(__amdgpu_buffer_rsrc_t rs, f4 (&ring)[NOUT], const f4 (&x)[TW],
+                                          f4 (&o)[NOUT], f4* slab, int w, int lane) {
+    f4 po[NOUT];
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) po[k] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < TW; ++j) {
+        f4 nx[NOUT];
+        if (j + 1 < TW) {
+#pragma unroll
+            for (int k = 0; k < NOUT; ++k) nx[k] = wload(rs, lane * 16, ((w * TW + j + 1) * NOUT + k) * 1024);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < NOUT; ++k)
+                po[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[k][r], x[j][r], po[k], 0, 0, 0);
+        if (j + 1 < TW) {
+#pragma unroll
+            for (int k = 0; k < NOUT; ++k) ring[k] = nx[k];
+        }
+    }
+    if constexpr (!GRP_DIAG_NOBAR) __syncthreads();       // every wave is done reading the slab
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) slab[(NOUT * w + k) * 64 + lane] = po[k];
+    if constexpr (!GRP_DIAG_NOBAR) __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) o[k] = slab[k * 64 + lane];
+#pragma unroll
+    for (int g = 1; g < NW; ++g)                        // fixed summation order
+#pragma unroll
+        for (int k = 0; k < NOUT; ++k) o[k] += slab[(NOUT * g + k) * 64 + lane];
+}
+
 // One dense stack of the block, all layers fp32 MFMA.  Layer 0 reads its two
 // input tiles from registers (x0); hidden layers read the shared slab; each
 // wave owns TW = T/NW output tiles; the output layer (NOUT tiles) is K-split
@@ -169,27 +242,16 @@ template <int T, int NW, int NOUT, int ACT, bool LN>
 __device__ __forceinline__ void group_mlp(const StackView& sv, f4 (&ring)[T / NW], const float (&x0)[2][4],
                                           f4 (&o)[NOUT], f4* slab, float* red, int w, int lane) {
     constexpr int TW = T / NW;          // output tiles per wave
-    constexpr int UO = T / NW;          // output-layer u-steps per wave
     const int q = lane >> 4;
-    const int voff = lane * 16;
     const int tile0 = w * TW;
     // ---- layer 0 from registers: ring holds u-step 0 (prefetched by the caller) ----
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(sv.w[0], sv.wbytes[0]);
     f4 acc[TW];
 #pragma unroll
     for (int j = 0; j < TW; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < TW; ++j)
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[j][r], x0[u][r], acc[j], 0, 0, 0);
-        if (u == 0) {
-#pragma unroll
-            for (int j = 0; j < TW; ++j) ring[j] = wload(rs0, voff, (w * 2 + 1) * TW * 1024 + j * 1024);
-        }
-    }
+    layer0_mfma<TW>(rs0, ring, x0, acc, w, lane);
+    const __amdgpu_buffer_rsrc_t rso = layer_rsrc(sv.w[sv.L], sv.wbytes[sv.L]);
+    f4 v[TW];
     for (int l = 0; l < sv.L; ++l) {
         if (l > 0) {
             // ---- hidden layer l: [h -> h] from the slab ----
@@ -198,32 +260,73 @@ __device__ __forceinline__ void group_mlp(const StackView& sv, f4 (&ring)[T / NW
             mm_slab<TW, (TW >= 16 ? 1 : 2)>(layer_rsrc(sv.w[l], sv.wbytes[l]), w * T * TW * 1024, 0, T, slab, acc,
                                            lane);
         }
-        // bias + activation (+ LN) in registers, then hand over through the slab
-        f4 v[TW];
+        // bias + activation (+ LN) in registers
 #pragma unroll
         for (int j = 0; j < TW; ++j) v[j] = bias_act<ACT>(acc[j], sv.bias + l * T * 16, tile0 + j, q);
-        if constexpr (LN) group_layer_norm<TW, NW>(v, tile0, sv.lng[l], sv.lnb[l], sv.hidden, red, w, lane);
-        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // every wave is done reading the slab
+        if constexpr (LN) group_layer_norm<TW, NW>(v, tile0, tile0, sv.lng[l], sv.lnb[l], sv.hidden, red, w, lane);
+        if (l + 1 < sv.L) {                             // hand over through the slab
+            if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // every wave is done reading the slab
+#pragma unroll
+            for (int j = 0; j < TW; ++j) slab[(tile0 + j) * 64 + lane] = v[j];
+            if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // new activations visible
+        }
+    }
+    // ---- output layer: [h -> NOUT tiles] from this wave's own tiles, K-split ----
+    f4 oring[NOUT];
+    out_prefetch<NOUT>(rso, oring, w * TW, lane);
+    group_out<TW, NW, NOUT>(rso, oring, v, o, slab, w, lane);
+}
+
+// Reward net of NNDynamicsRewardModel.build_network (dynamics.py:150-177), same
+// work split: trunk [S+A -> h] (T tiles) from registers; both heads' hidden
+// layers as ONE [h -> 2h] layer (host-concatenated kernels dense_1 | dense_3,
+// 2T tiles: waves [0, NW/2) own the delta head, [NW/2, NW) the reward head, each
+// half LayerNorm'd on its own); then one block-diagonal [2h -> 32] output layer
+// (rows 0..S-1 = dense_2 from the delta half, row S = dense_4 from the reward
+// half), K-split over the group and fed from the head registers, so the 2h head
+// activations never touch LDS.  Every head neuron is computed exactly once.
+template <int T, int NW, bool LN>
+__device__ __forceinline__ void group_mlp_rw(const StackView& sv, f4 (&ring)[T / NW], const float (&x0)[2][4],
+                                             f4 (&o)[2], f4* slab, float* red, int w, int lane) {
+    constexpr int TW = T / NW;          // trunk tiles per wave
+    constexpr int TW2 = 2 * T / NW;     // head tiles per wave
+    static_assert(NW % 2 == 0 && (2 * T) % NW == 0, "heads must split evenly over the group");
+    const int q = lane >> 4;
+    const int tile0 = w * TW;
+    const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(sv.w[0], sv.wbytes[0]);
+    {
+        f4 acc[TW];
+#pragma unroll
+        for (int j = 0; j < TW; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
+        layer0_mfma<TW>(rs0, ring, x0, acc, w, lane);
+        f4 v[TW];
+#pragma unroll
+        for (int j = 0; j < TW; ++j) v[j] = bias_act<BCMPC_ACT_TANH>(acc[j], sv.bias, tile0 + j, q);
+        if constexpr (LN) group_layer_norm<TW, NW>(v, tile0, tile0, sv.lng[0], sv.lnb[0], sv.hidden, red, w, lane);
+        __syncthreads();
 #pragma unroll
         for (int j = 0; j < TW; ++j) slab[(tile0 + j) * 64 + lane] = v[j];
-        if constexpr (!GRP_DIAG_NOBAR) __syncthreads();   // new activations visible
+        __syncthreads();
     }
-    // ---- output layer: [h -> NOUT tiles], u split over the group ----
-    f4 po[NOUT];
+    {
+        const int htile0 = w * TW2;                     // first head tile of this wave (0..2T)
+        f4 acc[TW2];
 #pragma unroll
-    for (int k = 0; k < NOUT; ++k) po[k] = (f4){0.f, 0.f, 0.f, 0.f};
-    mm_slab<NOUT, (UO % 2 == 0) ? 2 : 1>(layer_rsrc(sv.w[sv.L], sv.wbytes[sv.L]), 0, w * UO, (w + 1) * UO, slab, po,
-                                         lane);
-    if constexpr (!GRP_DIAG_NOBAR) __syncthreads();       // done reading activations
+        for (int j = 0; j < TW2; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
+        mm_slab<TW2, 1>(layer_rsrc(sv.w[1], sv.wbytes[1]), w * T * TW2 * 1024, 0, T, slab, acc,
+                                          lane);
+        f4 v[TW2];
 #pragma unroll
-    for (int k = 0; k < NOUT; ++k) slab[(NOUT * w + k) * 64 + lane] = po[k];
-    if constexpr (!GRP_DIAG_NOBAR) __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NOUT; ++k) o[k] = slab[k * 64 + lane];
-#pragma unroll
-    for (int g = 1; g < NW; ++g)                        // fixed summation order
-#pragma unroll
-        for (int k = 0; k < NOUT; ++k) o[k] += slab[(NOUT * g + k) * 64 + lane];
+        for (int j = 0; j < TW2; ++j) v[j] = bias_act<BCMPC_ACT_TANH>(acc[j], sv.bias + T * 16, htile0 + j, q);
+        const __amdgpu_buffer_rsrc_t rso = layer_rsrc(sv.w[2], sv.wbytes[2]);
+        f4 oring[2];
+        out_prefetch<2>(rso, oring, htile0, lane);
+        if constexpr (LN)
+            group_layer_norm<TW2, NW, NW / 2>(v, htile0, htile0 - (w >= NW / 2 ? T : 0), sv.lng[1], sv.lnb[1],
+                                              sv.hidden, red, w, lane);
+        // ---- block-diagonal output [2h -> S+1] from this wave's own head tiles ----
+        group_out<TW2, NW, 2>(rso, oring, v, o, slab, w, lane);
+    }
 }
 
 template <int T, int NW>
@@ -244,15 +347,25 @@ __device__ __forceinline__ float rng_normal(uint64_t seed, uint64_t g, int h, in
     return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
 }
 
-template <int HP, int ACT, bool LN, int NW, int PHP>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(grp_waves_per_eu(HP, NW, PHP), 8)))
+// Dynamics-net shape facts shared by the kernel and its launcher.
+//   RW = false: NNDynamicsModel, L hidden layers of HP, output [HP -> S]
+//   RW = true : NNDynamicsRewardModel, trunk HP + heads 2*HP, output [2HP -> S+1]
+// bias rows (LB x HP floats, then 32 output-bias floats) and the widest slab layer.
+__host__ __device__ constexpr int grp_bias_rows(int L, bool RW) { return RW ? 3 : L; }
+__host__ __device__ constexpr int grp_widest_tiles(int HP, int PHP, bool) {
+    return (HP > PHP ? HP : PHP) / 16;    // the reward heads (2*HP) stay in registers
+}
+
+template <int HP, int ACT, bool LN, int NW, int PHP, bool RW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(grp_waves_per_eu(HP, NW, PHP, RW), 8)))
 void rollout_grp(const RolloutArgs a) {
-    constexpr int T = HP / 16;          // hidden tiles of the dynamics MLP
+    constexpr int T = HP / 16;          // hidden tiles of the dynamics MLP (reward net: of the trunk)
     constexpr int TW = T / NW;
     constexpr int TP = PHP / 16;        // hidden tiles of the fused policy MLP (0: none)
     constexpr int TPW = (TP > 0 ? TP : NW) / NW;
-    constexpr int TMAX = T > TP ? T : TP;
+    constexpr int TMAX = grp_widest_tiles(HP, PHP, RW);
     static_assert(T % NW == 0 && (TP == 0 || TP % NW == 0), "hidden tiles must split evenly over the group");
+    static_assert(!RW || ACT == BCMPC_ACT_TANH, "the reward net is tanh (dynamics.py:150)");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
@@ -262,22 +375,29 @@ void rollout_grp(const RolloutArgs a) {
     const int64_t cand = (int64_t)blockIdx.x * 16 + m;
     const bool valid = cand < a.K;
     const int S = a.S, A = a.A, L = a.L;
+    const int LB = grp_bias_rows(L, RW);
 
     // ---- per-block parameters in LDS: consts (f64), biases, policy params ----
     double* C = reinterpret_cast<double*>(lds);
     float* Bl = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kConstRows * kConstCols * 8);
     for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
-    for (int l = 0; l < L; ++l)
-        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i];
-    for (int i = threadIdx.x; i < 32; i += blockDim.x) Bl[L * HP + i] = a.b[L][i];
-    float* Pb = Bl + L * HP + 32;                       // policy: [PL][PHP] hidden biases, then params
+    if constexpr (RW) {                                 // [trunk HP][heads 2HP][out 32]
+        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[i] = a.b[0][i];
+        for (int i = threadIdx.x; i < 2 * HP; i += blockDim.x) Bl[HP + i] = a.b[1][i];
+    } else {
+        for (int l = 0; l < L; ++l)
+            for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i];
+    }
+    float* const Bout = Bl + LB * HP;
+    for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[RW ? 2 : L][i];
+    float* Pb = Bout + 32;                              // policy: [PL][PHP] hidden biases, then params
     const int PL = a.pL;
     if constexpr (TP > 0) {
         for (int l = 0; l < PL; ++l)
             for (int i = threadIdx.x; i < PHP; i += blockDim.x) Pb[l * PHP + i] = a.pb[l][i];
         for (int i = threadIdx.x; i < kPolParams; i += blockDim.x) Pb[PL * PHP + i] = a.pparams[i];
     }
-    f4* slab = reinterpret_cast<f4*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP) + pol_param_bytes(PL, PHP));
+    f4* slab = reinterpret_cast<f4*>(reinterpret_cast<char*>(lds) + param_bytes(LB, HP) + pol_param_bytes(PL, PHP));
     float* red = reinterpret_cast<float*>(slab + grp_slab_tiles(TMAX, NW) * 64);
     for (int i = threadIdx.x; i < 64; i += blockDim.x) slab[TMAX * 64 + i] = (f4){0.f, 0.f, 0.f, 0.f};
     if constexpr (GRP_STAGGER > 0) {            // de-phase co-resident groups (speed only)
@@ -304,7 +424,9 @@ void rollout_grp(const RolloutArgs a) {
                 if (d < S) a.traj[cand * S + d] = s[v][r];
             }
     }
-    double cost = 0.0;   // trajectory_cost = 0 (cost_functions.py:60)
+    // cheetah: trajectory_cost = 0 (cost_functions.py:60); reward: the running
+    // np.sum over steps of reward * gamma**i (controllers.py:139,150)
+    double cost = 0.0;
     const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
     // uniform draw j of step h: the caller's [H,K,A] array (np.random.uniform, controllers.py:53/191) or Philox
     auto fetch_uniform = [&](int h, int j) -> double {
@@ -386,7 +508,8 @@ void rollout_grp(const RolloutArgs a) {
                 x0[v][r] = xv;
             }
         f4 o[2];
-        group_mlp<T, NW, 2, ACT, LN>(dyn, ring, x0, o, slab, red, w, lane);
+        if constexpr (RW) group_mlp_rw<T, NW, LN>(dyn, ring, x0, o, slab, red, w, lane);
+        else group_mlp<T, NW, 2, ACT, LN>(dyn, ring, x0, o, slab, red, w, lane);
 
         // ---- cheetah penalties on the current state (cost_functions.py:16-26) ----
         double pen = 0.0;
@@ -398,7 +521,7 @@ void rollout_grp(const RolloutArgs a) {
         // ---- de-normalise + residual (dynamics.py:113,116), f64, no FMA, in place ----
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
-            const f4 bv = *reinterpret_cast<const f4*>(Bl + L * HP + 16 * v + 4 * q);
+            const f4 bv = *reinterpret_cast<const f4*>(Bout + 16 * v + 4 * q);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int d = 16 * v + 4 * q + r;
@@ -409,8 +532,19 @@ void rollout_grp(const RolloutArgs a) {
                 }
             }
         }
-        // ---- progress term + trajectory sum (cost_functions.py:28, :59-63) ----
-        if (a.cost == BCMPC_COST_CHEETAH) {
+        if constexpr (RW) {
+            // ---- learned reward (dynamics.py:236) * gamma**h, running sum (controllers.py:139,150) ----
+            float nr = 0.f;                                // output row S: tile S>>4, lane group (S&15)>>2, reg S&3
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (v == (S >> 4) && r == (S & 3)) nr = o[v][r];
+            nr = __shfl(nr, m + 16 * ((S & 15) >> 2)) + Bout[S];
+            const double rw = __dadd_rn(__dmul_rn((double)nr, a.std_reward), a.mean_reward);
+            cost = __dadd_rn(cost, __dmul_rn(rw, a.gpow[h]));
+        } else if (a.cost == BCMPC_COST_CHEETAH) {
+            // ---- progress term + trajectory sum (cost_functions.py:28, :59-63) ----
             const double score = __dsub_rn(pen, __ddiv_rn(__dsub_rn(s[1][1], s17), 0.01));
             cost = __dadd_rn(cost, score);
         }
@@ -428,40 +562,58 @@ void rollout_grp(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
-template <int HP, int ACT, bool LN, int NW, int PHP>
+template <int HP, int ACT, bool LN, int NW, int PHP, bool RW>
 static hipError_t launch_grp_t(const RolloutArgs& a, hipStream_t st) {
-    constexpr int TMAX = (HP > PHP ? HP : PHP) / 16;
-    const size_t lds = (size_t)param_bytes(a.L, HP) + pol_param_bytes(a.pL, PHP) +
+    constexpr int TMAX = grp_widest_tiles(HP, PHP, RW);
+    const size_t lds = (size_t)param_bytes(grp_bias_rows(a.L, RW), HP) + pol_param_bytes(a.pL, PHP) +
                        (size_t)grp_slab_tiles(TMAX, NW) * 64 * 16 + 2 * NW * 16 * 4 + GRP_LDS_PAD;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)rollout_grp<HP, ACT, LN, NW, PHP>,
+        hipError_t e = hipFuncSetAttribute((const void*)rollout_grp<HP, ACT, LN, NW, PHP, RW>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int64_t blocks = (a.K + 15) / 16;
-    hipLaunchKernelGGL((rollout_grp<HP, ACT, LN, NW, PHP>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
+    hipLaunchKernelGGL((rollout_grp<HP, ACT, LN, NW, PHP, RW>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
     return hipGetLastError();
 }
 
 template <int HP, int NW, int PHP>
 static hipError_t launch_grp_act(const RolloutArgs& a, hipStream_t st) {
-    if (a.ln) return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, true, NW, PHP>(a, st)
-                                             : launch_grp_t<HP, BCMPC_ACT_TANH, true, NW, PHP>(a, st);
-    return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, false, NW, PHP>(a, st)
-                                   : launch_grp_t<HP, BCMPC_ACT_TANH, false, NW, PHP>(a, st);
+    if (a.model == BCMPC_MODEL_REWARD) {               // tanh two-head net (dynamics.py:150-177)
+        if constexpr ((NW == 4 || NW == 8) && HP >= 128 && HP <= 512)
+            return a.ln ? launch_grp_t<HP, BCMPC_ACT_TANH, true, NW, PHP, true>(a, st)
+                        : launch_grp_t<HP, BCMPC_ACT_TANH, false, NW, PHP, true>(a, st);
+        return hipErrorInvalidValue;
+    }
+    if (a.ln) return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, true, NW, PHP, false>(a, st)
+                                             : launch_grp_t<HP, BCMPC_ACT_TANH, true, NW, PHP, false>(a, st);
+    return a.act == BCMPC_ACT_RELU ? launch_grp_t<HP, BCMPC_ACT_RELU, false, NW, PHP, false>(a, st)
+                                   : launch_grp_t<HP, BCMPC_ACT_TANH, false, NW, PHP, false>(a, st);
 }
 
 template <int NW>
 static hipError_t launch_grp_nw(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
-    if (a.pL > 0) {   // fused policy: NW = 4 only, policy hidden padded to 128
-        if constexpr (NW == 4) {
+    if (a.model == BCMPC_MODEL_REWARD) {               // trunk hidden padded to 128 / 256 / 512
+        if constexpr (NW == 4 || NW == 8) {
+            if (a.pL > 0 && a.phidden_padded != 128) return hipErrorInvalidValue;
+            switch (hidden_padded) {
+                case 128: return a.pL > 0 ? launch_grp_act<128, NW, 128>(a, st) : launch_grp_act<128, NW, 0>(a, st);
+                case 256: return a.pL > 0 ? launch_grp_act<256, NW, 128>(a, st) : launch_grp_act<256, NW, 0>(a, st);
+                case 512: return a.pL > 0 ? launch_grp_act<512, NW, 128>(a, st) : launch_grp_act<512, NW, 0>(a, st);
+                default: return hipErrorInvalidValue;
+            }
+        }
+        return hipErrorInvalidValue;
+    }
+    if (a.pL > 0) {   // fused policy: NW = 4 / 8, policy hidden padded to 128
+        if constexpr (NW == 4 || NW == 8) {
             if (a.phidden_padded != 128) return hipErrorInvalidValue;
             switch (hidden_padded) {
-                case 128: return launch_grp_act<128, 4, 128>(a, st);
-                case 256: return launch_grp_act<256, 4, 128>(a, st);
-                case 512: return launch_grp_act<512, 4, 128>(a, st);
+                case 128: return launch_grp_act<128, NW, 128>(a, st);
+                case 256: return launch_grp_act<256, NW, 128>(a, st);
+                case 512: return launch_grp_act<512, NW, 128>(a, st);
                 default: return hipErrorInvalidValue;
             }
         }
@@ -484,10 +636,13 @@ static hipError_t launch_grp_nw(const RolloutArgs& a, int hidden_padded, hipStre
     }
 }
 
-size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_padded, int policy_layers) {
-    const int tmax = (hidden_padded > policy_hidden_padded ? hidden_padded : policy_hidden_padded) / 16;
-    return (size_t)param_bytes(n_layers, hidden_padded) + pol_param_bytes(policy_layers, policy_hidden_padded) +
-           (size_t)grp_slab_tiles(tmax, nw) * 64 * 16 + 2 * nw * 16 * 4;
+size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_padded, int policy_layers,
+                     int model) {
+    const bool rw = model == BCMPC_MODEL_REWARD;
+    const int tmax = grp_widest_tiles(hidden_padded, policy_hidden_padded, rw);
+    return (size_t)param_bytes(grp_bias_rows(n_layers, rw), hidden_padded) +
+           pol_param_bytes(policy_layers, policy_hidden_padded) + (size_t)grp_slab_tiles(tmax, nw) * 64 * 16 +
+           2 * nw * 16 * 4;
 }
 
 hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st) {

@@ -1,4 +1,4 @@
-"""NNDynamicsModel weight container (dynamics.py:7-119 API) for the engine.
+"""NNDynamicsModel / NNDynamicsRewardModel weight containers (dynamics.py:7-238 API).
 
 The reference builds a TF1 graph (dynamics.py:54-71) whose variables the
 rollout engine must read.  This class is the MI355X-side container: the
@@ -118,5 +118,104 @@ class NNDynamicsModel():
         return d_traj[1].cpu().numpy()
 
     def fit(self, data):  # dynamics.py:81-104
+        raise NotImplementedError("dynamics training is outside the rollout engine (SURVEY 8f rank 4); "
+                                  "fit elsewhere and call load_weights()")
+
+
+class NNDynamicsRewardModel():
+    """Two-head learned-reward net (dynamics.py:121-238 API) for the engine.
+
+    Same constructor as the reference (no n_layers / size / activation: the net
+    is hard-wired to a 500-wide tanh trunk and two 500-wide tanh heads,
+    dynamics.py:150-177; ``size`` is exposed for smaller test nets).  Weights
+    are held in TF creation order dense .. dense_4 (+ LayerNorm, _1, _2).
+    ``predict`` returns ``(next_state [K,S] f64, reward [K,1] f64)`` computed by
+    the HIP kernel (one horizon step, per-candidate states)."""
+
+    def __init__(self,
+                 env,
+                 normalization,
+                 batch_size,
+                 iterations,
+                 learning_rate,
+                 sess=None,
+                 layer_norm: bool = False,
+                 size: int = 500,
+                 seed: int = 0,
+                 device: Optional[int] = None):
+        import torch
+        self.env = env
+        S = int(np.prod(env.observation_space.shape))
+        A = int(np.prod(env.action_space.shape))
+        self.state_dim, self.action_dim, self.size = S, A, int(size)
+        self.layer_norm = bool(layer_norm)
+        (self.mean_obs, self.std_obs, self.mean_action, self.std_action, self.mean_reward, self.std_reward,
+         self.mean_nxt_state, self.std_nxt_state, self.mean_deltas, self.std_deltas) = normalization
+        self.batch_size, self.iterations, self.learning_rate, self.sess = batch_size, iterations, learning_rate, sess
+        self.device = device
+        h = self.size
+        shapes = [(S + A, h), (h, h), (h, S), (h, h), (h, 1)]
+        g = torch.Generator().manual_seed(seed)
+        self.kernels = [(torch.rand(*sh, generator=g) * 2 - 1) * float(np.sqrt(6.0 / sum(sh))) for sh in shapes]
+        self.biases = [torch.zeros(sh[1]) for sh in shapes]
+        self.ln_gamma = [torch.ones(h) for _ in range(3)] if self.layer_norm else None
+        self.ln_beta = [torch.zeros(h) for _ in range(3)] if self.layer_norm else None
+        self.version = 1
+        self._engines = {}
+
+    def load_weights(self, kernels: Sequence, biases: Sequence, ln_gamma: Optional[Sequence] = None,
+                     ln_beta: Optional[Sequence] = None) -> None:
+        """Replace the weights (TF order dense .. dense_4); bumps ``version``."""
+        import torch
+        if len(kernels) != 5 or len(biases) != 5:
+            raise ValueError("expected 5 kernels and biases (dense .. dense_4)")
+        for i, (k, b) in enumerate(zip(kernels, biases)):
+            k = torch.as_tensor(np.asarray(k, dtype=np.float32))
+            b = torch.as_tensor(np.asarray(b, dtype=np.float32))
+            if k.shape != self.kernels[i].shape or b.shape != self.biases[i].shape:
+                raise ValueError(f"layer {i}: shape {tuple(k.shape)} != {tuple(self.kernels[i].shape)}")
+            self.kernels[i], self.biases[i] = k.clone(), b.clone()
+        if self.layer_norm:
+            if ln_gamma is None or ln_beta is None or len(ln_gamma) != 3 or len(ln_beta) != 3:
+                raise ValueError("layer_norm reward model needs 3 ln_gamma / ln_beta arrays")
+            self.ln_gamma = [torch.as_tensor(np.asarray(x, dtype=np.float32)).clone() for x in ln_gamma]
+            self.ln_beta = [torch.as_tensor(np.asarray(x, dtype=np.float32)).clone() for x in ln_beta]
+        self.version += 1
+
+    def mlp_spec(self) -> MLPSpec:
+        f = lambda t: t.detach().cpu().numpy().astype(np.float32)  # noqa: E731
+        return MLPSpec([f(k) for k in self.kernels], [f(b) for b in self.biases], "tanh",
+                       [f(x) for x in self.ln_gamma] if self.layer_norm else None,
+                       [f(x) for x in self.ln_beta] if self.layer_norm else None, model="reward")
+
+    def normalization(self) -> List[np.ndarray]:
+        return [self.mean_obs, self.std_obs, self.mean_action, self.std_action, self.mean_reward,
+                self.std_reward, self.mean_nxt_state, self.std_nxt_state, self.mean_deltas, self.std_deltas]
+
+    # dynamics.py:225-238
+    def predict(self, unnormalized_state, unnormalized_action):
+        import torch
+        s = np.ascontiguousarray(unnormalized_state, dtype=np.float64)
+        a = np.ascontiguousarray(unnormalized_action, dtype=np.float64)
+        if s.ndim != 2 or a.ndim != 2 or s.shape[0] != a.shape[0]:
+            raise ValueError("predict expects states [K, S] and actions [K, A]")
+        K = s.shape[0]
+        dev_index = self.device if self.device is not None else torch.cuda.current_device()
+        eng = self._engines.get(K)
+        if eng is None:
+            eng = RolloutEngine(self.state_dim, self.action_dim, self.size, 2, "tanh", self.layer_norm, 1, K,
+                                device=dev_index, cost="reward", model="reward")
+            self._engines[K] = eng
+        eng.set_weights(self.mlp_spec(), self.normalization(), self.version)
+        dev = torch.device("cuda", dev_index)
+        d_s = torch.from_numpy(s).to(dev)
+        d_a = torch.from_numpy(a).to(dev).reshape(1, K, self.action_dim)
+        d_traj = torch.empty((2, K, self.state_dim), dtype=torch.float64, device=dev)
+        d_r = torch.empty(K, dtype=torch.float64, device=dev)        # reward * gamma**0
+        eng.rollout_async(d_s.data_ptr(), self.state_dim, d_a.data_ptr(), 0, 0, d_r.data_ptr(), d_traj.data_ptr(),
+                          None, torch.cuda.current_stream(dev).cuda_stream)
+        return d_traj[1].cpu().numpy(), d_r.cpu().numpy().reshape(K, 1)
+
+    def fit(self, data):  # dynamics.py:179-223
         raise NotImplementedError("dynamics training is outside the rollout engine (SURVEY 8f rank 4); "
                                   "fit elsewhere and call load_weights()")

@@ -20,16 +20,22 @@ _ACT = {"tanh": _lib.ACT_TANH, "relu": _lib.ACT_RELU}
 @dataclass
 class MLPSpec:
     """Dense stack in TF layout: kernels[l] is ``[in, out]`` (tf.layers.dense,
-    dynamics.py:67,70), biases[l] ``[out]``; LN params per hidden layer."""
+    dynamics.py:67,70), biases[l] ``[out]``; LN params per hidden layer.
+
+    ``model="reward"``: the two-head NNDynamicsRewardModel net (dynamics.py:150-177),
+    kernels in TF creation order dense (trunk), dense_1 (delta hidden), dense_2
+    (delta out), dense_3 (reward hidden), dense_4 (reward out [h, 1]); LN params
+    LayerNorm (trunk), LayerNorm_1 (delta), LayerNorm_2 (reward); tanh."""
     kernels: List[np.ndarray]
     biases: List[np.ndarray]
     activation: str = "tanh"
     ln_gamma: Optional[List[np.ndarray]] = None
     ln_beta: Optional[List[np.ndarray]] = None
+    model: str = "delta"
 
     @property
     def n_layers(self) -> int:
-        return len(self.kernels) - 1
+        return 2 if self.model == "reward" else len(self.kernels) - 1
 
     @property
     def hidden(self) -> int:
@@ -90,7 +96,8 @@ class RolloutEngine:
     def __init__(self, state_dim: int, action_dim: int, hidden: int, n_layers: int,
                  activation: str, layer_norm: bool, horizon: int, num_paths: int,
                  device: int = 0, cost: str = "cheetah", kernel: Optional[str] = None,
-                 policy_hidden: int = 0, policy_layers: int = 0, policy_mode: str = "explore"):
+                 policy_hidden: int = 0, policy_layers: int = 0, policy_mode: str = "explore",
+                 model: str = "delta"):
         self._lib = _lib.load()
         if activation not in _ACT:
             raise ValueError(f"unsupported activation {activation!r} (tanh | relu)")
@@ -99,7 +106,11 @@ class RolloutEngine:
         cfg.activation = _ACT[activation]
         cfg.layer_norm = int(bool(layer_norm))
         cfg.horizon = int(horizon)
-        cfg.cost = _lib.COST_CHEETAH if cost == "cheetah" else _lib.COST_NONE
+        costs = {"cheetah": _lib.COST_CHEETAH, "none": _lib.COST_NONE, "reward": _lib.COST_REWARD}
+        models = {"delta": _lib.MODEL_DELTA, "reward": _lib.MODEL_REWARD}
+        if cost not in costs or model not in models:
+            raise ValueError(f"cost must be one of {sorted(costs)}, model one of {sorted(models)}")
+        cfg.cost, cfg.model = costs[cost], models[model]
         cfg.num_paths = int(num_paths)
         cfg.precision = _lib.PREC_FP32
         cfg.device = int(device)
@@ -117,19 +128,24 @@ class RolloutEngine:
         self.state_dim, self.action_dim = state_dim, action_dim
         self.hidden, self.n_layers, self.activation = hidden, n_layers, activation
         self.layer_norm, self.horizon, self.num_paths = bool(layer_norm), horizon, num_paths
-        self.device, self.cost = device, cost
+        self.device, self.cost, self.model = device, cost, model
         self.policy_hidden, self.policy_layers, self.policy_mode = policy_hidden, policy_layers, policy_mode
         self._keep = []
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, spec: MLPSpec, normalization: Sequence, version: int) -> None:
         """Re-sync hook; idempotent on ``version``."""
-        if spec.n_layers != self.n_layers or spec.hidden != self.hidden:
+        if spec.model != self.model or spec.n_layers != self.n_layers or spec.hidden != self.hidden:
             raise ValueError("weight shapes do not match the engine configuration")
         ks = [_f32(k) for k in spec.kernels]
         bs = [_f32(b) for b in spec.biases]
         S, A, h = self.state_dim, self.action_dim, self.hidden
-        exp = [(S + A, h)] + [(h, h)] * (self.n_layers - 1) + [(h, S)]
+        if self.model == "reward":
+            exp = [(S + A, h), (h, h), (h, S), (h, h), (h, 1)]
+        else:
+            exp = [(S + A, h)] + [(h, h)] * (self.n_layers - 1) + [(h, S)]
+        if len(ks) != len(exp) or len(bs) != len(exp):
+            raise ValueError(f"expected {len(exp)} dense layers, got {len(ks)} kernels / {len(bs)} biases")
         for k, b, e in zip(ks, bs, exp):
             if k.shape != e or b.shape != (e[1],):
                 raise ValueError(f"kernel {k.shape}/bias {b.shape} != expected {e}")
@@ -144,6 +160,9 @@ class RolloutEngine:
                 raise ValueError("engine built with layer_norm but weights have no LN params")
             gs = [_f32(g) for g in spec.ln_gamma]
             bts = [_f32(b) for b in spec.ln_beta]
+            n_ln = 3 if self.model == "reward" else self.n_layers
+            if len(gs) != n_ln or len(bts) != n_ln or any(x.shape != (h,) for x in gs + bts):
+                raise ValueError(f"expected {n_ln} LayerNorm gamma/beta pairs of shape ({h},)")
             garr = (FP * len(gs))(*[g.ctypes.data_as(FP) for g in gs])
             btarr = (FP * len(bts))(*[b.ctypes.data_as(FP) for b in bts])
             w.ln_gamma, w.ln_beta = garr, btarr
@@ -156,6 +175,12 @@ class RolloutEngine:
                 raise ValueError(f"normalization vector of shape {x.shape}, expected ({n},)")
         (w.mean_obs, w.std_obs, w.mean_action, w.std_action, w.mean_deltas, w.std_deltas) = [_dp(x) for x in stats]
         keep.append(stats)
+        if self.model == "reward":      # dynamics.py:236 (mean_reward / std_reward: one value each)
+            rstats = [_f64(normalization[4]).reshape(-1), _f64(normalization[5]).reshape(-1)]
+            if any(x.shape != (1,) for x in rstats):
+                raise ValueError("mean_reward / std_reward must hold exactly one value")
+            w.mean_reward, w.std_reward = _dp(rstats[0]), _dp(rstats[1])
+            keep.append(rstats)
         _lib.check(self._lib.bcmpc_set_weights(self._h, ctypes.byref(w), ctypes.c_uint64(version)))
 
     def set_policy(self, spec: PolicySpec, explore: float, version: int) -> None:
@@ -184,6 +209,10 @@ class RolloutEngine:
         out = np.empty((self.num_paths, self.action_dim), dtype=np.float64)
         _lib.check(self._lib.bcmpc_first_actions(self._h, _dp(out)))
         return out
+
+    def set_discount(self, gamma: float) -> None:
+        """MPCcontrollerReward.gamma (controllers.py:139): step h's reward is scaled by gamma**h."""
+        _lib.check(self._lib.bcmpc_set_discount(self._h, ctypes.c_double(float(gamma))))
 
     @property
     def weights_version(self) -> int:

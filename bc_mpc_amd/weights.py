@@ -14,7 +14,12 @@ runs the MLP on the GPU, so it needs the weights.  Supported containers:
    op types.  Its ``fit`` (dynamics.py:81) is wrapped to bump a version stamp
    so weights are re-synced after every refit (train_mpc_ppo.py:279).
 
-Normalization stats are the attributes set at dynamics.py:41.
+The learned-reward net of ``NNDynamicsRewardModel`` (dynamics.py:121-238) is
+recognised by its shape -- five dense layers in TF creation order, the last
+``[h, 1]`` (dense_4, the reward output) -- and read into an ``MLPSpec`` with
+``model="reward"``.
+
+Normalization stats are the attributes set at dynamics.py:41 / :143.
 """
 from __future__ import annotations
 
@@ -50,6 +55,16 @@ def _act_name(act) -> str:
     raise ValueError(f"unsupported activation {act!r}")
 
 
+def is_reward_net(kernels) -> bool:
+    """dense, dense_1, dense_2, dense_3, dense_4 of NNDynamicsRewardModel.build_network
+    (dynamics.py:150-177): trunk [S+A,h], two [h,h] head layers, outputs [h,S] and [h,1]."""
+    if len(kernels) != 5:
+        return False
+    sh = [tuple(np.shape(k)) for k in kernels]
+    h = sh[0][1]
+    return sh[1] == (h, h) and sh[3] == (h, h) and sh[2][0] == h and sh[4] == (h, 1)
+
+
 def _tf_weights(dyn_model) -> MLPSpec:  # pragma: no cover - TF1 is absent in this image
     import tensorflow as tf
     scope = getattr(dyn_model, "scope", "NNDynamicsModel")
@@ -69,7 +84,8 @@ def _tf_weights(dyn_model) -> MLPSpec:  # pragma: no cover - TF1 is absent in th
     b = [by_name[f"{scope}/LayerNorm{'' if i == 0 else f'_{i}'}/beta:0"] for i in lns] or None
     ops = {op.type for op in dyn_model.sess.graph.get_operations() if op.name.startswith(scope + "/dense")}
     act = "tanh" if "Tanh" in ops else "relu"
-    return MLPSpec(kernels, biases, act, g, b)
+    model = "reward" if hasattr(dyn_model, "reward_predict") and is_reward_net(kernels) else "delta"
+    return MLPSpec(kernels, biases, act, g, b, model=model)
 
 
 def _install_fit_hook(dyn_model) -> None:
@@ -94,9 +110,11 @@ def extract(dyn_model) -> Tuple[MLPSpec, List[np.ndarray], int]:
         return dyn_model.mlp_spec(), norm, int(dyn_model.version)
     w = getattr(dyn_model, "weights", None)
     if w is not None and hasattr(w, "kernels"):             # NumPy stand-ins
-        spec = MLPSpec([np.asarray(k) for k in w.kernels], [np.asarray(b) for b in w.biases],
+        kernels = [np.asarray(k) for k in w.kernels]
+        spec = MLPSpec(kernels, [np.asarray(b) for b in w.biases],
                        _act_name(getattr(w, "activation", "tanh")),
-                       getattr(w, "ln_gamma", None), getattr(w, "ln_beta", None))
+                       getattr(w, "ln_gamma", None), getattr(w, "ln_beta", None),
+                       model="reward" if is_reward_net(kernels) else "delta")
         version = getattr(dyn_model, "version", None)
         if version is None:      # no stamp: content digest (~1 MB of weights, <1 ms)
             d = hashlib.blake2b(digest_size=8)

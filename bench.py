@@ -38,37 +38,57 @@ WORKLOADS = {
     # self_exp=False, explore=0.5 (train_mpc_ppo.py:36-37,178 defaults)
     "cfg3_policy": dict(K=65536, H=20, hidden=500, L=2, act="tanh", policy=(128, 2), explore=0.5),
     "ppo_defaults": dict(K=400, H=7, hidden=256, L=2, act="relu"),
+    # MPCcontrollerReward (controllers.py:90-158) on NNDynamicsRewardModel (dynamics.py:121-238): tanh trunk 500,
+    # two 500 heads, argmax of sum_h reward * gamma**h
+    "cfg3_reward": dict(K=65536, H=20, hidden=500, L=2, act="tanh", reward=True, gamma=0.99),
+    # MPCcontrollerPolicyNetReward (controllers.py:289-363) at cfg3 dims, self_exp=False explore=0.5
+    "cfg3_polrew": dict(K=65536, H=20, hidden=500, L=2, act="tanh", reward=True, policy=(128, 2), explore=0.5),
+    # run.sh's active recipe: --LEARN_REWARD=True --SELFEXP=True --mpc_horizon=30, simulated_paths 400
+    # (train_mpc_ppo.py:71): MPCcontrollerPolicyNetReward with the stochastic policy
+    "runsh_recipe": dict(K=400, H=30, hidden=500, L=2, act="tanh", reward=True, policy=(128, 2), explore=0.5,
+                         policy_mode="stochastic"),
 }
 S_DIM, A_DIM = 20, 6
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix, v_mfma_f32_16x16x4_f32
 HBM_PEAK_GBS = 8000.0
 
 
-def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None):
+def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None, reward=False):
     """Algorithmic MLP FLOPs per candidate-step: 2*[(S+A)h + (L-1)h^2 + hS]
+    (reward net, dynamics.py:167-174: 2*[(S+A)h + 2h^2 + hS + h])
     (+ the policy stack 2*[S*ph + (PL-1)ph^2 + ph*A] when fused)."""
-    f = 2 * ((S + A) * hidden + (L - 1) * hidden * hidden + hidden * S)
+    if reward:
+        f = 2 * ((S + A) * hidden + 2 * hidden * hidden + hidden * S + hidden)
+    else:
+        f = 2 * ((S + A) * hidden + (L - 1) * hidden * hidden + hidden * S)
     if policy:
         ph, pl = policy
         f += 2 * (S * ph + (pl - 1) * ph * ph + ph * A)
     return f
 
 
-def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5):
+def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5, gamma=1.0):
     """The oracle (NumPy restatement of the reference path, kind "port") timed on
     the host cores over a bounded sample of the same workload."""
     from oracle import mpc_oracle as orc
+    reward = isinstance(spec_w, orc.RewardMLPWeights)
     try:
         from threadpoolctl import threadpool_info
         threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    dyn = orc.NumpyDynamics(spec_w, norm)
+    dyn = orc.NumpyRewardDynamics(spec_w, norm) if reward else orc.NumpyDynamics(spec_w, norm)
     Ks = min(8192, K_full)
     rs = np.random.RandomState(0)
+    low, high = -np.ones(A_DIM), np.ones(A_DIM)
     done, calls, t0 = 0, 0, time.perf_counter()
     while True:
-        if pol is None:
+        if reward and pol is None:        # MPCcontrollerReward body (env.sample stand-in: one uniform draw)
+            orc.reward_rollout(dyn, state, rs.uniform(low, high, (H, Ks, A_DIM)), gamma)
+        elif reward:
+            orc.policy_reward_get_action(dyn, orc.NumpyPolicy(orc.PolicyWeights(*pol)), state, H, Ks, low, high,
+                                         explore, rng=rs)
+        elif pol is None:
             orc.get_action(dyn, state, H, Ks, -np.ones(A_DIM), np.ones(A_DIM), rng=rs)
         else:
             orc.policy_get_action(dyn, orc.NumpyPolicy(orc.PolicyWeights(*pol)), state, H, Ks, -np.ones(A_DIM),
@@ -122,21 +142,28 @@ def main():
     offset = rank * K
 
     # synthetic inputs: glorot kernels, 0.1 N biases, synthetic stats/state
-    rs = np.random.RandomState(1000)
-    dims = [S_DIM + A_DIM] + [hidden] * L + [S_DIM]
+    reward = bool(wl.get("reward"))
+    if reward:   # dense, dense_1 (delta hidden), dense_2 (delta out), dense_3 (reward hidden), dense_4 (reward out)
+        shapes = [(S_DIM + A_DIM, hidden), (hidden, hidden), (hidden, S_DIM), (hidden, hidden), (hidden, 1)]
+    else:
+        dims = [S_DIM + A_DIM] + [hidden] * L + [S_DIM]
+        shapes = list(zip(dims[:-1], dims[1:]))
     kernels, biases = [], []
-    for i in range(len(dims) - 1):
+    for i, (fi, fo) in enumerate(shapes):
         r = np.random.RandomState(1000 + i)
-        lim = np.sqrt(6.0 / (dims[i] + dims[i + 1]))
-        kernels.append(r.uniform(-lim, lim, (dims[i], dims[i + 1])).astype(np.float32))
-        biases.append((0.1 * r.standard_normal(dims[i + 1])).astype(np.float32))
+        lim = np.sqrt(6.0 / (fi + fo))
+        kernels.append(r.uniform(-lim, lim, (fi, fo)).astype(np.float32))
+        biases.append((0.1 * r.standard_normal(fo)).astype(np.float32))
     r7 = np.random.RandomState(7)
     mean_obs = 0.1 * r7.standard_normal(S_DIM)
     std_obs = np.abs(r7.standard_normal(S_DIM)) * 0.5 + 0.2
     mean_d = 0.005 * r7.standard_normal(S_DIM)
     std_d = 0.05 * (np.abs(r7.standard_normal(S_DIM)) + 0.2)
-    norm = [mean_obs, std_obs, np.zeros(A_DIM), np.full(A_DIM, 1 / np.sqrt(3)), np.zeros(1), np.zeros(1),
+    norm = [mean_obs, std_obs, np.zeros(A_DIM), np.full(A_DIM, 1 / np.sqrt(3)), np.full(1, 0.3), np.full(1, 1.2),
             mean_obs, std_obs, mean_d, std_d]
+    model = "reward" if reward else "delta"
+    cost = "reward" if reward else "cheetah"
+    gamma = float(wl.get("gamma", 1.0))
     state = mean_obs + 0.5 * std_obs * np.random.RandomState(11).standard_normal(S_DIM)
 
     policy = wl.get("policy")
@@ -154,11 +181,13 @@ def main():
         pol_arrays = (pks, pbs, mean_obs.astype(np.float32), (std_obs + 0.05).astype(np.float32),
                       np.full(A_DIM, -0.5, np.float32))
         eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, policy_hidden=ph,
-                            policy_layers=pl, policy_mode="explore")
+                            policy_layers=pl, policy_mode=wl.get("policy_mode", "explore"), cost=cost, model=model)
         eng.set_policy(PolicySpec(*pol_arrays), wl["explore"], 1)
     else:
-        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local)
-    eng.set_weights(MLPSpec(kernels, biases, act), norm, 1)
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, cost=cost, model=model)
+    eng.set_weights(MLPSpec(kernels, biases, act, model=model), norm, 1)
+    if reward:
+        eng.set_discount(gamma)
     info = eng.info()
     kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
                    "group8": "rollout_grp<NW=8>"}.get(
@@ -180,7 +209,8 @@ def main():
         best_i = int(raw[:8].view(np.int64)[0])
         best_c = float(raw[8:16].view(np.float64)[0])
         first = raw[16:16 + 8 * A_DIM].view(np.float64).copy()
-        return bdist.allgather_minloc(True, best_c, best_i, first, A_DIM)
+        sign = -1.0 if reward else 1.0                  # argmax of the reward == argmin of its negation
+        return bdist.allgather_minloc(True, sign * best_c, best_i, first, A_DIM)
 
     for i in range(args.warmup):
         step(i)
@@ -205,7 +235,7 @@ def main():
 
     total_cand_steps = K * world * H * args.steps
     value = total_cand_steps / elapsed
-    fpcs = flop_per_cand_step(hidden, L, policy=policy)
+    fpcs = flop_per_cand_step(hidden, L, policy=policy, reward=reward)
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
     achieved_tflops = K * H * fpcs / kern_avg_s / 1e12
     out = {
@@ -220,10 +250,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (HalfCheetah dims s=20,a=6; random-init 2x500 tanh dynamics MLP; "
+        "data": f"synthetic (HalfCheetah dims s=20,a=6; random-init {'two-head reward net' if reward else 'dynamics MLP'}; "
                 f"actions {'resident in HBM as [H,K,6] f64' if args.actions == 'hbm' else 'drawn in-kernel (Philox)'})",
         "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
-                               f"{L}x{hidden} {act}" + (f" + fused policy {policy[1]}x{policy[0]} tanh" if policy else "")
+                               + (f"reward net {hidden} trunk + 2x{hidden} heads tanh, argmax sum r*{gamma}^h"
+                                  if reward else f"{L}x{hidden} {act}")
+                               + (f" + fused policy {policy[1]}x{policy[0]} tanh "
+                                  f"({wl.get('policy_mode', 'explore')})" if policy else "")
                                + ", fp32 MFMA, 1 RCCL all-gather min-loc per step",
                    "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
                    "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
@@ -248,10 +281,12 @@ def main():
             pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import mpc_oracle as orc
-        w = orc.MLPWeights(kernels, biases, act)
-        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K,
-                                           f"{L}x{hidden} {act}" + (f" + policy {policy}" if policy else ""),
-                                           pol_arrays, wl.get("explore", 0.5))
+        w = orc.RewardMLPWeights(kernels, biases) if reward else orc.MLPWeights(kernels, biases, act)
+        net = (f"reward net {hidden}" if reward else f"{L}x{hidden} {act}") + (f" + policy {policy}" if policy else "")
+        if policy and wl.get("policy_mode") == "stochastic":
+            net += " (oracle policy in its deterministic explore branch: TF's sampler is not restatable)"
+        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, net,
+                                           pol_arrays, wl.get("explore", 0.5), gamma)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -6,6 +6,11 @@
  *     -> H x dynamics.NNDynamicsModel.predict       (dynamics.py:106-119, MLP dynamics.py:54-71)
  *     -> cost_functions.trajectory_cost_fn(cheetah) (cost_functions.py:9-30, :59-63)
  *     -> np.argmin + first action                   (controllers.py:82-85)
+ * and its siblings on the same engine:
+ *   MPCcontrollerPolicyNet.get_action      (controllers.py:160-237; policy fused, bcmpc_set_policy)
+ *   MPCcontrollerReward.get_action         (controllers.py:90-158; NNDynamicsRewardModel,
+ *                                           dynamics.py:121-238; argmax of the discounted reward)
+ *   MPCcontrollerPolicyNetReward.get_action (controllers.py:289-363)
  * The reference binds that path in-process from Python; the host mirror
  * (bc_mpc_amd/controllers.py) binds these symbols through ctypes.
  *
@@ -23,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BCMPC_ABI_VERSION 1
+#define BCMPC_ABI_VERSION 2
 #define BCMPC_MAX_LAYERS 8      /* hidden layers supported (dynamics.py:66 n_layers) */
 #define BCMPC_MAX_STATE 32      /* S: observation dim (HalfCheetah: 20, cheetah_env.py:21-27) */
 #define BCMPC_MAX_INPUT 32      /* S + A (dynamics.py:26 concat) */
@@ -44,9 +49,18 @@ typedef enum bcmpc_activation {  /* dynamics.py:60 activation / train_mpc_ppo.py
 } bcmpc_activation;
 
 typedef enum bcmpc_cost {
-    BCMPC_COST_CHEETAH = 0,     /* fused cheetah_cost_fn (cost_functions.py:10-30) */
-    BCMPC_COST_NONE = 1         /* no fused cost: caller scores the trajectory     */
+    BCMPC_COST_CHEETAH = 0,     /* fused cheetah_cost_fn (cost_functions.py:10-30), argmin  */
+    BCMPC_COST_NONE = 1,        /* no fused cost: caller scores the trajectory              */
+    BCMPC_COST_REWARD = 2       /* learned reward: sum_h reward_h * gamma**h, ARGMAX
+                                   (controllers.py:139,150-152); needs BCMPC_MODEL_REWARD  */
 } bcmpc_cost;
+
+typedef enum bcmpc_model {      /* which dynamics net (dynamics.py)                          */
+    BCMPC_MODEL_DELTA = 0,      /* NNDynamicsModel: L x dense(h) -> dense(S) (:54-71)        */
+    BCMPC_MODEL_REWARD = 1      /* NNDynamicsRewardModel: tanh trunk dense(h) -> {delta head
+                                   dense(h) -> dense(S), reward head dense(h) -> dense(1)},
+                                   LayerNorm per head (:150-177); n_layers must be 2         */
+} bcmpc_model;
 
 typedef enum bcmpc_precision {
     BCMPC_PREC_FP32 = 0         /* f32 MLP on v_mfma_f32_16x16x4_f32 (exact f32 fma chain) */
@@ -83,12 +97,18 @@ typedef struct bcmpc_config {
     int32_t policy_hidden;  /* 0: MPCcontroller; >0: MPCcontrollerPolicyNet policy width (hid_size) */
     int32_t policy_layers;  /* policy hidden layers (num_hid_layers, train_mpc_ppo.py:178)         */
     int32_t policy_mode;    /* bcmpc_policy_mode                                                   */
-    int32_t reserved[4];  /* must be zero                                          */
+    int32_t model;        /* bcmpc_model                                           */
+    int32_t reserved[3];  /* must be zero                                          */
 } bcmpc_config;
 
 /* Replaces the state NNDynamicsModel holds: TF variables
  * NNDynamicsModel/dense{,_1,..}/{kernel,bias} (+ LayerNorm/{gamma,beta}) and
- * the normalization stats of dynamics.py:41.  Host pointers, copied. */
+ * the normalization stats of dynamics.py:41.  Host pointers, copied.
+ * BCMPC_MODEL_REWARD (dynamics.py:150-177) passes the variables in TF creation
+ * order: kernels/biases = dense (trunk [S+A,h]), dense_1 (delta hidden [h,h]),
+ * dense_2 (delta out [h,S]), dense_3 (reward hidden [h,h]), dense_4 (reward out
+ * [h,1]); ln_gamma/ln_beta = LayerNorm (trunk), LayerNorm_1 (delta), LayerNorm_2
+ * (reward); plus mean_reward / std_reward (dynamics.py:143, 236). */
 typedef struct bcmpc_weights {
     const float* const* kernels;   /* L+1 arrays, kernel[l] is [in, out] row-major  */
     const float* const* biases;    /* L+1 arrays of length out                      */
@@ -100,12 +120,16 @@ typedef struct bcmpc_weights {
     const double* std_action;      /* A */
     const double* mean_deltas;     /* S */
     const double* std_deltas;      /* S */
+    const double* mean_reward;     /* 1 (BCMPC_MODEL_REWARD only, else NULL) */
+    const double* std_reward;      /* 1 (BCMPC_MODEL_REWARD only, else NULL) */
 } bcmpc_weights;
 
 /* Output of one control step (controllers.py:82-85). */
 typedef struct bcmpc_result {
-    int64_t best_index;                       /* global candidate index, np.argmin semantics */
-    double best_cost;                         /* costs[best_index] (controllers.py:83)       */
+    int64_t best_index;                       /* global candidate index, np.argmin semantics
+                                                 (np.argmax for BCMPC_COST_REWARD)           */
+    double best_cost;                         /* costs[best_index] (controllers.py:83); the best
+                                                 discounted reward sum for BCMPC_COST_REWARD */
     double first_action[BCMPC_MAX_ACTION];    /* action_paths[0, best_index, :]              */
 } bcmpc_result;
 
@@ -138,6 +162,10 @@ uint64_t bcmpc_weights_version(const bcmpc_engine* eng);
 /* Policy weights for MPCcontrollerPolicyNet engines (config.policy_hidden > 0). */
 int bcmpc_set_policy(bcmpc_engine* eng, const bcmpc_policy* p, uint64_t version);
 
+/* MPCcontrollerReward.gamma (controllers.py:99,139): step h's reward is scaled by
+ * gamma**h (host pow, as Python's float ** int).  Default 1.0.  Reward engines only. */
+int bcmpc_set_discount(bcmpc_engine* eng, double gamma);
+
 /* env.action_space.low / .high (controllers.py:53). Defaults: [-1, 1]^A. */
 int bcmpc_set_action_bounds(bcmpc_engine* eng, const double* low, const double* high);
 
@@ -148,7 +176,8 @@ int bcmpc_set_action_bounds(bcmpc_engine* eng, const double* low, const double* 
  *              Philox4x32-10 keyed by (seed, cand_offset + k, h, j)
  *   cand_offset : global index of this device's first candidate (multi-GPU shard)
  *   out      : best index (global) / cost / first action
- *   costs_out: optional K doubles, per-candidate trajectory cost (cost_functions.py:59-63) */
+ *   costs_out: optional K doubles, per-candidate trajectory cost (cost_functions.py:59-63),
+ *              or discounted reward sum (BCMPC_COST_REWARD, controllers.py:150) */
 int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actions,
                      uint64_t seed, int64_t cand_offset, bcmpc_result* out, double* costs_out);
 
@@ -160,7 +189,7 @@ int bcmpc_first_actions(bcmpc_engine* eng, double* out);
  *   d_state      : device, S doubles, or [K, S] when state_stride == S (predict mode,
  *                  dynamics.py:106 on per-candidate states)
  *   d_actions    : device [H, K, A] doubles, or NULL => device RNG
- *   d_costs      : device K doubles (required when cost == CHEETAH)
+ *   d_costs      : device K doubles (required when cost == CHEETAH or REWARD)
  *   d_traj       : device [H+1, K, S] doubles or NULL (states_paths_all, controllers.py:65-74)
  *   d_result     : device bcmpc_result or NULL (argmin + first action)
  *   stream       : hipStream_t the launches are enqueued on, used verbatim (NULL is HIP's
