@@ -9,11 +9,12 @@ The compute path is libbcmpc.so (HIP, gfx950); see DESIGN.md.
 from . import _lib
 from .controllers import (Controller, MPCcontroller, MPCcontrollerPolicyNet, MPCcontrollerPolicyNetReward,
                           MPCcontrollerReward, RandomController)
+from .cem import CEMcontroller
 from .cost_functions import cheetah_cost_fn, trajectory_cost_fn
 from .engine import MLPSpec, PolicySpec, RolloutEngine, StepResult
 
 __all__ = ["Controller", "MPCcontroller", "MPCcontrollerPolicyNet", "MPCcontrollerReward",
-           "MPCcontrollerPolicyNetReward", "RandomController", "PolicySpec", "cheetah_cost_fn",
+           "MPCcontrollerPolicyNetReward", "CEMcontroller", "RandomController", "PolicySpec", "cheetah_cost_fn",
            "trajectory_cost_fn", "MLPSpec", "RolloutEngine", "StepResult"]
 
 _lib.load()   # fail loudly at import when the HIP library is missing

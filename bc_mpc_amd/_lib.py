@@ -91,6 +91,19 @@ class Policy(ctypes.Structure):
 POLICY_MODES = {"explore": 0, "stochastic": 1}
 
 
+class Cem(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_int32),
+        ("n_elite", ctypes.c_int32),
+        ("alpha", ctypes.c_double),
+        ("k_global", ctypes.c_int64),
+    ]
+
+
+class Elite(ctypes.Structure):
+    _fields_ = [("cost", ctypes.c_double), ("index", ctypes.c_int64)]
+
+
 class Result(ctypes.Structure):
     _fields_ = [
         ("best_index", ctypes.c_int64),
@@ -116,6 +129,17 @@ SIGNATURES = [
     ("bcmpc_rollout_async", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("bcmpc_cem_get_action", ctypes.c_int,
+     [ctypes.c_void_p, _DP, ctypes.POINTER(Cem), ctypes.c_uint64, _DP, _DP, ctypes.POINTER(Result)]),
+    ("bcmpc_cem_rollout_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32,
+      ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    ("bcmpc_select_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("bcmpc_cem_refit_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_double,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("bcmpc_stream", ctypes.c_void_p, [ctypes.c_void_p]),
     ("bcmpc_last_kernel_ms", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),

@@ -105,6 +105,11 @@ struct bcmpc_engine {
     // learned reward (NNDynamicsRewardModel)
     double* d_gpow = nullptr;                       // [H] gamma**h
     double mean_reward = 0.0, std_reward = 0.0;
+    // CEM (bcmpc_cem_get_action)
+    double* d_mu = nullptr;                         // [H][A] each
+    double* d_sigma = nullptr;
+    bcmpc_elite* d_elite = nullptr; int32_t elite_cap = 0;
+    int32_t* d_count = nullptr;
     double explore = 0.0;
     uint64_t pol_version = 0;
     bool has_policy = false;
@@ -265,7 +270,8 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
-                    (void*)e->d_first, (void*)e->d_gpow})
+                    (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
+                    (void*)e->d_count})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
     for (auto& ev : e->ev)
@@ -430,9 +436,18 @@ int bcmpc_set_discount(bcmpc_engine* e, double gamma) {
 
 void* bcmpc_stream(bcmpc_engine* e) { return e ? (void*)e->stream : nullptr; }
 
+struct CemLaunch {           // one CEM iteration's sampling distribution + result merge rule
+    const double* mu;
+    const double* sigma;
+    int32_t iter;
+    int32_t merge;
+    int64_t pos_base;
+};
+
 static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, const double* d_actions,
                         uint64_t seed, int64_t cand_offset, double* d_costs, double* d_traj,
-                        bcmpc_result* d_result, hipStream_t st) {
+                        bcmpc_result* d_result, hipStream_t st, const CemLaunch* cem = nullptr,
+                        bool record_events = true) {
     const bcmpc_config& c = e->cfg;
     if (!e->has_weights) return fail(BCMPC_ERR_STATE, "bcmpc_set_weights has not been called");
     if (c.num_paths == 0) return fail(BCMPC_ERR_EMPTY, "attempt to get argmin of an empty sequence");
@@ -482,23 +497,73 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.act_out = e->d_first;
         a.act_out_steps = 1;
     }
-    HIP_TRY(hipEventRecord(e->ev[0], st));
+    if (cem) {
+        if (e->kernel == BCMPC_KERNEL_SOLO || e->PL > 0)
+            return fail(BCMPC_ERR_UNSUPPORTED, "CEM runs on group-kernel engines without a policy");
+        a.cem_mu = cem->mu;
+        a.cem_sigma = cem->sigma;
+        a.cem_iter = cem->iter;
+    }
+    if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
     if (e->kernel == BCMPC_KERNEL_SOLO) {
         HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
     } else {
         HIP_TRY(launch_rollout_grp(a, e->HP, kern_waves(e->kernel), st));
     }
-    HIP_TRY(hipEventRecord(e->ev[1], st));
+    if (record_events) HIP_TRY(hipEventRecord(e->ev[1], st));
     if (d_result) {
         ArgminArgs m{};
         m.costs = d_costs; m.actions = d_actions; m.consts = e->d_consts; m.out = d_result;
         m.act_out = e->PL > 0 ? e->d_first : nullptr;
         m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
         m.maximize = c.cost == BCMPC_COST_REWARD;
+        if (cem) {
+            m.cem_mu = cem->mu; m.cem_sigma = cem->sigma; m.cem_iter = cem->iter;
+            m.merge = cem->merge; m.pos_base = cem->pos_base;
+        }
         HIP_TRY(launch_argmin(m, st));
     }
-    HIP_TRY(hipEventRecord(e->ev[2], st));
+    if (record_events) HIP_TRY(hipEventRecord(e->ev[2], st));
     e->timed = d_result != nullptr;
+    return BCMPC_OK;
+}
+
+static int cem_buffers(bcmpc_engine* e, int32_t n_elite) {
+    const size_t ha = (size_t)e->cfg.horizon * e->cfg.action_dim;
+    if (!e->d_mu) {
+        HIP_TRY(hipMalloc(&e->d_mu, ha * sizeof(double)));
+        HIP_TRY(hipMalloc(&e->d_sigma, ha * sizeof(double)));
+        HIP_TRY(hipMalloc(&e->d_count, sizeof(int32_t)));
+    }
+    if (n_elite > e->elite_cap) {
+        if (e->d_elite) (void)hipFree(e->d_elite);
+        e->d_elite = nullptr;
+        e->elite_cap = 0;
+        HIP_TRY(hipMalloc(&e->d_elite, (size_t)n_elite * sizeof(bcmpc_elite)));
+        e->elite_cap = n_elite;
+    }
+    return BCMPC_OK;
+}
+
+static int select_impl(bcmpc_engine* e, const bcmpc_elite* d_pairs, const double* d_costs, int64_t m,
+                       int64_t index_base, int32_t n_elite, bcmpc_elite* d_out, int32_t* d_count, hipStream_t st) {
+    if (n_elite < 1) return fail(BCMPC_ERR_ARG, "n_elite must be >= 1");
+    if (m < 0 || (!d_pairs && !d_costs) || !d_out || !d_count) return fail(BCMPC_ERR_ARG, "null argument");
+    SelectArgs s{};
+    s.pairs = d_pairs; s.costs = d_costs; s.m = m; s.index_base = index_base; s.n_elite = n_elite;
+    s.maximize = e->cfg.cost == BCMPC_COST_REWARD;
+    s.out = d_out; s.count = d_count;
+    HIP_TRY(launch_select(s, st));
+    return BCMPC_OK;
+}
+
+static int refit_impl(bcmpc_engine* e, const bcmpc_elite* d_elite, const int32_t* d_count, uint64_t seed,
+                      int32_t iter, double alpha, double* d_mu, double* d_sigma, hipStream_t st) {
+    if (!d_elite || !d_count || !d_mu || !d_sigma) return fail(BCMPC_ERR_ARG, "null argument");
+    RefitArgs r{};
+    r.elite = d_elite; r.count = d_count; r.mu = d_mu; r.sigma = d_sigma; r.consts = e->d_consts;
+    r.seed = seed; r.iter = iter; r.H = e->cfg.horizon; r.A = e->cfg.action_dim; r.alpha = alpha;
+    HIP_TRY(launch_refit(r, st));
     return BCMPC_OK;
 }
 
@@ -540,6 +605,71 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
     HIP_TRY(hipStreamSynchronize(e->stream));
     *out = *e->h_result;
     return BCMPC_OK;
+}
+
+int bcmpc_cem_get_action(bcmpc_engine* e, const double* state, const bcmpc_cem* p, uint64_t seed, double* mu,
+                         double* sigma, bcmpc_result* out) {
+    if (!e || !state || !p || !mu || !sigma || !out) return fail(BCMPC_ERR_ARG, "null argument");
+    const bcmpc_config& c = e->cfg;
+    if (c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "CEM needs a fused objective");
+    if (p->iterations < 1 || p->iterations > (1 << 22)) return fail(BCMPC_ERR_ARG, "iterations must be in [1, 2^22]");
+    if (p->n_elite < 1) return fail(BCMPC_ERR_ARG, "n_elite must be >= 1");
+    if (p->k_global != 0 && p->k_global != c.num_paths)
+        return fail(BCMPC_ERR_ARG, "single-device CEM: k_global must be 0 or num_paths");
+    if (c.num_paths == 0) return fail(BCMPC_ERR_EMPTY, "attempt to get argmin of an empty sequence");
+    HIP_TRY(hipSetDevice(c.device));
+    int rc = cem_buffers(e, p->n_elite);
+    if (rc != BCMPC_OK) return rc;
+    const size_t ha = (size_t)c.horizon * c.action_dim;
+    hipStream_t st = e->stream;
+    HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d_mu, mu, ha * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(e->d_sigma, sigma, ha * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(e->ev[0], st));
+    for (int it = 0; it < p->iterations; ++it) {
+        const CemLaunch cl{e->d_mu, e->d_sigma, it, it > 0, (int64_t)it * c.num_paths};
+        rc = rollout_impl(e, e->d_state, 0, nullptr, seed, 0, e->d_costs, nullptr, e->d_result, st, &cl, false);
+        if (rc != BCMPC_OK) return rc;
+        rc = select_impl(e, nullptr, e->d_costs, c.num_paths, 0, p->n_elite, e->d_elite, e->d_count, st);
+        if (rc != BCMPC_OK) return rc;
+        rc = refit_impl(e, e->d_elite, e->d_count, seed, it, p->alpha, e->d_mu, e->d_sigma, st);
+        if (rc != BCMPC_OK) return rc;
+    }
+    HIP_TRY(hipEventRecord(e->ev[1], st));
+    HIP_TRY(hipEventRecord(e->ev[2], st));
+    e->timed = true;
+    HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(mu, e->d_mu, ha * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(sigma, e->d_sigma, ha * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *out = *e->h_result;
+    return BCMPC_OK;
+}
+
+int bcmpc_cem_rollout_async(bcmpc_engine* e, const double* d_state, const double* d_mu, const double* d_sigma,
+                            uint64_t seed, int32_t iteration, int64_t cand_offset, int64_t k_global,
+                            double* d_costs, bcmpc_result* d_result, int32_t merge, void* stream) {
+    if (!e || !d_state || !d_mu || !d_sigma || !d_costs) return fail(BCMPC_ERR_ARG, "null argument");
+    if (iteration < 0 || iteration >= (1 << 22)) return fail(BCMPC_ERR_ARG, "iteration must be in [0, 2^22)");
+    if (k_global < e->cfg.num_paths + cand_offset) return fail(BCMPC_ERR_ARG, "k_global smaller than this shard's range");
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    const CemLaunch cl{d_mu, d_sigma, iteration, merge != 0, (int64_t)iteration * k_global + cand_offset};
+    return rollout_impl(e, d_state, 0, nullptr, seed, cand_offset, d_costs, nullptr, d_result, (hipStream_t)stream,
+                        &cl);
+}
+
+int bcmpc_select_async(bcmpc_engine* e, const bcmpc_elite* d_pairs, const double* d_costs, int64_t m,
+                       int64_t index_base, int32_t n_elite, bcmpc_elite* d_out, int32_t* d_count, void* stream) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    return select_impl(e, d_pairs, d_costs, m, index_base, n_elite, d_out, d_count, (hipStream_t)stream);
+}
+
+int bcmpc_cem_refit_async(bcmpc_engine* e, const bcmpc_elite* d_elite, const int32_t* d_count, uint64_t seed,
+                          int32_t iteration, double alpha, double* d_mu, double* d_sigma, void* stream) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    return refit_impl(e, d_elite, d_count, seed, iteration, alpha, d_mu, d_sigma, (hipStream_t)stream);
 }
 
 int bcmpc_last_kernel_ms(bcmpc_engine* e, float* rollout_ms, float* argmin_ms) {

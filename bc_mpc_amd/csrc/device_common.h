@@ -38,6 +38,28 @@ __device__ __forceinline__ double rng_action(uint64_t seed, uint64_t g, int h, i
     return __dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u));   // low + (high-low)*u, no FMA
 }
 
+// CEM sample (DESIGN.md "CEM"): z = Irwin-Hall(12) - 6 from three Philox blocks
+// (twelve 24-bit uniforms; their integer sum is exact, so z is exact in f64 and
+// restatable bit-for-bit), a = clip(mu + sd*z, lo, hi) with np.clip's NaN rule.
+// Counter (lo32(g), hi32(g), h, 0x40000000 | it<<8 | j<<2 | c), key = seed.
+__device__ __forceinline__ double cem_normal(uint64_t seed, uint64_t g, int h, int j, int it) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        uint32_t x[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)h,
+                         0x40000000u | ((uint32_t)it << 8) | ((uint32_t)j << 2) | (uint32_t)c};
+        philox4x32_10(x, (uint32_t)seed, (uint32_t)(seed >> 32));
+        sum += (x[0] >> 8) + (x[1] >> 8) + (x[2] >> 8) + (x[3] >> 8);
+    }
+    return __dsub_rn((double)sum * (1.0 / 16777216.0), 6.0);
+}
+
+__device__ __forceinline__ double cem_action(uint64_t seed, uint64_t g, int h, int j, int it, double mu, double sd,
+                                             double lo, double hi) {
+    const double a = __dadd_rn(mu, __dmul_rn(sd, cem_normal(seed, g, h, j, it)));
+    return a < lo ? lo : (a > hi ? hi : a);          // np.clip = minimum(maximum(a, lo), hi)
+}
+
 // ------------------------------------------------------------ activation ---
 // Branch-free tanh: odd Taylor polynomial below |x| = 0.4, else
 // 1 - 2/(1 + e^{2|x|}) with v_exp_f32 / v_rcp_f32 (<= ~4 ulp vs float64 tanh,

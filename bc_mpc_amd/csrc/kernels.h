@@ -42,6 +42,31 @@ struct RolloutArgs {
     int32_t model;
     double mean_reward, std_reward;          // dynamics.py:236 denomalize
     const double* gpow;                      // [H] gamma**h (controllers.py:139)
+    // CEM sampling (DESIGN.md "CEM"): actions = clip(mu + sigma * IrwinHall12(seed, g, h, j, iter))
+    const double* cem_mu;                    // [H][A] or nullptr
+    const double* cem_sigma;                 // [H][A]
+    int32_t cem_iter;
+};
+
+struct SelectArgs {                          // top-E of (cost, index) pairs, NaN last, ties -> lower index
+    const bcmpc_elite* pairs;                // [m] pairs (index < 0: empty), or nullptr =>
+    const double* costs;                     // [m] costs with index = index_base + i
+    int64_t m, index_base;
+    int32_t n_elite;
+    int32_t maximize;                        // learned reward: the n_elite LARGEST
+    bcmpc_elite* out;                        // [n_elite], ascending index, padded with index -1
+    int32_t* count;                          // number selected
+};
+
+struct RefitArgs {                           // per-(h, j) elite mean / std, smoothed in place
+    const bcmpc_elite* elite;
+    const int32_t* count;
+    double* mu;                              // [H][A]
+    double* sigma;
+    const double* consts;                    // action bounds (rows 6, 7)
+    uint64_t seed;
+    int32_t iter, H, A;
+    double alpha;
 };
 constexpr int kPolParams = 96;
 
@@ -56,6 +81,12 @@ struct ArgminArgs {
     int64_t K;
     int32_t A;
     int32_t maximize;        // np.argmax (learned reward, controllers.py:152) instead of np.argmin
+    // CEM: first action regenerated from the sampler; merge with the running best by stream position
+    const double* cem_mu;
+    const double* cem_sigma;
+    int32_t cem_iter;
+    int32_t merge;           // keep out's previous best unless strictly better (np.argmin over iterations)
+    int64_t pos_base;        // position of candidate 0 in the concatenated stream (iter * K_global + offset)
 };
 
 int max_waves_per_block(int hidden_padded, int n_layers);
@@ -63,5 +94,7 @@ hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per
 size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_padded, int policy_layers, int model);
 hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
+hipError_t launch_select(const SelectArgs& a, hipStream_t st);
+hipError_t launch_refit(const RefitArgs& a, hipStream_t st);
 
 }  // namespace bcmpc

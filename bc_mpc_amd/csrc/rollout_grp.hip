@@ -431,6 +431,9 @@ void rollout_grp(const RolloutArgs a) {
     // uniform draw j of step h: the caller's [H,K,A] array (np.random.uniform, controllers.py:53/191) or Philox
     auto fetch_uniform = [&](int h, int j) -> double {
         if (!valid) return 0.0;
+        if (a.cem_mu)                                   // CEM iteration: clip(mu + sigma * z) (DESIGN.md "CEM")
+            return cem_action(a.seed, gcand, h, j, a.cem_iter, a.cem_mu[h * A + j], a.cem_sigma[h * A + j],
+                              C[6 * 32 + j], C[7 * 32 + j]);
         return a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
                          : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
     };

@@ -260,6 +260,50 @@ class RolloutEngine:
             ctypes.c_void_p(d_traj) if d_traj else None, ctypes.c_void_p(d_result) if d_result else None,
             ctypes.c_void_p(stream)))
 
+    # ------------------------------------------------------------------ CEM
+    def cem_get_action(self, state, mu, sigma, iterations: int, n_elite: int, alpha: float,
+                       seed: int) -> Tuple[StepResult, np.ndarray, np.ndarray]:
+        """All CEM iterations on this device (bcmpc_cem_get_action).  ``mu``/``sigma`` are
+        ``[H, A]``; returns (result with best_index = iteration*K + candidate, mu', sigma')."""
+        st = _f64(state).reshape(-1)
+        if st.shape[0] != self.state_dim:
+            raise ValueError(f"state has {st.shape[0]} dims, expected {self.state_dim}")
+        shape = (self.horizon, self.action_dim)
+        m = np.array(mu, dtype=np.float64, copy=True).reshape(shape)
+        s = np.array(sigma, dtype=np.float64, copy=True).reshape(shape)
+        p = _lib.Cem(int(iterations), int(n_elite), float(alpha), 0)
+        res = _lib.Result()
+        _lib.check(self._lib.bcmpc_cem_get_action(self._h, _dp(st), ctypes.byref(p),
+                                                  ctypes.c_uint64(seed & (2**64 - 1)), _dp(m), _dp(s),
+                                                  ctypes.byref(res)))
+        return (StepResult(int(res.best_index), float(res.best_cost),
+                           np.array(res.first_action[: self.action_dim], dtype=np.float64)), m, s)
+
+    def cem_rollout_async(self, d_state: int, d_mu: int, d_sigma: int, seed: int, iteration: int,
+                          cand_offset: int, k_global: int, d_costs: int, d_result: Optional[int], merge: bool,
+                          stream: Optional[int] = None) -> None:
+        stream = self.stream if stream is None else stream
+        _lib.check(self._lib.bcmpc_cem_rollout_async(
+            self._h, ctypes.c_void_p(d_state), ctypes.c_void_p(d_mu), ctypes.c_void_p(d_sigma),
+            ctypes.c_uint64(seed & (2**64 - 1)), int(iteration), int(cand_offset), int(k_global),
+            ctypes.c_void_p(d_costs), ctypes.c_void_p(d_result) if d_result else None, int(bool(merge)),
+            ctypes.c_void_p(stream)))
+
+    def select_async(self, d_pairs: Optional[int], d_costs: Optional[int], m: int, index_base: int, n_elite: int,
+                     d_out: int, d_count: int, stream: Optional[int] = None) -> None:
+        stream = self.stream if stream is None else stream
+        _lib.check(self._lib.bcmpc_select_async(
+            self._h, ctypes.c_void_p(d_pairs) if d_pairs else None, ctypes.c_void_p(d_costs) if d_costs else None,
+            int(m), int(index_base), int(n_elite), ctypes.c_void_p(d_out), ctypes.c_void_p(d_count),
+            ctypes.c_void_p(stream)))
+
+    def cem_refit_async(self, d_elite: int, d_count: int, seed: int, iteration: int, alpha: float, d_mu: int,
+                        d_sigma: int, stream: Optional[int] = None) -> None:
+        stream = self.stream if stream is None else stream
+        _lib.check(self._lib.bcmpc_cem_refit_async(
+            self._h, ctypes.c_void_p(d_elite), ctypes.c_void_p(d_count), ctypes.c_uint64(seed & (2**64 - 1)),
+            int(iteration), float(alpha), ctypes.c_void_p(d_mu), ctypes.c_void_p(d_sigma), ctypes.c_void_p(stream)))
+
     @property
     def stream(self) -> int:
         return int(self._lib.bcmpc_stream(self._h) or 0)

@@ -45,6 +45,9 @@ WORKLOADS = {
     "cfg3_polrew": dict(K=65536, H=20, hidden=500, L=2, act="tanh", reward=True, policy=(128, 2), explore=0.5),
     # run.sh's active recipe: --LEARN_REWARD=True --SELFEXP=True --mpc_horizon=30, simulated_paths 400
     # (train_mpc_ppo.py:71): MPCcontrollerPolicyNetReward with the stochastic policy
+    # BASELINE cfg5: K=65536, H=50, 3x1024 tanh with the CEM outer loop (4 iterations; elites 10%, smoothing 0.1;
+    # DESIGN.md "CEM" -- the reference has no CEM).  One step = one CEMcontroller.get_action = 4 rollout passes.
+    "cfg5": dict(K=65536, H=50, hidden=1024, L=3, act="tanh", cem=dict(iterations=4, elite_frac=0.1, alpha=0.1)),
     "runsh_recipe": dict(K=400, H=30, hidden=500, L=2, act="tanh", reward=True, policy=(128, 2), explore=0.5,
                          policy_mode="stochastic"),
 }
@@ -67,7 +70,7 @@ def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None, reward=False):
     return f
 
 
-def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5, gamma=1.0):
+def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5, gamma=1.0, cem=None):
     """The oracle (NumPy restatement of the reference path, kind "port") timed on
     the host cores over a bounded sample of the same workload."""
     from oracle import mpc_oracle as orc
@@ -78,12 +81,17 @@ def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explor
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     dyn = orc.NumpyRewardDynamics(spec_w, norm) if reward else orc.NumpyDynamics(spec_w, norm)
-    Ks = min(8192, K_full)
+    Ks = min(1024 if cem else 8192, K_full)
     rs = np.random.RandomState(0)
     low, high = -np.ones(A_DIM), np.ones(A_DIM)
     done, calls, t0 = 0, 0, time.perf_counter()
     while True:
-        if reward and pol is None:        # MPCcontrollerReward body (env.sample stand-in: one uniform draw)
+        if cem:                           # the oracle's CEM loop: cem iterations x Ks x H candidate-steps
+            E = max(1, int(round(cem["elite_frac"] * Ks)))
+            orc.cem_get_action(lambda s, a: orc.rollout(dyn, s, a)[0], state, H, Ks, low, high, cem["iterations"],
+                               E, cem["alpha"], calls, np.zeros((H, A_DIM)), np.full((H, A_DIM), 0.5))
+            done += Ks * H * (cem["iterations"] - 1)
+        elif reward and pol is None:        # MPCcontrollerReward body (env.sample stand-in: one uniform draw)
             orc.reward_rollout(dyn, state, rs.uniform(low, high, (H, Ks, A_DIM)), gamma)
         elif reward:
             orc.policy_reward_get_action(dyn, orc.NumpyPolicy(orc.PolicyWeights(*pol)), state, H, Ks, low, high,
@@ -201,8 +209,39 @@ def main():
     d_costs = torch.empty(K, dtype=torch.float64, device=dev)
     d_res = torch.zeros(__import__("ctypes").sizeof(L_.Result), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    cem = wl.get("cem")
+    iters = cem["iterations"] if cem else 1
+    if cem:
+        from bc_mpc_amd.cem import cem_multi_rank
+        n_elite = max(1, int(round(cem["elite_frac"] * K * world)))
+        mu0, sd0 = np.zeros((H, A_DIM)), np.full((H, A_DIM), 0.5)
+
+        class _Shard:                                   # cem._EngineShard around this engine
+            device = dev
+
+            def rollout(self, d_state, d_mu, d_sigma, seed, it, lo, k_global, d_costs, d_res, merge):
+                eng.cem_rollout_async(d_state.data_ptr(), d_mu.data_ptr(), d_sigma.data_ptr(), seed, it, lo,
+                                      k_global, d_costs.data_ptr(), d_res.data_ptr(), merge, stream.cuda_stream)
+
+            def select(self, d_pairs, d_costs, m, index_base, n, d_out, d_count):
+                eng.select_async(d_pairs.data_ptr() if d_pairs is not None else None,
+                                 d_costs.data_ptr() if d_costs is not None else None, m, index_base, n,
+                                 d_out.data_ptr(), d_count.data_ptr(), stream.cuda_stream)
+
+            def refit(self, d_elite, d_count, seed, it, alpha, d_mu, d_sigma):
+                eng.cem_refit_async(d_elite.data_ptr(), d_count.data_ptr(), seed, it, alpha, d_mu.data_ptr(),
+                                    d_sigma.data_ptr(), stream.cuda_stream)
+
+    def cem_step(i):
+        if world == 1:
+            res, _, _ = eng.cem_get_action(state, mu0, sd0, iters, n_elite, cem["alpha"], 0xB0B + i)
+            return res
+        return cem_multi_rank(_Shard(), state, mu0, sd0, iters, n_elite, cem["alpha"], 0xB0B + i, offset,
+                              offset + K, K * world, A_DIM, reward)
 
     def step(i):
+        if cem:
+            return cem_step(i)
         eng.rollout_async(d_state.data_ptr(), 0, d_actions.data_ptr() if d_actions is not None else None,
                           0xB0B + i, offset, d_costs.data_ptr(), None, d_res.data_ptr(), stream.cuda_stream)
         raw = d_res.cpu().numpy()                       # D2H of the result; syncs the stream
@@ -223,7 +262,7 @@ def main():
         ts = time.perf_counter()
         step(args.warmup + i)
         step_s.append(time.perf_counter() - ts)
-        kern_ms.append(eng.last_kernel_ms()[0])
+        kern_ms.append(eng.last_kernel_ms()[0] if not (cem and world > 1) else float("nan"))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -233,13 +272,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_cand_steps = K * world * H * args.steps
+    total_cand_steps = K * world * H * iters * args.steps
     value = total_cand_steps / elapsed
     fpcs = flop_per_cand_step(hidden, L, policy=policy, reward=reward)
+    if cem and world > 1:                              # per-launch device time: the wall-clock share
+        kern_ms = [t * 1e3 for t in step_s]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
-    achieved_tflops = K * H * fpcs / kern_avg_s / 1e12
+    achieved_tflops = K * H * iters * fpcs / kern_avg_s / 1e12
     out = {
         "metric": "candidate-steps/sec (K x H per get_action), HalfCheetah dims",
+        # CEM workloads count every iteration's K x H candidate-steps (iterations x K x H per get_action)
         "value": value,
         "unit": "candidate-steps/s",
         "n_gpus": world,
@@ -257,7 +299,9 @@ def main():
                                   if reward else f"{L}x{hidden} {act}")
                                + (f" + fused policy {policy[1]}x{policy[0]} tanh "
                                   f"({wl.get('policy_mode', 'explore')})" if policy else "")
-                               + ", fp32 MFMA, 1 RCCL all-gather min-loc per step",
+                               + (f" + CEM {iters} iterations, {n_elite} elites, alpha {cem['alpha']}" if cem else "")
+                               + ", fp32 MFMA, 1 RCCL all-gather min-loc per step"
+                               + (" (+1 all-gather of the local top-E per CEM iteration)" if cem else ""),
                    "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
                    "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
                    "collective": f"{backend} all_gather min-loc, {3 + A_DIM} f64 per rank per step" if world > 1
@@ -267,7 +311,9 @@ def main():
         "kernel_ms_avg": kern_avg_s * 1e3,
         "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                     "kernel": kernel_name, "flop_per_launch": K * H * fpcs,
+                     "kernel": kernel_name + (" x CEM iterations + select/refit (HIP events around the "
+                                              "whole device-side CEM call)" if cem else ""),
+                     "flop_per_launch": K * H * fpcs,
                      "flop_per_cand_step": fpcs},
         "cpu_baseline": None,
     }
@@ -286,7 +332,7 @@ def main():
         if policy and wl.get("policy_mode") == "stochastic":
             net += " (oracle policy in its deterministic explore branch: TF's sampler is not restatable)"
         out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, net,
-                                           pol_arrays, wl.get("explore", 0.5), gamma)
+                                           pol_arrays, wl.get("explore", 0.5), gamma, cem)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

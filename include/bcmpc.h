@@ -145,6 +145,27 @@ typedef struct bcmpc_policy {
     double explore;                /* MPCcontrollerPolicyNet.explore */
 } bcmpc_policy;
 
+/* CEM outer loop (BASELINE cfg5 "CEM outer loop (4 elite iters)"; not in the reference,
+ * semantics in DESIGN.md "CEM").  Iteration i samples every candidate's actions as
+ * clip(mu + sigma * z, low, high), z = Irwin-Hall(12) - 6 from Philox keyed by
+ * (seed, global candidate, h, j, i); scores them like get_action; keeps the n_elite
+ * lowest (cost, index) (NaN last, ties -> lower index); refits mu / sigma [H][A] to
+ * the elites' mean / std (fixed reduction order) smoothed by alpha.  The answer is
+ * the first action of the best candidate over ALL iterations (np.argmin over the
+ * iteration-major concatenation of the cost vectors). */
+typedef struct bcmpc_cem {
+    int32_t iterations;   /* CEM iterations (cfg5: 4)                                   */
+    int32_t n_elite;      /* elites per iteration, over all ranks (>= 1)               */
+    double alpha;         /* new = alpha * old + (1 - alpha) * elite statistic         */
+    int64_t k_global;     /* candidates over all ranks; result positions are
+                             iteration * k_global + global index                      */
+} bcmpc_cem;
+
+typedef struct bcmpc_elite {   /* one (cost, global candidate index) record; index < 0 = empty */
+    double cost;
+    int64_t index;
+} bcmpc_elite;
+
 typedef struct bcmpc_engine bcmpc_engine;
 
 int bcmpc_abi_version(void);
@@ -197,6 +218,30 @@ int bcmpc_first_actions(bcmpc_engine* eng, double* out);
 int bcmpc_rollout_async(bcmpc_engine* eng, const double* d_state, int64_t state_stride,
                         const double* d_actions, uint64_t seed, int64_t cand_offset,
                         double* d_costs, double* d_traj, bcmpc_result* d_result, void* stream);
+
+/* CEM, single device, synchronous: all iterations on the engine's stream.
+ *   mu, sigma : host [H][A] doubles, in: the initial distribution, out: the refit one
+ *   out       : best_index = iteration * K + candidate, best_cost, first action
+ * Needs a group-kernel engine with the fused objective (cheetah cost or learned reward;
+ * for the reward objective "best" is the argmax). */
+int bcmpc_cem_get_action(bcmpc_engine* eng, const double* state, const bcmpc_cem* params, uint64_t seed,
+                         double* mu, double* sigma, bcmpc_result* out);
+
+/* CEM building blocks for multi-device runs (device pointers, stream-ordered):
+ *   cem_rollout : one iteration's sampling + rollout of this device's shard into d_costs;
+ *                 with d_result, also the shard's best, merged (merge != 0) with the
+ *                 running best already in d_result
+ *   select      : the n_elite lowest of m records -- d_pairs, or d_costs (index =
+ *                 index_base + i) when d_pairs is NULL -- written in ascending index
+ *                 order to d_out (padded with index -1), the count to d_count
+ *   cem_refit   : mu / sigma update from the selected elites (regenerated from Philox) */
+int bcmpc_cem_rollout_async(bcmpc_engine* eng, const double* d_state, const double* d_mu, const double* d_sigma,
+                            uint64_t seed, int32_t iteration, int64_t cand_offset, int64_t k_global,
+                            double* d_costs, bcmpc_result* d_result, int32_t merge, void* stream);
+int bcmpc_select_async(bcmpc_engine* eng, const bcmpc_elite* d_pairs, const double* d_costs, int64_t m,
+                       int64_t index_base, int32_t n_elite, bcmpc_elite* d_out, int32_t* d_count, void* stream);
+int bcmpc_cem_refit_async(bcmpc_engine* eng, const bcmpc_elite* d_elite, const int32_t* d_count, uint64_t seed,
+                          int32_t iteration, double alpha, double* d_mu, double* d_sigma, void* stream);
 
 /* Device stream the engine launches on (hipStream_t as void*). */
 void* bcmpc_stream(bcmpc_engine* eng);

@@ -22,6 +22,8 @@ It is a NumPy restatement of the reference path, function by function:
 * ``NumpyRewardDynamics``     <- ``dynamics.py:121-238`` (NNDynamicsRewardModel two-head net).
 * ``reward_get_action``       <- ``controllers.py:90-158`` (MPCcontrollerReward, argmax).
 * ``policy_reward_get_action``<- ``controllers.py:289-363`` (MPCcontrollerPolicyNetReward).
+* ``cem_*``                   <- no reference (BASELINE cfg5 CEM): the engine's own CEM semantics
+  (DESIGN.md "CEM"), restated exactly; parity there is self-consistency, not reference-pinned.
 
 Parity status: the controller / cost / RNG half is PINNED bit-exactly against
 fixtures produced by running the reference's own ``controllers.py`` +
@@ -490,6 +492,117 @@ def device_rng_actions(seed: int, cand_offset: int, K: int, H: int, low, high) -
                 u[:, 2 * j + p] = (a * 67108864.0 + b) / 9007199254740992.0
         out[h] = low + (high - low) * u[:, :A]
     return out
+
+
+# ----------------------------------------------------------------------------
+# CEM outer loop (BASELINE cfg5; NOT in the reference -- semantics defined in
+# DESIGN.md "CEM" and restated here exactly as the engine computes them)
+# ----------------------------------------------------------------------------
+def cem_normals(seed: int, iteration: int, cand_offset: int, K: int, H: int, A: int, index=None) -> np.ndarray:
+    """z = Irwin-Hall(12) - 6 per (h, k, j) as ``[H, K, A]`` f64: twelve 24-bit uniforms from
+    three Philox blocks, counter (lo32(g), hi32(g), h, 0x40000000 | it<<8 | j<<2 | c); the
+    integer sum is exact, so z is exact (engine: cem_normal, device_common.h).  Candidates
+    are cand_offset + [0, K), or the global indices ``index`` when given."""
+    if index is not None:
+        g = np.asarray(index, dtype=np.uint64)
+        K = g.shape[0]
+    else:
+        g = np.arange(K, dtype=np.uint64) + np.uint64(cand_offset)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    out = np.empty((H, K, A), dtype=np.float64)
+    for h in range(H):
+        for j in range(A):
+            tot = np.zeros(K, dtype=np.uint64)
+            for c in range(3):
+                w3 = 0x40000000 | (iteration << 8) | (j << 2) | c
+                r = philox4x32_10(g & _M32, g >> np.uint64(32), np.full(K, h, np.uint64),
+                                  np.full(K, w3, np.uint64), k0, k1)
+                for x in r:
+                    tot += x.astype(np.uint64) >> np.uint64(8)
+            out[h, :, j] = tot.astype(np.float64) * (1.0 / 16777216.0) - 6.0
+    return out
+
+
+def cem_actions(seed, iteration, cand_offset, K, H, mu, sigma, low, high, index=None) -> np.ndarray:
+    """``np.clip(mu + sigma * z, low, high)`` as ``[H, K, A]`` (mu, sigma: ``[H, A]``)."""
+    mu = np.asarray(mu, dtype=np.float64)
+    sigma = np.asarray(sigma, dtype=np.float64)
+    z = cem_normals(seed, iteration, cand_offset, K, H, mu.shape[1], index)
+    return np.clip(mu[:, None, :] + sigma[:, None, :] * z, np.asarray(low, np.float64), np.asarray(high, np.float64))
+
+
+def cem_select(costs, index, n_elite: int, maximize: bool = False) -> np.ndarray:
+    """The n_elite best records (stable sort: NaN last, ties to the lower index; +-0
+    equal), returned as global indices in ascending order (engine: select_kernel)."""
+    costs = np.asarray(costs, dtype=np.float64)
+    index = np.asarray(index, dtype=np.int64)
+    keep = index >= 0
+    costs, index = costs[keep], index[keep]
+    pos = np.argsort(index, kind="stable")
+    costs, index = costs[pos], index[pos]
+    obj = -costs if maximize else costs
+    order = np.argsort(obj, kind="stable")[:n_elite]
+    return np.sort(index[order])
+
+
+def _wave_sum(x: np.ndarray) -> float:
+    """Lane l adds elements l, l+64, ... in order (from 0.0); the 64 partials are then
+    combined by the xor butterfly (offsets 32, 16, ..., 1): p[:off] + p[off:2*off]."""
+    p = np.zeros(64, dtype=np.float64)
+    for start in range(0, x.shape[0], 64):
+        chunk = x[start:start + 64]
+        p[:chunk.shape[0]] = p[:chunk.shape[0]] + chunk
+    off = 32
+    while off >= 1:
+        p = p[:off] + p[off:2 * off]
+        off //= 2
+    return float(p[0])
+
+
+def cem_refit(elite_index, seed, iteration, mu, sigma, low, high, alpha: float):
+    """Elite mean / std (np.std ddof 0, two passes) per (h, j) in the engine's reduction
+    order, smoothed: new = alpha*old + (1-alpha)*stat (engine: refit_kernel)."""
+    mu = np.asarray(mu, dtype=np.float64)
+    sigma = np.asarray(sigma, dtype=np.float64)
+    n = len(elite_index)
+    if n == 0:
+        return mu.copy(), sigma.copy()
+    H, A = mu.shape
+    acts = cem_actions(seed, iteration, 0, 0, H, mu, sigma, low, high, index=elite_index)   # [H, n, A]
+    new_mu, new_sd = np.empty_like(mu), np.empty_like(sigma)
+    beta = 1.0 - alpha
+    for h in range(H):
+        for j in range(A):
+            a = acts[h, :, j]
+            mean = _wave_sum(a) / float(n)
+            d = a - mean
+            sd = np.sqrt(_wave_sum(d * d) / float(n))
+            new_mu[h, j] = alpha * mu[h, j] + beta * mean
+            new_sd[h, j] = alpha * sigma[h, j] + beta * sd
+    return new_mu, new_sd
+
+
+def cem_get_action(score, state, H: int, K: int, low, high, iterations: int, n_elite: int, alpha: float,
+                   seed: int, mu0, sigma0, maximize: bool = False):
+    """The CEM loop the engine runs (bcmpc_cem_get_action).  ``score(state, actions [H,K,A])
+    -> objective [K]`` (e.g. ``lambda s, a: rollout(dyn, s, a)[0]``).  Returns
+    ``(first_action, position, objective_concat, mu, sigma, history)`` where position
+    = iteration*K + candidate is np.argmin (np.argmax when maximize) over the
+    iteration-major concatenation, and history holds each iteration's (mu, sigma)."""
+    mu, sd = np.array(mu0, dtype=np.float64), np.array(sigma0, dtype=np.float64)
+    objs, hist = [], []
+    for it in range(iterations):
+        hist.append((mu.copy(), sd.copy()))
+        acts = cem_actions(seed, it, 0, K, H, mu, sd, low, high)
+        obj = np.asarray(score(state, acts), dtype=np.float64)
+        objs.append(obj)
+        el = cem_select(obj, np.arange(K), n_elite, maximize)
+        mu, sd = cem_refit(el, seed, it, mu, sd, low, high, alpha)
+    flat = np.concatenate(objs)
+    pos = int(np.argmax(flat) if maximize else np.argmin(flat))
+    it, i = divmod(pos, K)
+    first = cem_actions(seed, it, i, 1, 1, hist[it][0], hist[it][1], low, high)[0, 0]
+    return first, pos, flat, mu, sd, hist
 
 
 # ----------------------------------------------------------------------------
