@@ -71,6 +71,39 @@ void pack_out_rows(const float* W, int in, int out, int Tin, const int* rowmap, 
             }
 }
 
+// Split-f16 kernel (rollout_x3.hip): W [in][out] scaled by sw, every element as
+// hi = f16(w), lo = f16(w - hi), in fragment order [ws][p][j][hi|lo][lane][i],
+// t = ws*TWp + j: lane's 8 halves of tile t, k-step p are W[k][n] with
+// n = 16t + (lane&15), k = 32p + 16(i>>2) + 4(lane>>4) + (i&3) -- the k order in
+// which an output tile pair's accumulators ARE the next layer's B fragment.
+void pack_x3_layer(const float* W, int in, int out, int Pin, int Tout, int TWp, float sw, _Float16* dst) {
+    for (int t = 0; t < Tout; ++t) {
+        const int ws = t / TWp, j = t % TWp;
+        for (int p = 0; p < Pin; ++p)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int i = 0; i < 8; ++i) {
+                    const int k = 32 * p + 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3);
+                    const int n = 16 * t + (lane & 15);
+                    const float v = (k < in && n < out) ? W[(size_t)k * out + n] * sw : 0.f;
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    const size_t o = ((((size_t)ws * Pin + p) * TWp + j) * 2 * 64 + lane) * 8 + i;
+                    dst[o] = hi;
+                    dst[o + 64 * 8] = lo;
+                }
+    }
+}
+
+// power of two s with max|W| * s in [2^11, 2^12) (1 for an all-zero kernel)
+float x3_scale(const float* W, size_t n) {
+    float mx = 0.f;
+    for (size_t i = 0; i < n; ++i) mx = std::max(mx, std::fabs(W[i]));
+    if (!(mx > 0.f) || !std::isfinite(mx)) return 1.f;
+    int e = 0;
+    (void)std::frexp(mx, &e);
+    return std::ldexp(1.0f, std::max(-100, std::min(100, 12 - e)));
+}
+
 }  // namespace
 
 struct bcmpc_engine {
@@ -79,6 +112,9 @@ struct bcmpc_engine {
     int kernel = BCMPC_KERNEL_SOLO;    // resolved kernel layout
     int nw = 1;                        // waves per group (group kernels)
     int pack_tb = 4;                   // output tiles per packed block of layers 0..L-1
+    bool split = false;                // BCMPC_PREC_SPLIT_F16 (rollout_x3)
+    int nc = 0;                        // split kernel: 16-candidate columns per workgroup
+    float winv[BCMPC_MAX_LAYERS + 1]{};  // split kernel: 1 / operand scales per layer
     bool reward = false;               // BCMPC_MODEL_REWARD (NNDynamicsRewardModel)
     hipStream_t stream = nullptr;
     // device buffers
@@ -146,7 +182,19 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (c.state_dim > 31) return fail(BCMPC_ERR_UNSUPPORTED, "reward model: state_dim must be <= 31");
     }
     if (c.cost == BCMPC_COST_CHEETAH && c.state_dim < 18) return fail(BCMPC_ERR_UNSUPPORTED, "cheetah cost needs state_dim >= 18");
-    if (c.precision != BCMPC_PREC_FP32) return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32");
+    if (c.precision != BCMPC_PREC_FP32 && c.precision != BCMPC_PREC_SPLIT_F16)
+        return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32 or SPLIT_F16");
+    const bool split = c.precision == BCMPC_PREC_SPLIT_F16;
+    if (split) {
+        // f16 operands need bounded hidden activations (tanh) and the plain delta net
+        if (c.activation != BCMPC_ACT_TANH || c.layer_norm || reward || c.policy_hidden > 0)
+            return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports the tanh NNDynamicsModel without "
+                                               "LayerNorm or fused policy in this build (use FP32)");
+        if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLIT4))
+            return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4 kernels");
+    } else if (c.kernel >= BCMPC_KERNEL_SPLIT1) {
+        return fail(BCMPC_ERR_ARG, "split kernels need precision SPLIT_F16");
+    }
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (c.device < 0 || c.device >= ndev) return fail(BCMPC_ERR_ARG, "device ordinal out of range");
@@ -185,9 +233,28 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->TP = 8;
         e->PL = c.policy_layers;
     }
-    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_GROUP8) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
-    const int nw = kern_waves(kern);
-    if (kern != BCMPC_KERNEL_SOLO &&
+    if (split) {
+        // widest workgroup (most candidates per weight read) that still gives every CU work and fits LDS
+        const int64_t cols = (c.num_paths + 15) / 16;
+        int nc = c.kernel == BCMPC_KERNEL_SPLIT1 ? 1 : c.kernel == BCMPC_KERNEL_SPLIT2 ? 2
+               : c.kernel == BCMPC_KERNEL_SPLIT4 ? 4 : 0;
+        const int nwx = x3_waves(e->HP);
+        auto fits = [&](int n) { return n <= nwx && x3_lds(e->HP, c.n_layers, n) <= 160 * 1024; };
+        if (nc == 0) {
+            nc = 1;
+            for (int n : {4, 2})
+                if (fits(n) && cols >= (int64_t)n * 256) { nc = n; break; }
+        }
+        if (!fits(nc)) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "split kernel does not fit this shape"); }
+        e->split = true;
+        e->nc = nc;
+        e->kernel = nc == 1 ? BCMPC_KERNEL_SPLIT1 : nc == 2 ? BCMPC_KERNEL_SPLIT2 : BCMPC_KERNEL_SPLIT4;
+        e->nw = nwx;
+        kern = e->kernel;
+    }
+    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_SPLIT4) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
+    const int nw = split ? e->nw : kern_waves(kern);
+    if (!split && kern != BCMPC_KERNEL_SOLO &&
         (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw, e->PHP, e->PL, c.model) > 160 * 1024)) {
         if (c.kernel != BCMPC_KERNEL_AUTO) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group kernel does not fit this shape"); }
         kern = BCMPC_KERNEL_SOLO;
@@ -199,7 +266,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     }
     e->kernel = kern;
     e->nw = nw;
-    e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->T / nw;
+    e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->T / nw;   // split: output tiles per wave
     const int L = c.n_layers, T = e->T;
     size_t off = 0, boff = 0;
     if (reward) {
@@ -304,6 +371,22 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
     const int tb = e->pack_tb;
     std::vector<float> hb(rw ? 3 * (size_t)HP + 32 : (size_t)L * HP + 32, 0.f);
     std::vector<float> hln(2 * (size_t)NLN * HP, 0.f);
+    if (e->split) {
+        // same sizes as the f32 layout (4 bytes per weight: two halves)
+        _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
+        const int P = T / 2;
+        for (int l = 0; l <= L; ++l) {
+            const int in = l == 0 ? S + A : h, out = l == L ? S : h;
+            const float sw = x3_scale(w->kernels[l], (size_t)in * out);
+            if (l == 0) pack_x3_layer(w->kernels[0], in, out, 1, T, tb, sw, hh + 2 * e->w_off[0]);
+            else if (l < L) pack_x3_layer(w->kernels[l], in, out, P, T, tb, sw, hh + 2 * e->w_off[l]);
+            else pack_x3_layer(w->kernels[L], in, out, P, 2, 2, sw, hh + 2 * e->w_off[L]);
+            // layer 0's input scale is per candidate (kernel); hidden inputs are tanh * 2^12
+            e->winv[l] = (1.0f / sw) * (l == 0 ? 1.0f : 1.0f / 4096.0f);
+        }
+        for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
+        std::memcpy(hb.data() + e->b_off[L], w->biases[L], sizeof(float) * S);
+    } else {
     pack_layer(w->kernels[0], S + A, h, 2, T, tb, hw.data() + e->w_off[0]);
     if (rw) {
         // heads' hidden layers side by side: W1c[k][n] = dense_1 (n < HP) | dense_3 (n >= HP)
@@ -343,6 +426,7 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
                 std::memcpy(hln.data() + (size_t)l * HP, w->ln_gamma[l], sizeof(float) * h);
                 std::memcpy(hln.data() + (size_t)(L + l) * HP, w->ln_beta[l], sizeof(float) * h);
             }
+    }
     }
     double* C = e->h_consts;
     for (int i = 0; i < kConstCols; ++i) {
@@ -497,6 +581,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.act_out = e->d_first;
         a.act_out_steps = 1;
     }
+    for (int l = 0; l <= c.n_layers; ++l) a.winv[l] = e->winv[l];
     if (cem) {
         if (e->kernel == BCMPC_KERNEL_SOLO || e->PL > 0)
             return fail(BCMPC_ERR_UNSUPPORTED, "CEM runs on group-kernel engines without a policy");
@@ -505,7 +590,9 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.cem_iter = cem->iter;
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
-    if (e->kernel == BCMPC_KERNEL_SOLO) {
+    if (e->split) {
+        HIP_TRY(launch_rollout_x3(a, e->HP, e->nc, st));
+    } else if (e->kernel == BCMPC_KERNEL_SOLO) {
         HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
     } else {
         HIP_TRY(launch_rollout_grp(a, e->HP, kern_waves(e->kernel), st));
@@ -688,7 +775,7 @@ int bcmpc_engine_info(const bcmpc_engine* e, int32_t* hidden_padded, int64_t* pa
     if (!e) return fail(BCMPC_ERR_ARG, "null argument");
     if (hidden_padded) *hidden_padded = e->HP;
     if (packed_weight_bytes) *packed_weight_bytes = (int64_t)(e->w_floats * sizeof(float));
-    if (waves_per_block) *waves_per_block = e->kernel == BCMPC_KERNEL_SOLO ? e->wpb : kern_waves(e->kernel);
+    if (waves_per_block) *waves_per_block = e->kernel == BCMPC_KERNEL_SOLO ? e->wpb : e->nw;
     if (kernel) *kernel = e->kernel;
     return BCMPC_OK;
 }

@@ -97,7 +97,10 @@ class RolloutEngine:
                  activation: str, layer_norm: bool, horizon: int, num_paths: int,
                  device: int = 0, cost: str = "cheetah", kernel: Optional[str] = None,
                  policy_hidden: int = 0, policy_layers: int = 0, policy_mode: str = "explore",
-                 model: str = "delta"):
+                 model: str = "delta", precision: Optional[str] = None):
+        """``precision``: "fp32" (v_mfma_f32_16x16x4_f32) or "split" (f32-accurate hi/lo f16
+        operands on v_mfma_f32_16x16x32_f16, rollout_x3.hip; tanh nets without LayerNorm).
+        Default: "split" for the split* kernels, else $BCMPC_PRECISION or "fp32"."""
         self._lib = _lib.load()
         if activation not in _ACT:
             raise ValueError(f"unsupported activation {activation!r} (tanh | relu)")
@@ -112,12 +115,17 @@ class RolloutEngine:
             raise ValueError(f"cost must be one of {sorted(costs)}, model one of {sorted(models)}")
         cfg.cost, cfg.model = costs[cost], models[model]
         cfg.num_paths = int(num_paths)
-        cfg.precision = _lib.PREC_FP32
         cfg.device = int(device)
         kernel = kernel or os.environ.get("BCMPC_KERNEL", "auto")
         if kernel not in _lib.KERNELS:
             raise ValueError(f"unknown kernel {kernel!r}; one of {sorted(_lib.KERNELS)}")
         cfg.kernel = _lib.KERNELS[kernel]
+        if precision is None:
+            precision = "split" if kernel.startswith("split") else os.environ.get("BCMPC_PRECISION", "fp32")
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"unknown precision {precision!r}; one of {sorted(_lib.PRECISIONS)}")
+        cfg.precision = _lib.PRECISIONS[precision]
+        self.precision = precision
         if policy_mode not in _lib.POLICY_MODES:
             raise ValueError(f"unknown policy_mode {policy_mode!r}")
         cfg.policy_hidden, cfg.policy_layers = int(policy_hidden), int(policy_layers)

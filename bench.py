@@ -53,6 +53,10 @@ WORKLOADS = {
 }
 S_DIM, A_DIM = 20, 6
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix, v_mfma_f32_16x16x4_f32
+F16_MFMA_PEAK_TFLOPS = 2516.6     # dense f16/bf16 MFMA: 512 MAC/clk/SIMD x 1024 SIMDs x 2.4 GHz
+# split precision: every f32 product = 3 f16 MFMA passes (hi*hi + hi*lo + lo*hi), so the
+# f32-equivalent (algorithmic) ceiling is a third of the f16 peak
+SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
 
 
@@ -119,6 +123,8 @@ def main():
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
     ap.add_argument("--actions", default="hbm", choices=["hbm", "device"],
                     help="hbm: [H,K,A] f64 actions resident in HBM (parity mode input); device: in-kernel Philox")
+    ap.add_argument("--precision", default=os.environ.get("BCMPC_PRECISION", "fp32"), choices=["fp32", "split"],
+                    help="fp32: f32 MFMA (rollout_grp); split: f32-accurate hi/lo f16 MFMA (rollout_x3, tanh nets)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -192,13 +198,15 @@ def main():
                             policy_layers=pl, policy_mode=wl.get("policy_mode", "explore"), cost=cost, model=model)
         eng.set_policy(PolicySpec(*pol_arrays), wl["explore"], 1)
     else:
-        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, cost=cost, model=model)
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, cost=cost, model=model,
+                            precision=args.precision)
     eng.set_weights(MLPSpec(kernels, biases, act, model=model), norm, 1)
     if reward:
         eng.set_discount(gamma)
     info = eng.info()
     kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
-                   "group8": "rollout_grp<NW=8>"}.get(
+                   "group8": "rollout_grp<NW=8>", "split1": "rollout_x3<NC=1>", "split2": "rollout_x3<NC=2>",
+                   "split4": "rollout_x3<NC=4>"}.get(
         info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
     d_state = torch.from_numpy(state).to(dev)
     d_actions = None
@@ -278,6 +286,7 @@ def main():
     if cem and world > 1:                              # per-launch device time: the wall-clock share
         kern_ms = [t * 1e3 for t in step_s]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    peak = FP32_MFMA_PEAK_TFLOPS if eng.precision == "fp32" else SPLIT_PEAK_TFLOPS
     achieved_tflops = K * H * iters * fpcs / kern_avg_s / 1e12
     out = {
         "metric": "candidate-steps/sec (K x H per get_action), HalfCheetah dims",
@@ -291,7 +300,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if eng.precision == "fp32" else "f32 (hi/lo f16 split operands, 3 MFMA passes, f32 accumulate)",
         "data": f"synthetic (HalfCheetah dims s=20,a=6; random-init {'two-head reward net' if reward else 'dynamics MLP'}; "
                 f"actions {'resident in HBM as [H,K,6] f64' if args.actions == 'hbm' else 'drawn in-kernel (Philox)'})",
         "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
@@ -300,7 +309,8 @@ def main():
                                + (f" + fused policy {policy[1]}x{policy[0]} tanh "
                                   f"({wl.get('policy_mode', 'explore')})" if policy else "")
                                + (f" + CEM {iters} iterations, {n_elite} elites, alpha {cem['alpha']}" if cem else "")
-                               + ", fp32 MFMA, 1 RCCL all-gather min-loc per step"
+                               + (", fp32 MFMA" if eng.precision == "fp32" else ", split-f16 MFMA (f32-accurate)")
+                               + ", 1 RCCL all-gather min-loc per step"
                                + (" (+1 all-gather of the local top-E per CEM iteration)" if cem else ""),
                    "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
                    "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
@@ -309,8 +319,10 @@ def main():
         "p50_ms": float(np.percentile(step_s, 50) * 1e3),
         "p90_ms": float(np.percentile(step_s, 90) * 1e3),
         "kernel_ms_avg": kern_avg_s * 1e3,
-        "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved_tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+        "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved_tflops / peak, "traffic": None,
+                     "peak_note": "fp32 matrix peak (v_mfma_f32_16x16x4_f32)" if eng.precision == "fp32" else
+                                  "f16 dense MFMA peak 2516.6 / 3 passes per f32 product (f32-equivalent)",
                      "kernel": kernel_name + (" x CEM iterations + select/refit (HIP events around the "
                                               "whole device-side CEM call)" if cem else ""),
                      "flop_per_launch": K * H * fpcs,
@@ -320,7 +332,7 @@ def main():
     prof = os.path.join(REPO, "profiles", "traffic_per_launch.json")
     if os.path.exists(prof):
         try:
-            tr = json.load(open(prof)).get(args.workload)
+            tr = json.load(open(prof)).get(args.workload + ("" if eng.precision == "fp32" else ":split"))
             if tr:
                 out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
         except Exception:

@@ -63,7 +63,11 @@ typedef enum bcmpc_model {      /* which dynamics net (dynamics.py)             
 } bcmpc_model;
 
 typedef enum bcmpc_precision {
-    BCMPC_PREC_FP32 = 0         /* f32 MLP on v_mfma_f32_16x16x4_f32 (exact f32 fma chain) */
+    BCMPC_PREC_FP32 = 0,        /* f32 MLP on v_mfma_f32_16x16x4_f32 (exact f32 fma chain) */
+    BCMPC_PREC_SPLIT_F16 = 1    /* f32-accurate MLP on the f16 matrix cores: every operand as
+                                   hi + lo f16 halves (22 bits), three v_mfma_f32_16x16x32_f16
+                                   passes hi*hi + hi*lo + lo*hi, f32 accumulate (DESIGN.md
+                                   "split kernel"); tanh, no LayerNorm, NNDynamicsModel only */
 } bcmpc_precision;
 
 typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")              */
@@ -71,7 +75,10 @@ typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")  
     BCMPC_KERNEL_SOLO = 1,      /* one wave owns 16 candidates, activations in VGPRs     */
     BCMPC_KERNEL_GROUP2 = 2,    /* 2 waves share 16 candidates through an LDS slab       */
     BCMPC_KERNEL_GROUP4 = 3,    /* 4 waves share 16 candidates                           */
-    BCMPC_KERNEL_GROUP8 = 4     /* 8 waves share 16 candidates (small K)                 */
+    BCMPC_KERNEL_GROUP8 = 4,    /* 8 waves share 16 candidates (small K)                 */
+    BCMPC_KERNEL_SPLIT1 = 5,    /* BCMPC_PREC_SPLIT_F16: one workgroup = 1 x 16 candidates  */
+    BCMPC_KERNEL_SPLIT2 = 6,    /*                                      2 x 16 candidates  */
+    BCMPC_KERNEL_SPLIT4 = 7     /*                                      4 x 16 candidates  */
 } bcmpc_kernel;
 
 typedef enum bcmpc_policy_mode {   /* MPCcontrollerPolicyNet.self_exp (controllers.py:201-208) */

@@ -73,14 +73,16 @@ def _engine(spec, norm, K, H, model, kernel="auto"):
     return eng
 
 
-@pytest.mark.parametrize("model", ["delta", "reward"])
+@pytest.mark.parametrize("model", ["delta", "reward", "delta-split"])
 def test_cem_iterations_pinned_to_oracle(model):
     import torch
     from oracle import mpc_oracle as orc
     K, H, A, E, iters, alpha, seed = 2048, 8, 6, 205, 4, 0.1, 0xC0FFEE
     low, high = -np.ones(A), np.ones(A)
+    kernel = "split2" if model == "delta-split" else "auto"
+    model = "delta" if model == "delta-split" else model
     spec, norm, dyn, score, state = _problem(model)
-    eng = _engine(spec, norm, K, H, model)
+    eng = _engine(spec, norm, K, H, model, kernel)
     dev = torch.device("cuda", 0)
     b = _bufs(K, H, A, E, dev)
     mu0, sd0 = np.zeros((H, A)), np.full((H, A), 0.5)

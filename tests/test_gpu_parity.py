@@ -22,7 +22,17 @@ pytestmark = pytest.mark.gpu
 ATOL, RTOL = 1e-4, 1e-5
 
 
-KERNELS = ["solo", "group2", "group4", "group8"]
+KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4"]
+
+
+def _skip_unsupported(g: Golden, kernel: str):
+    if kernel == "group8" and g.meta["hidden"] <= 64:
+        pytest.skip("group8 needs >= 8 hidden tiles")
+    if kernel.startswith("split"):
+        if g.meta["act"] != "tanh" or g.meta["ln"]:
+            pytest.skip("split precision: tanh nets without LayerNorm")
+        if kernel == "split4" and g.meta["hidden"] <= 64:
+            pytest.skip("split4 needs >= 4 waves (hidden > 64)")
 
 
 def _engine(g: Golden, K=None, H=None, cost="cheetah", kernel="auto"):
@@ -62,8 +72,7 @@ def argmin_is_decidable(g: Golden) -> bool:
 @pytest.mark.parametrize("name", golden_names("mpc"))
 def test_engine_matches_reference_fixture(name, kernel):
     g = Golden(name)
-    if kernel == "group8" and g.meta["hidden"] <= 64:
-        pytest.skip("group8 needs >= 8 hidden tiles")
+    _skip_unsupported(g, kernel)
     eng = _engine(g, kernel=kernel)
     assert eng.info()["kernel"] == kernel
     if g.meta.get("inject") == "philox":
@@ -119,8 +128,7 @@ def test_trajectory_states_match(name, kernel):
     g = Golden(name)
     if "states" not in g.z.files:
         pytest.skip("fixture holds no states")
-    if kernel == "group8" and g.meta["hidden"] <= 64:
-        pytest.skip("group8 needs >= 8 hidden tiles")
+    _skip_unsupported(g, kernel)
     eng = _engine(g, cost="none", kernel=kernel)
     dev = torch.device("cuda", 0)
     st = torch.from_numpy(g.state).to(dev)
@@ -192,7 +200,7 @@ def test_non_fused_cost_goes_through_trajectory_mode():
     assert ctrl.last_index == i and np.array_equal(a, want)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "solo", "group8"])
+@pytest.mark.parametrize("kernel", ["auto", "solo", "group8", "split4", "split1"])
 def test_full_size_cfg3_properties(kernel):
     """K=65536, H=20, 2x500 tanh (BASELINE cfg3 dims) at full size: shard
     invariance (bitwise), argmin consistency, determinism, and a 256-candidate
@@ -251,13 +259,15 @@ def test_errors_are_python_exceptions():
         e2.set_weights(MLPSpec(w.kernels[:2], w.biases[:2]), orc.synthetic_normalization(), 1)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "group4", "group8"])
+@pytest.mark.parametrize("kernel", ["auto", "group4", "group8", "split1", "split2"])
 @pytest.mark.parametrize("hidden,L,act,ln", [(1024, 3, "tanh", False), (768, 2, "tanh", False),
                                              (1000, 3, "relu", True), (600, 2, "tanh", False)])
 def test_large_hidden_vs_oracle(hidden, L, act, ln, kernel):
     """cfg5-class networks (3x1024) and odd widths on the group kernels."""
     from bc_mpc_amd.engine import MLPSpec, RolloutEngine
     from oracle import mpc_oracle as orc
+    if kernel.startswith("split") and (act != "tanh" or ln):
+        pytest.skip("split precision: tanh nets without LayerNorm")
     K, H = 96, 4
     w = orc.synthetic_weights(20, 6, hidden, L, act, ln, seed_base=77)
     norm = orc.synthetic_normalization()
