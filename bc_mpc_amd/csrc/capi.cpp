@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -239,7 +240,9 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         int nc = c.kernel == BCMPC_KERNEL_SPLIT1 ? 1 : c.kernel == BCMPC_KERNEL_SPLIT2 ? 2
                : c.kernel == BCMPC_KERNEL_SPLIT4 ? 4 : 0;
         const int nwx = x3_waves(e->HP);
-        auto fits = [&](int n) { return n <= nwx && x3_lds(e->HP, c.n_layers, n) <= 160 * 1024; };
+        auto fits = [&](int n) {
+            return n <= nwx && n <= x3_max_nc(e->HP) && x3_lds(e->HP, c.n_layers, n, c.action_dim) <= 160 * 1024;
+        };
         if (nc == 0) {
             nc = 1;
             for (int n : {4, 2})
@@ -591,7 +594,39 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
     if (e->split) {
+        // diagnostics: X3_STAMP builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
+        static uint64_t* d_st = nullptr;
+        static size_t st_n = 0;
+        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
+        const int nw = x3_waves(e->HP);
+        const size_t blocks = (size_t)((c.num_paths + 16 * e->nc - 1) / (16 * e->nc));
+        if (stamps) {
+            if (st_n < blocks * nw * 10) {
+                if (d_st) (void)hipFree(d_st);
+                st_n = blocks * nw * 10;
+                HIP_TRY(hipMalloc(&d_st, st_n * sizeof(uint64_t)));
+            }
+            HIP_TRY(hipMemsetAsync(d_st, 0, st_n * sizeof(uint64_t), st));
+            a.stamps = d_st;
+        }
         HIP_TRY(launch_rollout_x3(a, e->HP, e->nc, st));
+        if (stamps) {
+            std::vector<uint64_t> h(blocks * nw * 10);
+            HIP_TRY(hipMemcpyAsync(h.data(), d_st, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            const char* names[10] = {"owner", "input", "B1", "layer0", "slab", "mm", "epi", "out", "B3B4", "-"};
+            for (int grp = 0; grp < 2; ++grp) {
+                std::fprintf(stderr, "x3 stamps %s:", grp == 0 ? "owners " : "others ");
+                for (int k = 0; k < 9; ++k) {
+                    double sum = 0; size_t n = 0;
+                    for (size_t b = 0; b < blocks; ++b)
+                        for (int w = 0; w < nw; ++w)
+                            if ((w < e->nc) == (grp == 0)) { sum += (double)h[(b * nw + w) * 10 + k]; ++n; }
+                    std::fprintf(stderr, " %s=%.0f", names[k], n ? sum / n / c.horizon : 0.0);
+                }
+                std::fprintf(stderr, "  (per step, s_memtime ticks)\n");
+            }
+        }
     } else if (e->kernel == BCMPC_KERNEL_SOLO) {
         HIP_TRY(launch_rollout(a, e->HP, e->wpb, st));
     } else {

@@ -47,21 +47,74 @@
 namespace bcmpc {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
-// tanh(y) * 2^12: 4096 (1 - t) / (1 + t), t = e^{-2|y|}, sign restored.  Absolute
-// error ~1e-7 (x 4096) near 0, a few ulp elsewhere; NaN propagates, +-inf -> +-4096.
-__device__ __forceinline__ float tanh_x4096(float y) {
-    const float t = __builtin_amdgcn_exp2f(fabsf(y) * -2.8853900817779268f);
+// timing-only diagnostics (results wrong): no tanh / weights from a 16 KiB window /
+// no owner phase (f64 state, cost, normalisation) / no MFMAs
+#ifndef X3_DIAG_NOTANH
+#define X3_DIAG_NOTANH 0
+#endif
+#ifndef X3_DIAG_SMALLW
+#define X3_DIAG_SMALLW 0
+#endif
+#ifndef X3_DIAG_NOOWNER
+#define X3_DIAG_NOOWNER 0
+#endif
+#ifndef X3_DIAG_NOMFMA
+#define X3_DIAG_NOMFMA 0
+#endif
+#ifndef X3_DIAG_NOBAR            // no workgroup barriers inside the step loop
+#define X3_DIAG_NOBAR 0
+#endif
+#ifndef X3_STAMP                 // per-phase s_memtime totals, printed by two blocks at exit
+#define X3_STAMP 0
+#endif
+#define X3_ST(k)                                                        \
+    do {                                                                \
+        if constexpr (X3_STAMP) {                                       \
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();           \
+            ph_[k] += t_ - tp_;                                         \
+            tp_ = t_;                                                   \
+        }                                                               \
+    } while (0)
+
+#define X3_BARRIER()                                \
+    do {                                            \
+        if constexpr (!X3_DIAG_NOBAR) __syncthreads(); \
+    } while (0)
+
+// 2 log2(e): hidden-layer biases and result scales carry this factor, so the
+// epilogue's pre-activation is z = 2 log2(e) y with no extra multiply
+constexpr float kTanhK = 2.8853900817779268f;
+
+// tanh(y) * 2^12 from z = 2 log2(e) y: 4096 (1 - t) / (1 + t), t = 2^-|z| = e^{-2|y|},
+// sign restored (6 VALU ops, two of them transcendental).  Absolute error ~1e-7
+// (x 4096) near 0, a few ulp elsewhere; NaN propagates, +-inf -> +-4096.
+__device__ __forceinline__ float tanh_x4096(float z) {
+    if constexpr (X3_DIAG_NOTANH) return z * 1024.0f;
+    const float t = __builtin_amdgcn_exp2f(-fabsf(z));
     const float r = __builtin_amdgcn_rcpf(fmaf(t, 1.0f / 4096.0f, 1.0f / 4096.0f));
-    return __builtin_copysignf(fmaf(-t, r, r), y);
+    return __builtin_copysignf(fmaf(-t, r, r), z);
+}
+
+// (a, b) -> packed f16 hi = RNE(a, b) and lo = RNE(a - hi, b - hi): v_cvt_pk_f16_f32,
+// two v_fma_mix_f32 (x - hi with hi read as f16, exact), v_cvt_pk_f16_f32.
+__device__ __forceinline__ void split2(float a, float b, h2& hi, h2& lo) {
+    hi = __builtin_convertvector((f2){a, b}, h2);
+    float la, lb;
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(la) : "v"(hi), "v"(a));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lb) : "v"(hi), "v"(b));
+    lo = __builtin_convertvector((f2){la, lb}, h2);
 }
 
 __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const _Float16 h = (_Float16)v[i];
-        hi[i] = h;
-        lo[i] = (_Float16)(v[i] - (float)h);
+    for (int i = 0; i < 8; i += 2) {
+        h2 h, l;
+        split2(v[i], v[i + 1], h, l);
+        hi[i] = h[0]; hi[i + 1] = h[1];
+        lo[i] = l[0]; lo[i + 1] = l[1];
     }
 }
 
@@ -73,6 +126,7 @@ __device__ __forceinline__ h8 sread(const f4* p) { return __builtin_bit_cast(h8,
 __device__ __forceinline__ void swrite(f4* p, h8 v) { *p = __builtin_bit_cast(f4, v); }
 
 __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
+    if constexpr (X3_DIAG_NOMFMA) return c + (f4){(float)a[0], (float)b[0], 0.f, 0.f};
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
@@ -82,64 +136,85 @@ __device__ __forceinline__ int sidx(int p, int c, int part, int lane) {
     return ((p * NC + c) * 2 + part) * 64 + lane;
 }
 
-// acc[j][c] += sum over k-steps of W[tile j] * X[c]: weights streamed from L2
-// (this wave's contiguous slice, one k-step ahead in registers), activations
-// from the slab (one k-step ahead; the slab has one spare k-step at the end).
-template <int TW, int NC, int P>
-__device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
-                                      int lane) {
-    constexpr int STEPB = TW * 2048;
-    const int voff = lane * 16;
-    h8 ah[TW], al[TW], bh[NC], bl[NC];
-#pragma unroll
-    for (int j = 0; j < TW; ++j) {
-        ah[j] = fload(rs, voff, wbase + j * 2048);
-        al[j] = fload(rs, voff, wbase + j * 2048 + 1024);
-    }
+// One operand unit: acc[g*G + j][c] += W[tile g*G + j] * X[c] for j < G (the G
+// tiles' A fragments, hi / lo, in registers) and the k-step's B fragments (bh/bl,
+// all NC columns, read by the caller).
+template <int TW, int NC, int G>
+__device__ __forceinline__ void unit_x3(const h8 (&ah)[G], const h8 (&al)[G], const h8 (&bh)[NC],
+                                        const h8 (&bl)[NC], int g, f4 (&acc)[TW][NC]) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        bh[c] = sread(slab + sidx<NC>(0, c, 0, lane));
-        bl[c] = sread(slab + sidx<NC>(0, c, 1, lane));
-    }
-    for (int p = 0; p < P; ++p) {
-        h8 nah[TW], nal[TW], nbh[NC], nbl[NC];
 #pragma unroll
-        for (int j = 0; j < TW; ++j) {
-            nah[j] = fload(rs, voff, wbase + (p + 1) * STEPB + j * 2048);
-            nal[j] = fload(rs, voff, wbase + (p + 1) * STEPB + j * 2048 + 1024);
-        }
+        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bh[c], acc[g * G + j][c]);
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            nbh[c] = sread(slab + sidx<NC>(p + 1, c, 0, lane));
-            nbl[c] = sread(slab + sidx<NC>(p + 1, c, 1, lane));
-        }
+        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bl[c], acc[g * G + j][c]);
 #pragma unroll
-        for (int j = 0; j < TW; ++j)
-#pragma unroll
-            for (int c = 0; c < NC; ++c) acc[j][c] = mfma16(ah[j], bh[c], acc[j][c]);
-#pragma unroll
-        for (int j = 0; j < TW; ++j)
-#pragma unroll
-            for (int c = 0; c < NC; ++c) acc[j][c] = mfma16(ah[j], bl[c], acc[j][c]);
-#pragma unroll
-        for (int j = 0; j < TW; ++j)
-#pragma unroll
-            for (int c = 0; c < NC; ++c) acc[j][c] = mfma16(al[j], bh[c], acc[j][c]);
-#pragma unroll
-        for (int j = 0; j < TW; ++j) {
-            ah[j] = nah[j];
-            al[j] = nal[j];
-        }
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            bh[c] = nbh[c];
-            bl[c] = nbl[c];
-        }
+        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(al[j], bh[c], acc[g * G + j][c]);
     }
 }
 
+template <int NC>
+__device__ __forceinline__ void bread_x3(const f4* slab, int p, int lane, h8 (&bh)[NC], h8 (&bl)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        bh[c] = sread(slab + sidx<NC>(p, c, 0, lane));
+        bl[c] = sread(slab + sidx<NC>(p, c, 1, lane));
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, int base, h8 (&ah)[G], h8 (&al)[G]) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int o = X3_DIAG_SMALLW ? ((base + j * 2048) & 16383) : base + j * 2048;
+        ah[j] = fload(rs, voff, o);
+        al[j] = fload(rs, voff, o + 1024);
+    }
+}
+
+// acc[j][c] += sum over the P k-steps of W[tile j] * X[c]: this wave's contiguous
+// weight slice streamed from L2 in units of G tiles x one k-step (NG = TW/G units
+// per k-step) through two register sets (ping-pong: unit u+1's loads are in
+// flight while unit u's MFMAs run; set 0 arrives holding unit 0, loaded by the
+// caller before its epilogue and clobbered here); the layer input from the slab,
+// each k-step's B fragments read once at its first unit.
+template <int TW, int NC, int P, int G>
+__device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
+                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G]) {
+    constexpr int NG = TW / G;
+    static_assert(NG * G == TW && (NG == 1 || NG == 2), "one or two units per k-step");
+    static_assert((P * NG) % 2 == 0, "ping-pong over unit pairs");
+    constexpr int NU = P * NG;
+    constexpr int STEPB = TW * 2048;
+    const int voff = lane * 16;
+    auto uoff = [&](int u) { return wbase + (u / NG) * STEPB + (u % NG) * G * 2048; };
+    // unit u (even) is (k-step u/NG, group 0); unit u+1 is group 1 of the same
+    // k-step (NG = 2) or the next k-step (NG = 1)
+    constexpr int G1 = NG == 2 ? 1 : 0;
+    h8 s1h[G], s1l[G], bh[NC], bl[NC];
+    // (the last pair is peeled so that every load in the loop is unconditional: a
+    // conditional load would make the compiler drain vmcnt to 0 at the merge)
+    for (int u = 0; u < NU - 2; u += 2) {
+        aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l);
+        __builtin_amdgcn_sched_barrier(0);          // keep the loads ahead of the MFMAs they overlap
+        bread_x3<NC>(slab, u / NG, lane, bh, bl);
+        unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
+        aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (NG == 1) bread_x3<NC>(slab, u + 1, lane, bh, bl);
+        unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
+    }
+    aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l);
+    __builtin_amdgcn_sched_barrier(0);
+    bread_x3<NC>(slab, (NU - 2) / NG, lane, bh, bl);
+    unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
+    if constexpr (NG == 1) bread_x3<NC>(slab, NU - 1, lane, bh, bl);
+    unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
+}
+
 // Epilogue of one tile pair (k-step) for one column: BiasAdd (f32, after undoing
-// the operand scales with one exact power-of-two multiply), tanh, x 2^12, split.
+// the operand scales; f and the LDS biases carry the 2 log2(e) factor), tanh,
+// x 2^12, split.
 __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, const float* __restrict__ bias,
                                          int t0, int q, h8& hi, h8& lo) {
     const f4 b0 = *reinterpret_cast<const f4*>(bias + 16 * t0 + 4 * q);
@@ -153,19 +228,41 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
     split8(v, hi, lo);
 }
 
-template <int HP, int NC, int NW>
-__host__ __device__ constexpr int x3_lds_bytes(int L) {
-    // consts | biases (L*HP + 32) | column factors NC*16 | layer-0 slab NC*2 KiB | slab (P+1)*NC*2 KiB
-    return param_bytes(L, HP) + NC * 16 * 4 + NC * 2048 + (HP / 32 + 1) * NC * 2048;
+#ifndef X3_NW512                // waves per workgroup at hidden 512 (8: one 64-candidate group per CU;
+#define X3_NW512 8               // 4: two 32-candidate groups per CU, out of phase)
+#endif
+#ifndef X3_ONLY_NC
+#define X3_ONLY_NC 4
+#endif
+// tiles per streamed operand unit: a whole k-step up to 4 tiles per wave, else half
+__host__ __device__ constexpr int x3_group(int TW) { return TW <= 4 ? TW : TW / 2; }
+
+#ifndef X3_NCH
+#define X3_NCH 4                 // steps of layer-0 action inputs staged in LDS per fill
+#endif
+
+// waves per SIMD the register allocator must allow: two whenever two workgroups
+// (or two waves of one) should share a SIMD
+__host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
+    return (NW >= 8 || HP <= 512) ? 2 : 1;
+}
+
+// LDS carve-up: consts | biases (L*HP + 32) | column factors NC*16 | action inputs
+// X3_NCH*16NC*A (16-B aligned) | layer-0 slab NC*2 KiB | slab (P+1)*NC*2 KiB
+__host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
+__host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A) {
+    return param_bytes(L, HP) + NC * 16 * 4 + x3_xa_bytes(NC, A) + NC * 2048 + (HP / 32 + 1) * NC * 2048;
 }
 
 template <int HP, int NC, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW >= 8 ? 2 : 1, 8)))
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(x3_waves_per_eu(HP, NC, NW), 8)))
 void rollout_x3(const RolloutArgs a) {
     constexpr int T = HP / 16;          // hidden tiles
     constexpr int P = T / 2;            // hidden k-steps (32 wide)
     constexpr int TW = T / NW;          // output tiles per wave
     constexpr int PW = TW / 2;          // k-steps produced per wave
+    constexpr int CB = 16 * NC;         // candidates per block
+    constexpr int G = x3_group(TW);     // tiles per streamed operand unit
     static_assert(TW % 2 == 0 && TW * NW == T, "each wave must own whole tile pairs");
     static_assert(NC <= NW, "one owner wave per column");
     static_assert(P >= NW, "the output-layer partials reuse the slab");
@@ -177,7 +274,8 @@ void rollout_x3(const RolloutArgs a) {
     const int m = lane & 15;
     const bool owner = w < NC;
     const int cw = owner ? w : 0;                       // the owner's column
-    const int64_t cand = (int64_t)blockIdx.x * (16 * NC) + 16 * cw + m;
+    const int64_t cand0 = (int64_t)blockIdx.x * CB;
+    const int64_t cand = cand0 + 16 * cw + m;
     const bool valid = owner && cand < a.K;
     const int S = a.S, A = a.A, L = a.L;
 
@@ -185,11 +283,12 @@ void rollout_x3(const RolloutArgs a) {
     float* Bl = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kConstRows * kConstCols * 8);
     for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
     for (int l = 0; l < L; ++l)
-        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i];
+        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kTanhK;
     float* const Bout = Bl + L * HP;
     for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[L][i];
     float* colf = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP));
-    f4* slab0 = reinterpret_cast<f4*>(colf + NC * 16);
+    float* xa = colf + NC * 16;                         // [X3_NCH][CB][A] normalised action inputs (f32)
+    f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + x3_xa_bytes(NC, A));
     f4* slab = slab0 + NC * 2 * 64;
     __syncthreads();
 
@@ -211,42 +310,75 @@ void rollout_x3(const RolloutArgs a) {
             }
     }
     double cost = 0.0;                                  // trajectory_cost = 0 (cost_functions.py:60)
-    const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
-    auto fetch_uniform = [&](int h, int j) -> double {
-        if (!valid) return 0.0;
+    // action j of candidate c at step h: the caller's [H,K,A] array (np.random.uniform,
+    // controllers.py:53), Philox, or the CEM sampler
+    auto act_value = [&](int h, int64_t c, int j) -> double {
+        const uint64_t g = (uint64_t)(a.cand_offset + c);
         if (a.cem_mu)
-            return cem_action(a.seed, gcand, h, j, a.cem_iter, a.cem_mu[h * A + j], a.cem_sigma[h * A + j],
+            return cem_action(a.seed, g, h, j, a.cem_iter, a.cem_mu[h * A + j], a.cem_sigma[h * A + j],
                               C[6 * 32 + j], C[7 * 32 + j]);
-        return a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
-                         : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
+        return a.actions ? a.actions[((int64_t)h * a.K + c) * A + j]
+                         : rng_action(a.seed, g, h, j, C[6 * 32 + j], C[7 * 32 + j]);
     };
     const int voff = lane * 16;
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
     const __amdgpu_buffer_rsrc_t rso = layer_rsrc(a.w[L], a.wbytes[L]);
     const float fo = a.winv[L];
 
-    for (int h = 0; h < a.H; ++h) {
-        // ---- layer-0 weights first (state-independent): this wave's TW tiles, one k-step ----
-        h8 a0h[TW], a0l[TW];
+    // Operand sets in flight ahead of their MFMAs (issued before the preceding VALU phase):
+    //   a0h/a0l : layer-0 fragments of the NEXT step (issued after the output MFMAs)
+    //   uh/ul   : unit 0 of the next hidden layer, issued before each epilogue
+    //   oh/ol   : the output layer's first OP k-step pairs (slot 2*(pp % OP) + v = k-step
+    //             w*PW+pp, tile v), issued before the last epilogue; the rest stream in
+    constexpr int OP = PW < 2 ? PW : 2;
+    h8 a0h[TW], a0l[TW], uh[G], ul[G], oh[2 * OP], ol[2 * OP];
+    aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);
+    auto load_out = [&](int pp, int slot) {
 #pragma unroll
-        for (int j = 0; j < TW; ++j) {
-            a0h[j] = fload(rs0, voff, (w * TW + j) * 2048);
-            a0l[j] = fload(rs0, voff, (w * TW + j) * 2048 + 1024);
+        for (int v = 0; v < 2; ++v) {
+            const int o = (((w * PW + pp) * 2 + v) * 2) * 1024;
+            oh[2 * slot + v] = fload(rso, voff, o);
+            ol[2 * slot + v] = fload(rso, voff, o + 1024);
         }
-        if (owner) {
-            // ---- normalise (dynamics.py:109-110), cast to f32 (TF feed), column scale, split ----
+    };
+    auto load_next = [&](int l_next) {
+        if (l_next < L) {
+            aload_x3<G>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, w * P * TW * 2048, uh, ul);
+        } else {
+#pragma unroll
+            for (int pp = 0; pp < OP; ++pp) load_out(pp, pp);
+        }
+    };
+
+    uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    for (int h = 0; h < a.H; ++h) {
+        X3_ST(0);
+        if (h % X3_NCH == 0) {
+            // ---- stage the next X3_NCH steps' action inputs (all threads): f64 normalise
+            //      (dynamics.py:110), cast to f32 (TF feed) ----
+            const int nhs = (a.H - h < X3_NCH) ? a.H - h : X3_NCH;
+            const int per = CB * A;
+            for (int i = threadIdx.x; i < nhs * per; i += 64 * NW) {
+                const int hh = i / per, rem = i - hh * per, kl = rem / A, j = rem - kl * A;
+                float xv = 0.f;
+                if (cand0 + kl < a.K)
+                    xv = (float)__ddiv_rn(__dsub_rn(act_value(h + hh, cand0 + kl, j), C[2 * 32 + j]), C[3 * 32 + j]);
+                xa[(hh * CB + kl) * A + j] = xv;
+            }
+            X3_BARRIER();
+        }
+        if (owner && !X3_DIAG_NOOWNER) {
+            // ---- normalise the state (dynamics.py:109), cast to f32, column scale, split ----
             float x[8];
+            const float* xr = xa + ((h % X3_NCH) * CB + 16 * cw + m) * A;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int v = i >> 2, r = i & 3;
                 const int d = 16 * v + 4 * q + r;
                 float xv = 0.f;
-                if (d < S) {
-                    xv = (float)__ddiv_rn(__dsub_rn(s[v][r], C[0 * 32 + d]), C[1 * 32 + d]);
-                } else if (d < S + A) {
-                    const int j = d - S;
-                    xv = (float)__ddiv_rn(__dsub_rn(fetch_uniform(h, j), C[2 * 32 + j]), C[3 * 32 + j]);
-                }
+                if (d < S) xv = (float)__ddiv_rn(__dsub_rn(s[v][r], C[0 * 32 + d]), C[1 * 32 + d]);
+                else if (d < S + A) xv = xr[d - S];
                 x[i] = xv;
             }
             float mx = 0.f;
@@ -265,9 +397,11 @@ void rollout_x3(const RolloutArgs a) {
             split8(x, xh, xl);
             swrite(slab0 + (cw * 2 + 0) * 64 + lane, xh);
             swrite(slab0 + (cw * 2 + 1) * 64 + lane, xl);
-            if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh);
+            if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kTanhK;
         }
-        __syncthreads();                                  // layer-0 input published
+        X3_ST(1);
+        X3_BARRIER();                                  // layer-0 input published
+        X3_ST(2);
 
         // ---- layer 0 [S+A -> h] ----
         f4 acc[TW][NC];
@@ -283,18 +417,16 @@ void rollout_x3(const RolloutArgs a) {
                 bl[c] = sread(slab0 + (c * 2 + 1) * 64 + lane);
             }
 #pragma unroll
-            for (int j = 0; j < TW; ++j)
+            for (int c = 0; c < NC; ++c) {
 #pragma unroll
-                for (int c = 0; c < NC; ++c) acc[j][c] = mfma16(a0h[j], bh[c], acc[j][c]);
+                for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0h[j], bh[c], acc[j][c]);
 #pragma unroll
-            for (int j = 0; j < TW; ++j)
+                for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0h[j], bl[c], acc[j][c]);
 #pragma unroll
-                for (int c = 0; c < NC; ++c) acc[j][c] = mfma16(a0h[j], bl[c], acc[j][c]);
-#pragma unroll
-            for (int j = 0; j < TW; ++j)
-#pragma unroll
-                for (int c = 0; c < NC; ++c) acc[j][c] = mfma16(a0l[j], bh[c], acc[j][c]);
+                for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0l[j], bh[c], acc[j][c]);
+            }
         }
+        load_next(1);
         h8 xh[PW][NC], xl[PW][NC];                        // this wave's activations of the current layer
 #pragma unroll
         for (int pp = 0; pp < PW; ++pp)
@@ -302,11 +434,12 @@ void rollout_x3(const RolloutArgs a) {
             for (int c = 0; c < NC; ++c)
                 epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[c * 16 + m], Bl, w * TW + 2 * pp, q,
                          xh[pp][c], xl[pp][c]);
+        X3_ST(3);
 
         // ---- hidden layers 1..L-1 [h -> h] through the slab ----
         for (int l = 1; l < L; ++l) {
             // (l == 1: the slab's last readers were the owners' partial sums, before the barrier above)
-            if (l > 1) __syncthreads();                   // every wave is done reading the slab
+            if (l > 1) X3_BARRIER();                   // every wave is done reading the slab
 #pragma unroll
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
@@ -314,13 +447,16 @@ void rollout_x3(const RolloutArgs a) {
                     swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
                     swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
-            __syncthreads();                              // layer input complete
+            X3_BARRIER();                              // layer input complete
+            X3_ST(4);
 #pragma unroll
             for (int j = 0; j < TW; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
-            mm_x3<TW, NC, P>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane);
-            const float f = a.winv[l];
+            mm_x3<TW, NC, P, G>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane, uh, ul);
+            X3_ST(5);
+            load_next(l + 1);
+            const float f = a.winv[l] * kTanhK;
 #pragma unroll
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
@@ -328,6 +464,7 @@ void rollout_x3(const RolloutArgs a) {
                     epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
                              xl[pp][c]);
         }
+        X3_ST(6);
 
         // ---- output layer [h -> S] (2 tiles), K-split: this wave's own k-steps from registers ----
         f4 po[2][NC];
@@ -337,29 +474,28 @@ void rollout_x3(const RolloutArgs a) {
             for (int c = 0; c < NC; ++c) po[v][c] = (f4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int pp = 0; pp < PW; ++pp) {
-            const int p = w * PW + pp;
-            h8 oh[2], ol[2];
+            const int slot = pp % OP;
 #pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                oh[v] = fload(rso, voff, ((p * 2 + v) * 2 + 0) * 1024);
-                ol[v] = fload(rso, voff, ((p * 2 + v) * 2 + 1) * 1024);
-            }
+            for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int v = 0; v < 2; ++v)
-#pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    po[v][c] = mfma16(oh[v], xh[pp][c], po[v][c]);
-                    po[v][c] = mfma16(oh[v], xl[pp][c], po[v][c]);
-                    po[v][c] = mfma16(ol[v], xh[pp][c], po[v][c]);
+                for (int v = 0; v < 2; ++v) {
+                    po[v][c] = mfma16(oh[2 * slot + v], xh[pp][c], po[v][c]);
+                    po[v][c] = mfma16(oh[2 * slot + v], xl[pp][c], po[v][c]);
+                    po[v][c] = mfma16(ol[2 * slot + v], xh[pp][c], po[v][c]);
                 }
+            if (pp + OP < PW) load_out(pp + OP, slot);
         }
-        __syncthreads();                                  // every wave is done reading the slab
+        __builtin_amdgcn_sched_barrier(0);              // (not hoisted above the MFMAs' operand waits)
+        aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);                     // next step's layer 0
+        X3_ST(7);
+        X3_BARRIER();                                  // every wave is done reading the slab
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
             for (int c = 0; c < NC; ++c) slab[((w * 2 + v) * NC + c) * 64 + lane] = po[v][c];
-        __syncthreads();                                  // partials complete
-        if (!owner) continue;
+        X3_BARRIER();                                  // partials complete
+        X3_ST(8);
+        if (!owner || X3_DIAG_NOOWNER) continue;
 
         f4 o[2];
 #pragma unroll
@@ -405,12 +541,16 @@ void rollout_x3(const RolloutArgs a) {
         }
     }
     if (a.costs && valid && q == 0) a.costs[cand] = cost;
+    if constexpr (X3_STAMP) {
+        if (a.stamps && lane == 0)
+            for (int k = 0; k < 10; ++k) a.stamps[((size_t)blockIdx.x * NW + w) * 10 + k] = ph_[k];
+    }
 }
 
 // ------------------------------------------------------------ launchers ----
 template <int HP, int NC, int NW>
 static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
-    if constexpr (NC > NW || x3_lds_bytes<HP, NC, NW>(1) > 160 * 1024) {
+    if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1) > 160 * 1024) {
         (void)a; (void)st;
         return hipErrorInvalidValue;
     } else {
@@ -421,7 +561,7 @@ static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
             if (e != hipSuccess) return e;
             attr_set = true;
         }
-        const size_t lds = (size_t)x3_lds_bytes<HP, NC, NW>(a.L);
+        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, a.L, a.A);
         const int64_t blocks = (a.K + 16 * NC - 1) / (16 * NC);
         hipLaunchKernelGGL((rollout_x3<HP, NC, NW>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
         return hipGetLastError();
@@ -433,22 +573,38 @@ int x3_waves(int hidden_padded) {
         case 64: return 2;
         case 128: return 4;
         case 256: return 4;
-        default: return 8;          // 512, 768, 1024
+        case 512: return X3_NW512;
+        default: return 8;          // 768, 1024
     }
 }
 
-size_t x3_lds(int hidden_padded, int n_layers, int nc) {
-    const int P = hidden_padded / 32;
-    return (size_t)param_bytes(n_layers, hidden_padded) + nc * 16 * 4 + nc * 2048 + (size_t)(P + 1) * nc * 2048;
+// widest candidate group (16-candidate columns) the build instantiates for a width:
+// the accumulators of TW tiles x NC columns must fit beside the operand sets
+int x3_max_nc(int hidden_padded) {
+#ifdef X3_ONLY
+    return hidden_padded == X3_ONLY ? X3_ONLY_NC : 0;
+#else
+    const int tw = hidden_padded / 16 / x3_waves(hidden_padded);
+    return tw >= 8 ? 2 : 4;
+#endif
+}
+
+size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim) {
+    return (size_t)x3_lds_bytes_rt(hidden_padded, nc, n_layers, action_dim);
 }
 
 template <int NC>
 static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+#ifdef X3_ONLY          // variant builds (tools/build_variants.sh): one width, NC = 4 only
+    if constexpr (NC == X3_ONLY_NC)
+        return hidden_padded == X3_ONLY ? launch_x3_t<X3_ONLY, X3_ONLY_NC, X3_NW512>(a, st) : hipErrorInvalidValue;
+    return hipErrorInvalidValue;
+#else
     switch (hidden_padded) {
         case 64: return launch_x3_t<64, NC, 2>(a, st);
         case 128: return launch_x3_t<128, NC, 4>(a, st);
         case 256: return launch_x3_t<256, NC, 4>(a, st);
-        case 512: return launch_x3_t<512, NC, 8>(a, st);
+        case 512: return launch_x3_t<512, NC, X3_NW512>(a, st);
         case 768:
             if constexpr (NC <= 2) return launch_x3_t<768, NC, 8>(a, st);
             return hipErrorInvalidValue;
@@ -457,6 +613,7 @@ static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStrea
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
+#endif
 }
 
 hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st) {

@@ -1,17 +1,29 @@
 #!/bin/bash
 # Build A/B variants of libbcmpc.so into build/variants/ (selected at run time via BCMPC_LIB).
-# usage: tools/build_variants.sh "name:-DFLAG=1 ..." ...
+# usage: tools/build_variants.sh [-x] "name:-DFLAG=1 ..." ...
+#   default: flags apply to rollout.hip + rollout_grp.hip (f32 kernels)
+#   -x     : flags apply to rollout_x3.hip only, built for hidden 512 / NC 4 (-DX3_ONLY=512)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/variants
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize"
+X3=0
+if [ "${1:-}" = "-x" ]; then X3=1; shift; fi
+make -s -j8 ARCH=gfx950 >/dev/null
 $H -x hip -c bc_mpc_amd/csrc/capi.cpp -o build/variants/capi.o
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  ( $H $flags -c bc_mpc_amd/csrc/rollout.hip -o build/variants/rollout_$name.o &&
-    $H $flags -c bc_mpc_amd/csrc/rollout_grp.hip -o build/variants/rollout_grp_$name.o &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
-        build/variants/rollout_$name.o build/variants/rollout_grp_$name.o build/variants/capi.o ) &
+  if [ $X3 = 1 ]; then
+    ( $H $flags -DX3_ONLY=512 -c bc_mpc_amd/csrc/rollout_x3.hip -o build/variants/rollout_x3_$name.o &&
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
+          build/rollout.o build/rollout_grp.o build/cem.o build/variants/rollout_x3_$name.o build/variants/capi.o ) &
+  else
+    ( $H $flags -c bc_mpc_amd/csrc/rollout.hip -o build/variants/rollout_$name.o &&
+      $H $flags -c bc_mpc_amd/csrc/rollout_grp.hip -o build/variants/rollout_grp_$name.o &&
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
+          build/variants/rollout_$name.o build/variants/rollout_grp_$name.o build/cem.o build/rollout_x3.o \
+          build/variants/capi.o ) &
+  fi
 done
 wait
 ls build/variants/*.so
