@@ -439,6 +439,8 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         C[3 * 32 + i] = i < A ? w->std_action[i] + 1e-10 : 1.0;    // dynamics.py:110
         C[4 * 32 + i] = i < S ? w->mean_deltas[i] : 0.0;
         C[5 * 32 + i] = i < S ? w->std_deltas[i] : 0.0;
+        C[8 * 32 + i] = 1.0 / C[1 * 32 + i];
+        C[9 * 32 + i] = 1.0 / C[3 * 32 + i];
     }
     HIP_TRY(hipMemcpyAsync(e->d_w, hw.data(), hw.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemcpyAsync(e->d_b, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));

@@ -7,10 +7,11 @@
 
 namespace bcmpc {
 
-// consts block: [8][32] doubles
+// consts block: [10][32] doubles
 //   0 mean_obs   1 std_obs + 1e-10   2 mean_action   3 std_action + 1e-10
 //   4 mean_deltas  5 std_deltas      6 action low    7 action high
-constexpr int kConstRows = 8;
+//   8 1 / (std_obs + 1e-10)   9 1 / (std_action + 1e-10)   (correctly rounded, for div_rn)
+constexpr int kConstRows = 10;
 constexpr int kConstCols = 32;
 
 struct RolloutArgs {

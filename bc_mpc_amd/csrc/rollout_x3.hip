@@ -64,6 +64,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef X3_DIAG_NOMFMA
 #define X3_DIAG_NOMFMA 0
 #endif
+#ifndef X3_DIAG_LOADS            // 1: only hi fragments are loaded (lo = hi); 2: no weight loads in mm
+#define X3_DIAG_LOADS 0
+#endif
 #ifndef X3_DIAG_NOBAR            // no workgroup barriers inside the step loop
 #define X3_DIAG_NOBAR 0
 #endif
@@ -163,12 +166,18 @@ __device__ __forceinline__ void bread_x3(const f4* slab, int p, int lane, h8 (&b
 }
 
 template <int G>
-__device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, int base, h8 (&ah)[G], h8 (&al)[G]) {
+__device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, int base, h8 (&ah)[G], h8 (&al)[G],
+                                         bool diag = false) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int o = X3_DIAG_SMALLW ? ((base + j * 2048) & 16383) : base + j * 2048;
+        if (diag && X3_DIAG_LOADS == 2) {
+            ah[j] = ah[j] + (h8)(_Float16)1.0f;
+            al[j] = al[j] + (h8)(_Float16)1.0f;
+            continue;
+        }
         ah[j] = fload(rs, voff, o);
-        al[j] = fload(rs, voff, o + 1024);
+        al[j] = (diag && X3_DIAG_LOADS == 1) ? ah[j] + (h8)(_Float16)1.0f : fload(rs, voff, o + 1024);
     }
 }
 
@@ -195,16 +204,16 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     // (the last pair is peeled so that every load in the loop is unconditional: a
     // conditional load would make the compiler drain vmcnt to 0 at the merge)
     for (int u = 0; u < NU - 2; u += 2) {
-        aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l);
+        aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
         __builtin_amdgcn_sched_barrier(0);          // keep the loads ahead of the MFMAs they overlap
         bread_x3<NC>(slab, u / NG, lane, bh, bl);
         unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-        aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l);
+        aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (NG == 1) bread_x3<NC>(slab, u + 1, lane, bh, bl);
         unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
     }
-    aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l);
+    aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
     __builtin_amdgcn_sched_barrier(0);
     bread_x3<NC>(slab, (NU - 2) / NG, lane, bh, bl);
     unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
@@ -320,6 +329,22 @@ void rollout_x3(const RolloutArgs a) {
         return a.actions ? a.actions[((int64_t)h * a.K + c) * A + j]
                          : rng_action(a.seed, g, h, j, C[6 * 32 + j], C[7 * 32 + j]);
     };
+    // stage X3_NCH steps' action inputs from step h0: f64 normalise (dynamics.py:110),
+    // cast to f32 (TF feed); threads [0, nt) of the block
+    auto fill_actions = [&](int h0, int nt) {
+        const int nhs = (a.H - h0 < X3_NCH) ? a.H - h0 : X3_NCH;
+        const int per = CB * A;
+        for (int i = threadIdx.x; i < nhs * per; i += nt) {
+            const int hh = i / per, rem = i - hh * per, kl = rem / A, j = rem - kl * A;
+            float xv = 0.f;
+            if (cand0 + kl < a.K)
+                xv = (float)div_rn(__dsub_rn(act_value(h0 + hh, cand0 + kl, j), C[2 * 32 + j]), C[3 * 32 + j],
+                                   C[9 * 32 + j]);
+            xa[(hh * CB + kl) * A + j] = xv;
+        }
+    };
+    fill_actions(0, 64 * NW);
+    __syncthreads();
     const int voff = lane * 16;
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
     const __amdgpu_buffer_rsrc_t rso = layer_rsrc(a.w[L], a.wbytes[L]);
@@ -354,20 +379,6 @@ void rollout_x3(const RolloutArgs a) {
     uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.H; ++h) {
         X3_ST(0);
-        if (h % X3_NCH == 0) {
-            // ---- stage the next X3_NCH steps' action inputs (all threads): f64 normalise
-            //      (dynamics.py:110), cast to f32 (TF feed) ----
-            const int nhs = (a.H - h < X3_NCH) ? a.H - h : X3_NCH;
-            const int per = CB * A;
-            for (int i = threadIdx.x; i < nhs * per; i += 64 * NW) {
-                const int hh = i / per, rem = i - hh * per, kl = rem / A, j = rem - kl * A;
-                float xv = 0.f;
-                if (cand0 + kl < a.K)
-                    xv = (float)__ddiv_rn(__dsub_rn(act_value(h + hh, cand0 + kl, j), C[2 * 32 + j]), C[3 * 32 + j]);
-                xa[(hh * CB + kl) * A + j] = xv;
-            }
-            X3_BARRIER();
-        }
         if (owner && !X3_DIAG_NOOWNER) {
             // ---- normalise the state (dynamics.py:109), cast to f32, column scale, split ----
             float x[8];
@@ -377,7 +388,7 @@ void rollout_x3(const RolloutArgs a) {
                 const int v = i >> 2, r = i & 3;
                 const int d = 16 * v + 4 * q + r;
                 float xv = 0.f;
-                if (d < S) xv = (float)__ddiv_rn(__dsub_rn(s[v][r], C[0 * 32 + d]), C[1 * 32 + d]);
+                if (d < S) xv = (float)div_rn(__dsub_rn(s[v][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
                 else if (d < S + A) xv = xr[d - S];
                 x[i] = xv;
             }
@@ -487,6 +498,9 @@ void rollout_x3(const RolloutArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);              // (not hoisted above the MFMAs' operand waits)
         aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);                     // next step's layer 0
+        // the owners reach this point first (the older waves win the MFMA arbitration):
+        // they stage the next chunk's action inputs while the others finish
+        if (owner && (h + 1) % X3_NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * NC);
         X3_ST(7);
         X3_BARRIER();                                  // every wave is done reading the slab
 #pragma unroll
@@ -527,7 +541,7 @@ void rollout_x3(const RolloutArgs a) {
             }
         }
         if (a.cost == BCMPC_COST_CHEETAH) {
-            const double score = __dsub_rn(pen, __ddiv_rn(__dsub_rn(s[1][1], s17), 0.01));
+            const double score = __dsub_rn(pen, div_rn(__dsub_rn(s[1][1], s17), 0.01, 1.0 / 0.01));
             cost = __dadd_rn(cost, score);
         }
         if (a.traj && valid) {

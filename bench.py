@@ -123,8 +123,9 @@ def main():
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
     ap.add_argument("--actions", default="hbm", choices=["hbm", "device"],
                     help="hbm: [H,K,A] f64 actions resident in HBM (parity mode input); device: in-kernel Philox")
-    ap.add_argument("--precision", default=os.environ.get("BCMPC_PRECISION", "fp32"), choices=["fp32", "split"],
-                    help="fp32: f32 MFMA (rollout_grp); split: f32-accurate hi/lo f16 MFMA (rollout_x3, tanh nets)")
+    ap.add_argument("--precision", default=os.environ.get("BCMPC_PRECISION", "auto"), choices=["auto", "fp32", "split"],
+                    help="fp32: f32 MFMA (rollout_grp); split: f32-accurate hi/lo f16 MFMA (rollout_x3, tanh "
+                         "NNDynamicsModel without LayerNorm/policy); auto: split where it applies, else fp32")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -153,6 +154,8 @@ def main():
 
     wl = WORKLOADS[args.workload]
     K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
+    if args.precision == "auto":
+        args.precision = "split" if (act == "tanh" and not wl.get("reward") and not wl.get("policy")) else "fp32"
     offset = rank * K
 
     # synthetic inputs: glorot kernels, 0.1 N biases, synthetic stats/state

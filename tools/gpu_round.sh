@@ -11,7 +11,7 @@ stop_on() {  # stop on anything but success / ordinary test failures
     case $rc in 0) ;; 1) [ "$what" = pytest ] || exit $rc ;; *) echo "stopping after $what"; exit $rc ;; esac
 }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-    timeout -k 10 900 python -m pytest tests -m gpu -q -s -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+    timeout -k 10 900 python -u -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
     stop_on $? pytest
     tail -5 gpurun_out/pytest_gpu.log
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
