@@ -98,9 +98,10 @@ class RolloutEngine:
                  device: int = 0, cost: str = "cheetah", kernel: Optional[str] = None,
                  policy_hidden: int = 0, policy_layers: int = 0, policy_mode: str = "explore",
                  model: str = "delta", precision: Optional[str] = None):
-        """``precision``: "fp32" (v_mfma_f32_16x16x4_f32) or "split" (f32-accurate hi/lo f16
-        operands on v_mfma_f32_16x16x32_f16, rollout_x3.hip; tanh nets without LayerNorm).
-        Default: "split" for the split* kernels, else $BCMPC_PRECISION or "fp32"."""
+        """``precision``: "fp32" (v_mfma_f32_16x16x4_f32), "split" (f32-accurate hi/lo f16
+        operands on v_mfma_f32_16x16x32_f16, rollout_x3.hip; tanh NNDynamicsModel without
+        LayerNorm or fused policy) or "auto" (split where it applies, else fp32).
+        Default: "split" for the split* kernels, else $BCMPC_PRECISION or "auto"."""
         self._lib = _lib.load()
         if activation not in _ACT:
             raise ValueError(f"unsupported activation {activation!r} (tanh | relu)")
@@ -121,7 +122,11 @@ class RolloutEngine:
             raise ValueError(f"unknown kernel {kernel!r}; one of {sorted(_lib.KERNELS)}")
         cfg.kernel = _lib.KERNELS[kernel]
         if precision is None:
-            precision = "split" if kernel.startswith("split") else os.environ.get("BCMPC_PRECISION", "fp32")
+            precision = "split" if kernel.startswith("split") else os.environ.get("BCMPC_PRECISION", "auto")
+        if precision == "auto":
+            split_ok = (activation == "tanh" and not layer_norm and model == "delta" and not policy_hidden
+                        and kernel in ("auto", "split1", "split2", "split4"))
+            precision = "split" if split_ok else "fp32"
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"unknown precision {precision!r}; one of {sorted(_lib.PRECISIONS)}")
         cfg.precision = _lib.PRECISIONS[precision]

@@ -79,7 +79,7 @@ def test_cem_iterations_pinned_to_oracle(model):
     from oracle import mpc_oracle as orc
     K, H, A, E, iters, alpha, seed = 2048, 8, 6, 205, 4, 0.1, 0xC0FFEE
     low, high = -np.ones(A), np.ones(A)
-    kernel = "split2" if model == "delta-split" else "auto"
+    kernel = {"delta": "group4", "delta-split": "split2"}.get(model, "auto")   # f32 and split precision
     model = "delta" if model == "delta-split" else model
     spec, norm, dyn, score, state = _problem(model)
     eng = _engine(spec, norm, K, H, model, kernel)
