@@ -128,6 +128,8 @@ struct bcmpc_engine {
     double* d_actions = nullptr; size_t actions_cap = 0;
     double* d_costs = nullptr;
     bcmpc_result* d_result = nullptr;
+    double* d_amin_c = nullptr;         // argmin scratch: per-block best
+    int64_t* d_amin_i = nullptr;
     bcmpc_result* h_result = nullptr;   // pinned
     double h_consts[kConstRows * kConstCols]{};
     uint64_t version = 0;
@@ -296,6 +298,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         hipMalloc(&e->d_state, BCMPC_MAX_STATE * sizeof(double)) != hipSuccess ||
         hipMalloc(&e->d_costs, std::max<int64_t>(1, c.num_paths) * sizeof(double)) != hipSuccess ||
         hipMalloc(&e->d_result, sizeof(bcmpc_result)) != hipSuccess ||
+        hipMalloc(&e->d_amin_c, kArgminParts * sizeof(double)) != hipSuccess ||
+        hipMalloc(&e->d_amin_i, kArgminParts * sizeof(int64_t)) != hipSuccess ||
         hipHostMalloc(&e->h_result, sizeof(bcmpc_result), hipHostMallocDefault) != hipSuccess) {
         g_last_error = "device allocation failed";
         return cleanup(BCMPC_ERR_HIP);
@@ -341,7 +345,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
     for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
                     (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
-                    (void*)e->d_count})
+                    (void*)e->d_count, (void*)e->d_amin_c, (void*)e->d_amin_i})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
     for (auto& ev : e->ev)
@@ -641,6 +645,9 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         m.act_out = e->PL > 0 ? e->d_first : nullptr;
         m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
         m.maximize = c.cost == BCMPC_COST_REWARD;
+        m.scratch_c = e->d_amin_c;
+        m.scratch_i = e->d_amin_i;
+        m.nparts = argmin_parts(c.num_paths);
         if (cem) {
             m.cem_mu = cem->mu; m.cem_sigma = cem->sigma; m.cem_iter = cem->iter;
             m.merge = cem->merge; m.pos_base = cem->pos_base;

@@ -92,7 +92,12 @@ struct ArgminArgs {
     int32_t cem_iter;
     int32_t merge;           // keep out's previous best unless strictly better (np.argmin over iterations)
     int64_t pos_base;        // position of candidate 0 in the concatenated stream (iter * K_global + offset)
+    double* scratch_c;       // [kArgminParts] per-block best (argmin_partial -> argmin_final)
+    int64_t* scratch_i;
+    int32_t nparts;          // argmin_parts(K)
 };
+constexpr int kArgminParts = 256;
+int argmin_parts(int64_t K);
 
 int max_waves_per_block(int hidden_padded, int n_layers);
 hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per_block, hipStream_t st);

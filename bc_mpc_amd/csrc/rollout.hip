@@ -312,15 +312,12 @@ __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ argmin -------
-__global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
-    __shared__ double sc[16];
-    __shared__ int64_t si[16];
-    Best best{__builtin_inf(), INT64_MAX};
-    for (int64_t i = threadIdx.x; i < a.K; i += blockDim.x) {
-        const double v = a.costs[i];
-        const Best c{a.maximize ? -v : v, i};      // argmax(x) == argmin(-x), NaN-first and ties alike
-        if (better(c, best)) best = c;
-    }
+// np.argmin (controllers.py:82) in two short launches: argmin_partial reduces
+// contiguous chunks of the cost vector to one (cost, index) record per block,
+// argmin_final reduces the records and writes the result (index, cost, first
+// action).  better() is a total order (NaN first, then value, then lower index),
+// so the grouping cannot change the answer.
+__device__ __forceinline__ Best block_best(Best best, double* sc, int64_t* si) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         Best o{__shfl_xor(best.c, off), __shfl_xor(best.i, off)};
@@ -329,11 +326,40 @@ __global__ __launch_bounds__(1024) void argmin_kernel(const ArgminArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) { sc[wave] = best.c; si[wave] = best.i; }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0)
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
             const Best o{sc[w], si[w]};
             if (better(o, best)) best = o;
         }
+    return best;                                   // valid in thread 0
+}
+
+__global__ __launch_bounds__(256) void argmin_partial(const ArgminArgs a) {
+    __shared__ double sc[4];
+    __shared__ int64_t si[4];
+    const int64_t chunk = (a.K + gridDim.x - 1) / gridDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * chunk;
+    const int64_t i1 = i0 + chunk < a.K ? i0 + chunk : a.K;
+    Best best{__builtin_inf(), INT64_MAX};
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const double v = a.costs[i];
+        const Best c{a.maximize ? -v : v, i};      // argmax(x) == argmin(-x), NaN-first and ties alike
+        if (better(c, best)) best = c;
+    }
+    best = block_best(best, sc, si);
+    if (threadIdx.x == 0) { a.scratch_c[blockIdx.x] = best.c; a.scratch_i[blockIdx.x] = best.i; }
+}
+
+__global__ __launch_bounds__(256) void argmin_final(const ArgminArgs a) {
+    __shared__ double sc[4];
+    __shared__ int64_t si[4];
+    Best best{__builtin_inf(), INT64_MAX};
+    for (int b = threadIdx.x; b < a.nparts; b += blockDim.x) {
+        const Best c{a.scratch_c[b], a.scratch_i[b]};
+        if (better(c, best)) best = c;
+    }
+    best = block_best(best, sc, si);
+    if (threadIdx.x == 0) {
         bcmpc_result* out = a.out;
         if (a.merge) {        // CEM: np.argmin over the iteration-major concatenation; keep the earlier best on ties
             const double prev = out->best_cost;
@@ -402,8 +428,17 @@ hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per
 }
 
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(1024), 0, st, a);
+    if (a.nparts < 1 || a.nparts > kArgminParts) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(argmin_partial, dim3(a.nparts), dim3(256), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(argmin_final, dim3(1), dim3(256), 0, st, a);
     return hipGetLastError();
+}
+
+int argmin_parts(int64_t K) {
+    const int64_t p = (K + 511) / 512;             // >= 512 costs per block
+    return (int)(p < 1 ? 1 : (p > kArgminParts ? kArgminParts : p));
 }
 
 }  // namespace bcmpc

@@ -121,6 +121,21 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
     }
 }
 
+// cross-row exchanges on the VALU (gfx950 v_permlane16/32_swap) instead of LDS
+// round trips: max over the lane rows r^1 / r^2, and row 1's value in row 0
+__device__ __forceinline__ float max_rows16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_rows32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ int partner_row16(int v) {    // the value of row (r ^ 1), same column
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)r[0] == v ? (int)r[1] : (int)r[0];          // (equal values: either is right)
+}
+
 __device__ __forceinline__ h8 fload(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
     return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 }
@@ -155,6 +170,35 @@ __device__ __forceinline__ void unit_x3(const h8 (&ah)[G], const h8 (&al)[G], co
         for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(al[j], bh[c], acc[g * G + j][c]);
     }
 }
+
+// NG == 1 unit with the B fragments streamed per column (one column of lookahead,
+// 16 VGPRs instead of 8*NC): for register-tight layouts (X3_BSTREAM)
+template <int TW, int NC, int G>
+__device__ __forceinline__ void unit_x3s(const h8 (&ah)[G], const h8 (&al)[G], const f4* slab, int p, int lane,
+                                         f4 (&acc)[TW][NC]) {
+    h8 bh = sread(slab + sidx<NC>(p, 0, 0, lane));
+    h8 bl = sread(slab + sidx<NC>(p, 0, 1, lane));
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        h8 nbh = bh, nbl = bl;
+        if (c + 1 < NC) {
+            nbh = sread(slab + sidx<NC>(p, c + 1, 0, lane));
+            nbl = sread(slab + sidx<NC>(p, c + 1, 1, lane));
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) acc[j][c] = mfma16(ah[j], bh, acc[j][c]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) acc[j][c] = mfma16(ah[j], bl, acc[j][c]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) acc[j][c] = mfma16(al[j], bh, acc[j][c]);
+        bh = nbh;
+        bl = nbl;
+    }
+}
+
+#ifndef X3_BSTREAM
+#define X3_BSTREAM 0
+#endif
 
 template <int NC>
 __device__ __forceinline__ void bread_x3(const f4* slab, int p, int lane, h8 (&bh)[NC], h8 (&bl)[NC]) {
@@ -203,6 +247,22 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     h8 s1h[G], s1l[G], bh[NC], bl[NC];
     // (the last pair is peeled so that every load in the loop is unconditional: a
     // conditional load would make the compiler drain vmcnt to 0 at the merge)
+    if constexpr (NG == 1 && X3_BSTREAM) {
+        for (int u = 0; u < NU - 2; u += 2) {
+            aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
+            __builtin_amdgcn_sched_barrier(0);      // keep the loads ahead of the MFMAs they overlap
+            unit_x3s<TW, NC, G>(s0h, s0l, slab, u, lane, acc);
+            aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
+            __builtin_amdgcn_sched_barrier(0);
+            unit_x3s<TW, NC, G>(s1h, s1l, slab, u + 1, lane, acc);
+        }
+        aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
+        __builtin_amdgcn_sched_barrier(0);
+        unit_x3s<TW, NC, G>(s0h, s0l, slab, NU - 2, lane, acc);
+        unit_x3s<TW, NC, G>(s1h, s1l, slab, NU - 1, lane, acc);
+        (void)bh; (void)bl;
+        return;
+    }
     for (int u = 0; u < NU - 2; u += 2) {
         aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
         __builtin_amdgcn_sched_barrier(0);          // keep the loads ahead of the MFMAs they overlap
@@ -253,14 +313,15 @@ __host__ __device__ constexpr int x3_group(int TW) { return TW <= 4 ? TW : TW / 
 // waves per SIMD the register allocator must allow: two whenever two workgroups
 // (or two waves of one) should share a SIMD
 __host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
-    return (NW >= 8 || HP <= 512) ? 2 : 1;
+    return NW >= 16 ? 4 : (NW >= 8 || HP <= 512) ? 2 : 1;
 }
 
-// LDS carve-up: consts | biases (L*HP + 32) | column factors NC*16 | action inputs
+// LDS carve-up: consts | biases (L*HP + 32) | column factors NC*16 | column max [2][NC*16] |
+// penalty counts [2][NC*16] | action inputs
 // X3_NCH*16NC*A (16-B aligned) | layer-0 slab NC*2 KiB | slab (P+1)*NC*2 KiB
 __host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
 __host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A) {
-    return param_bytes(L, HP) + NC * 16 * 4 + x3_xa_bytes(NC, A) + NC * 2048 + (HP / 32 + 1) * NC * 2048;
+    return param_bytes(L, HP) + NC * 16 * 4 * 5 + x3_xa_bytes(NC, A) + NC * 2048 + (HP / 32 + 1) * NC * 2048;
 }
 
 template <int HP, int NC, int NW>
@@ -281,8 +342,14 @@ void rollout_x3(const RolloutArgs a) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4;
     const int m = lane & 15;
-    const bool owner = w < NC;
-    const int cw = owner ? w : 0;                       // the owner's column
+    // State ownership.  SO (2*NC <= NW): two waves per column, wave w < 2*NC owns half
+    // hv0 = w / NC of column w % NC (dims 16*hv0 + 4q + r), which halves the serial f64
+    // phase; otherwise waves w < NC own both halves of column w.
+    constexpr bool SO = 2 * NC <= NW;
+    constexpr int NHV = SO ? 1 : 2;                     // halves per state wave
+    const bool owner = w < (SO ? 2 * NC : NC);
+    const int cw = owner ? w % NC : 0;                  // the owner's column
+    const int hv0 = SO ? (owner ? w / NC : 0) : 0;      // the owner's first half
     const int64_t cand0 = (int64_t)blockIdx.x * CB;
     const int64_t cand = cand0 + 16 * cw + m;
     const bool valid = owner && cand < a.K;
@@ -296,29 +363,32 @@ void rollout_x3(const RolloutArgs a) {
     float* const Bout = Bl + L * HP;
     for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[L][i];
     float* colf = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP));
-    float* xa = colf + NC * 16;                         // [X3_NCH][CB][A] normalised action inputs (f32)
+    float* colmax = colf + NC * 16;                     // [half][NC*16]: per-half column max (split owners)
+    int* penbuf = reinterpret_cast<int*>(colmax + 2 * NC * 16);   // [step & 1][NC*16] penalty counts
+    float* xa = reinterpret_cast<float*>(penbuf + 2 * NC * 16);   // [X3_NCH][CB][A] normalised action inputs
     f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + x3_xa_bytes(NC, A));
     f4* slab = slab0 + NC * 2 * 64;
     __syncthreads();
 
-    double s[2][4];
+    double s[NHV][4];                                   // dims 16*(hv0+k) + 4q + r
 #pragma unroll
-    for (int v = 0; v < 2; ++v)
+    for (int k = 0; k < NHV; ++k)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int d = 16 * v + 4 * q + r;
-            s[v][r] = (valid && d < S) ? a.state[cand * a.state_stride + d] : 0.0;
+            const int d = 16 * (hv0 + k) + 4 * q + r;
+            s[k][r] = (valid && d < S) ? a.state[cand * a.state_stride + d] : 0.0;
         }
     if (a.traj && valid) {
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+        for (int k = 0; k < NHV; ++k)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int d = 16 * v + 4 * q + r;
-                if (d < S) a.traj[cand * S + d] = s[v][r];
+                const int d = 16 * (hv0 + k) + 4 * q + r;
+                if (d < S) a.traj[cand * S + d] = s[k][r];
             }
     }
     double cost = 0.0;                                  // trajectory_cost = 0 (cost_functions.py:60)
+    double prog_prev = 0.0;                             // SO: the half-1 owner's progress term, one step late
     // action j of candidate c at step h: the caller's [H,K,A] array (np.random.uniform,
     // controllers.py:53), Philox, or the CEM sampler
     auto act_value = [&](int h, int64_t c, int j) -> double {
@@ -379,36 +449,62 @@ void rollout_x3(const RolloutArgs a) {
     uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.H; ++h) {
         X3_ST(0);
+        float xin[4 * NHV];                               // layer-0 input slots 4*(hv0+k) + r
+        float mx = 0.f;
         if (owner && !X3_DIAG_NOOWNER) {
-            // ---- normalise the state (dynamics.py:109), cast to f32, column scale, split ----
-            float x[8];
+            // ---- normalise the state (dynamics.py:109), cast to f32 (TF feed), column max ----
             const float* xr = xa + ((h % X3_NCH) * CB + 16 * cw + m) * A;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int v = i >> 2, r = i & 3;
-                const int d = 16 * v + 4 * q + r;
-                float xv = 0.f;
-                if (d < S) xv = (float)div_rn(__dsub_rn(s[v][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
-                else if (d < S + A) xv = xr[d - S];
-                x[i] = xv;
-            }
-            float mx = 0.f;
+            for (int k = 0; k < NHV; ++k)
 #pragma unroll
-            for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fabsf(x[i]));
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
+                for (int r = 0; r < 4; ++r) {
+                    const int d = 16 * (hv0 + k) + 4 * q + r;
+                    float xv = 0.f;
+                    if (d < S) xv = (float)div_rn(__dsub_rn(s[k][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
+                    else if (d < S + A) xv = xr[d - S];
+                    xin[4 * k + r] = xv;
+                }
+#pragma unroll
+            for (int i = 0; i < 4 * NHV; ++i) mx = fmaxf(mx, fabsf(xin[i]));
+            mx = max_rows32(max_rows16(mx));
+            if constexpr (SO) {
+                if (q == 0) colmax[hv0 * NC * 16 + cw * 16 + m] = mx;
+            }
+        }
+        if constexpr (SO) {
+            X3_BARRIER();                                 // both halves' column maxima published
+            if (owner && !X3_DIAG_NOOWNER) mx = fmaxf(mx, colmax[(1 - hv0) * NC * 16 + cw * 16 + m]);
+        }
+        if (owner && !X3_DIAG_NOOWNER) {
+            // ---- column scale (max |x| -> [2^11, 2^12)), split, publish ----
             int e = 0;
             (void)frexpf(mx, &e);                         // mx in [2^(e-1), 2^e)
             int sh = 12 - e;
             sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
             const float sc = ldexpf(1.0f, sh);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] *= sc;
-            h8 xh, xl;
-            split8(x, xh, xl);
-            swrite(slab0 + (cw * 2 + 0) * 64 + lane, xh);
-            swrite(slab0 + (cw * 2 + 1) * 64 + lane, xl);
-            if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kTanhK;
+            for (int i = 0; i < 4 * NHV; ++i) xin[i] *= sc;
+            if constexpr (SO) {
+                typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                h4 xh, xl;
+#pragma unroll
+                for (int i = 0; i < 4; i += 2) {
+                    h2 hh, ll;
+                    split2(xin[i], xin[i + 1], hh, ll);
+                    xh[i] = hh[0]; xh[i + 1] = hh[1];
+                    xl[i] = ll[0]; xl[i + 1] = ll[1];
+                }
+                // this half's 4 slots are bytes [8*hv0, 8*hv0+8) of the lane's 16-byte B fragment
+                reinterpret_cast<h4*>(slab0 + (cw * 2 + 0) * 64 + lane)[hv0] = xh;
+                reinterpret_cast<h4*>(slab0 + (cw * 2 + 1) * 64 + lane)[hv0] = xl;
+                if (hv0 == 0 && q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kTanhK;
+            } else {
+                h8 xh, xl;
+                split8(xin, xh, xl);
+                swrite(slab0 + (cw * 2 + 0) * 64 + lane, xh);
+                swrite(slab0 + (cw * 2 + 1) * 64 + lane, xl);
+                if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kTanhK;
+            }
         }
         X3_ST(1);
         X3_BARRIER();                                  // layer-0 input published
@@ -500,7 +596,7 @@ void rollout_x3(const RolloutArgs a) {
         aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);                     // next step's layer 0
         // the owners reach this point first (the older waves win the MFMA arbitration):
         // they stage the next chunk's action inputs while the others finish
-        if (owner && (h + 1) % X3_NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * NC);
+        if (owner && (h + 1) % X3_NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * (SO ? 2 * NC : NC));
         X3_ST(7);
         X3_BARRIER();                                  // every wave is done reading the slab
 #pragma unroll
@@ -511,50 +607,72 @@ void rollout_x3(const RolloutArgs a) {
         X3_ST(8);
         if (!owner || X3_DIAG_NOOWNER) continue;
 
-        f4 o[2];
+        f4 o[NHV];
 #pragma unroll
-        for (int v = 0; v < 2; ++v) o[v] = slab[((0 * 2 + v) * NC + cw) * 64 + lane];
+        for (int k = 0; k < NHV; ++k) o[k] = slab[((0 * 2 + hv0 + k) * NC + cw) * 64 + lane];
 #pragma unroll
         for (int g = 1; g < NW; ++g)                      // fixed summation order
 #pragma unroll
-            for (int v = 0; v < 2; ++v) o[v] += slab[((g * 2 + v) * NC + cw) * 64 + lane];
+            for (int k = 0; k < NHV; ++k) o[k] += slab[((g * 2 + hv0 + k) * NC + cw) * 64 + lane];
 
-        // ---- cheetah penalties on the current state (cost_functions.py:16-26) ----
-        double pen = 0.0;
-        if (s[0][1] >= 0.2) pen += 10.0;
-        if (s[0][2] >= 0.0) pen += 10.0;
-        if (s[0][3] >= 0.0) pen += 10.0;
-        pen = __shfl(pen, m + 16);                        // dims 5,6,7 live in lane group q=1
-        const double s17 = s[1][1];                       // dim 17 lives in lane group q=0
+        // ---- cheetah penalties on the current state (cost_functions.py:16-26): dims 5, 6, 7
+        //      live in lane row q = 1 of half 0; 0 + 10 + 10 + 10 in the reference's order is
+        //      exactly 10 * count ----
+        int npen = 0;
+        if (hv0 == 0) npen = partner_row16((s[0][1] >= 0.2) + (s[0][2] >= 0.0) + (s[0][3] >= 0.0));
+        const double s17 = s[NHV - 1][1];                 // dim 17: half 1, row q = 0, r = 1
         // ---- de-normalise + residual (dynamics.py:113,116), f64, no FMA ----
 #pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            const f4 bv = *reinterpret_cast<const f4*>(Bout + 16 * v + 4 * q);
+        for (int k = 0; k < NHV; ++k) {
+            const f4 bv = *reinterpret_cast<const f4*>(Bout + 16 * (hv0 + k) + 4 * q);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int d = 16 * v + 4 * q + r;
+                const int d = 16 * (hv0 + k) + 4 * q + r;
                 if (d < S) {
-                    const float dn = fmaf(o[v][r], fo, bv[r]);             // BiasAdd (f32)
+                    const float dn = fmaf(o[k][r], fo, bv[r]);             // BiasAdd (f32)
                     const double ud = __dadd_rn(__dmul_rn((double)dn, C[5 * 32 + d]), C[4 * 32 + d]);
-                    s[v][r] = __dadd_rn(s[v][r], ud);
+                    s[k][r] = __dadd_rn(s[k][r], ud);
                 }
             }
         }
         if (a.cost == BCMPC_COST_CHEETAH) {
-            const double score = __dsub_rn(pen, div_rn(__dsub_rn(s[1][1], s17), 0.01, 1.0 / 0.01));
-            cost = __dadd_rn(cost, score);
+            // score = pen - (s'17 - s17) / 0.01 (cost_functions.py:28), summed in step order (:59-63)
+            if constexpr (SO) {
+                // half 0 hands its penalty count to half 1 through LDS; half 1 adds step h-1's
+                // score now (the count is visible after this step's barriers) and step H-1's
+                // after the loop
+                if (hv0 == 0) {
+                    if (q == 0) penbuf[(h & 1) * NC * 16 + cw * 16 + m] = npen;
+                } else {
+                    if (h > 0) {
+                        const double pen = 10.0 * (double)penbuf[((h - 1) & 1) * NC * 16 + cw * 16 + m];
+                        cost = __dadd_rn(cost, __dsub_rn(pen, prog_prev));
+                    }
+                    prog_prev = div_rn(__dsub_rn(s[0][1], s17), 0.01, 1.0 / 0.01);
+                }
+            } else {
+                const double score = __dsub_rn(10.0 * (double)npen, div_rn(__dsub_rn(s[1][1], s17), 0.01, 1.0 / 0.01));
+                cost = __dadd_rn(cost, score);
+            }
         }
         if (a.traj && valid) {
 #pragma unroll
-            for (int v = 0; v < 2; ++v)
+            for (int k = 0; k < NHV; ++k)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int d = 16 * v + 4 * q + r;
-                    if (d < S) a.traj[((int64_t)(h + 1) * a.K + cand) * S + d] = s[v][r];
+                    const int d = 16 * (hv0 + k) + 4 * q + r;
+                    if (d < S) a.traj[((int64_t)(h + 1) * a.K + cand) * S + d] = s[k][r];
                 }
         }
     }
-    if (a.costs && valid && q == 0) a.costs[cand] = cost;
+    if constexpr (SO) {
+        __syncthreads();                                  // the last step's penalty counts
+        if (a.cost == BCMPC_COST_CHEETAH && owner && hv0 == 1 && a.H > 0) {
+            const double pen = 10.0 * (double)penbuf[((a.H - 1) & 1) * NC * 16 + cw * 16 + m];
+            cost = __dadd_rn(cost, __dsub_rn(pen, prog_prev));
+        }
+    }
+    if (a.costs && valid && q == 0 && (SO ? hv0 == 1 : true)) a.costs[cand] = cost;   // the cost holder
     if constexpr (X3_STAMP) {
         if (a.stamps && lane == 0)
             for (int k = 0; k < 10; ++k) a.stamps[((size_t)blockIdx.x * NW + w) * 10 + k] = ph_[k];

@@ -13,8 +13,14 @@ make -s -j8 ARCH=gfx950 >/dev/null
 $H -x hip -c bc_mpc_amd/csrc/capi.cpp -o build/variants/capi.o
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
+  src=bc_mpc_amd/csrc/rollout_x3.hip
+  if [[ "$name" == *@* ]]; then     # name@gitref: the split kernel source at that revision
+    ref=${name#*@}; name=${name%%@*}
+    git show "$ref":bc_mpc_amd/csrc/rollout_x3.hip > bc_mpc_amd/csrc/_x3_$name.hip
+    src=bc_mpc_amd/csrc/_x3_$name.hip
+  fi
   if [ $X3 = 1 ]; then
-    ( $H $flags -DX3_ONLY=512 -c bc_mpc_amd/csrc/rollout_x3.hip -o build/variants/rollout_x3_$name.o &&
+    ( $H $flags -DX3_ONLY=512 -c $src -o build/variants/rollout_x3_$name.o &&
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
           build/rollout.o build/rollout_grp.o build/cem.o build/variants/rollout_x3_$name.o build/variants/capi.o ) &
   else
@@ -26,4 +32,5 @@ for spec in "$@"; do
   fi
 done
 wait
+rm -f bc_mpc_amd/csrc/_x3_*.hip
 ls build/variants/*.so
