@@ -4,7 +4,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
-OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/cem.o build/capi.o
+OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/cem.o build/fit.o build/capi.o
 HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h
 
 all: $(LIB)
@@ -18,6 +18,10 @@ build/rollout_grp.o: $(SRC)/rollout_grp.hip $(HDR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 build/rollout_x3.o: $(SRC)/rollout_x3.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build/fit.o: $(SRC)/fit.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

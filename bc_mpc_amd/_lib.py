@@ -114,6 +114,23 @@ class Result(ctypes.Structure):
 
 
 # (name, restype, argtypes) -- every symbol include/bcmpc.h declares
+class FitConfig(ctypes.Structure):
+    _fields_ = [
+        ("state_dim", ctypes.c_int32),
+        ("action_dim", ctypes.c_int32),
+        ("hidden", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("activation", ctypes.c_int32),
+        ("layer_norm", ctypes.c_int32),
+        ("batch_size", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("learning_rate", ctypes.c_float),
+        ("beta1", ctypes.c_float),
+        ("beta2", ctypes.c_float),
+        ("epsilon", ctypes.c_float),
+    ]
+
+
 SIGNATURES = [
     ("bcmpc_abi_version", ctypes.c_int, []),
     ("bcmpc_last_error", ctypes.c_char_p, []),
@@ -144,6 +161,15 @@ SIGNATURES = [
     ("bcmpc_stream", ctypes.c_void_p, [ctypes.c_void_p]),
     ("bcmpc_last_kernel_ms", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+    ("bcmpc_fit_create", ctypes.c_int, [ctypes.POINTER(FitConfig), ctypes.POINTER(ctypes.c_void_p)]),
+    ("bcmpc_fit_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("bcmpc_fit_set_params", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Weights)]),
+    ("bcmpc_fit_get_params", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(_FP), ctypes.POINTER(_FP), ctypes.POINTER(_FP), ctypes.POINTER(_FP)]),
+    ("bcmpc_fit_set_data", ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, ctypes.c_int64]),
+    ("bcmpc_fit_run", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _FP]),
+    ("bcmpc_fit_last_error", ctypes.c_char_p, []),
     ("bcmpc_engine_info", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
       ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
@@ -178,10 +204,11 @@ class BcmpcError(RuntimeError):
         self.code = code
 
 
-def check(code: int) -> None:
+def check(code: int, fit: bool = False) -> None:
     if code == OK:
         return
-    msg = load().bcmpc_last_error().decode(errors="replace")
+    lib = load()
+    msg = (lib.bcmpc_fit_last_error() if fit else lib.bcmpc_last_error()).decode(errors="replace")
     if code == ERR_EMPTY:
         raise ValueError(msg)                  # np.argmin on an empty sequence
     if code in (ERR_ARG, ERR_UNSUPPORTED):

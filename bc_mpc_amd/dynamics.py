@@ -9,8 +9,8 @@ controller's re-sync hook compares.
 
 ``predict`` (dynamics.py:106-119) runs one horizon step of the same HIP
 kernel in per-candidate-state mode; it never computes on the host.
-``fit`` (dynamics.py:81-104, Adam on normalized deltas) is outside the
-rollout hot path and not provided here.
+``fit`` (dynamics.py:81-104, Adam on normalized deltas) runs on the GPU
+(``bc_mpc_amd/fit.py``), off the control-step path.
 """
 from __future__ import annotations
 
@@ -118,8 +118,26 @@ class NNDynamicsModel():
         return d_traj[1].cpu().numpy()
 
     def fit(self, data):  # dynamics.py:81-104
-        raise NotImplementedError("dynamics training is outside the rollout engine (SURVEY 8f rank 4); "
-                                  "fit elsewhere and call load_weights()")
+        """``iterations`` Adam steps on the GPU (bc_mpc_amd/fit.py, csrc/fit.hip) on batches drawn
+        exactly as DataBufferGeneral.sample draws them; returns (last loss, 0) like the reference."""
+        import torch
+        from .fit import GPUFitter, buffer_arrays, sample_batches
+        dev = self.device if self.device is not None else torch.cuda.current_device()
+        if getattr(self, "_fitter", None) is None:
+            self._fitter = GPUFitter(self.state_dim, self.action_dim, self.size, self.n_layers, self.activation,
+                                     self.layer_norm, int(self.batch_size), float(self.learning_rate), dev)
+            self._fit_version = None
+        if self._fit_version != self.version:               # weights changed outside fit: re-upload
+            self._fitter.set_params(self.mlp_spec(), self.normalization())
+        states, actions, deltas = buffer_arrays(data)
+        self._fitter.set_data(states, actions, deltas)
+        size = int(getattr(data, "size", states.shape[0]))
+        print("Model fitting for ", self.iterations, "times ... ")   # dynamics.py:88
+        losses = self._fitter.run(sample_batches(size, int(self.batch_size), int(self.iterations)))
+        ks, bs, gs, bes = self._fitter.get_params()
+        self.load_weights(ks, bs, gs if self.layer_norm else None, bes if self.layer_norm else None)
+        self._fit_version = self.version
+        return (float(losses[-1]) if len(losses) else None), 0
 
 
 class NNDynamicsRewardModel():

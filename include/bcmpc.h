@@ -250,6 +250,44 @@ int bcmpc_select_async(bcmpc_engine* eng, const bcmpc_elite* d_pairs, const doub
 int bcmpc_cem_refit_async(bcmpc_engine* eng, const bcmpc_elite* d_elite, const int32_t* d_count, uint64_t seed,
                           int32_t iteration, double alpha, double* d_mu, double* d_sigma, void* stream);
 
+/* ------------------------------------------------------------------------
+ * NNDynamicsModel.fit (dynamics.py:81-104) on the GPU:
+ * `iterations` Adam steps (TF1 AdamOptimizer, dynamics.py:50-52) on the mean
+ * squared error of the normalised state deltas, batches gathered on the device
+ * from a resident copy of the model data buffer by host-chosen row indices (the
+ * caller draws them exactly as DataBufferGeneral.sample does, data_buffer.py:45-57).
+ * A fitter owns the f32 parameters and the Adam slots (m, v, beta powers), which
+ * persist across runs like the reference's optimizer variables. */
+typedef struct bcmpc_fit_config {
+    int32_t state_dim;     /* S */
+    int32_t action_dim;    /* A */
+    int32_t hidden;        /* h (true width, no padding) */
+    int32_t n_layers;      /* L */
+    int32_t activation;    /* bcmpc_activation */
+    int32_t layer_norm;    /* FLAGS.LAYER_NORM (dynamics.py:68) */
+    int32_t batch_size;    /* dynamics.py:48 batch_size (max rows per step) */
+    int32_t device;
+    float learning_rate;   /* dynamics.py:47 */
+    float beta1, beta2, epsilon;   /* tf.train.AdamOptimizer defaults 0.9, 0.999, 1e-8 */
+} bcmpc_fit_config;
+
+typedef struct bcmpc_fitter bcmpc_fitter;
+
+int bcmpc_fit_create(const bcmpc_fit_config* cfg, bcmpc_fitter** out);
+int bcmpc_fit_destroy(bcmpc_fitter* f);
+/* parameters (TF layout [in, out] kernels, biases, LN gamma/beta) + the normalization stats */
+int bcmpc_fit_set_params(bcmpc_fitter* f, const bcmpc_weights* w);
+int bcmpc_fit_get_params(bcmpc_fitter* f, float* const* kernels, float* const* biases, float* const* ln_gamma,
+                         float* const* ln_beta);
+/* the model data buffer: n rows of state (S), action (A), state delta (S), f64, uploaded to HBM */
+int bcmpc_fit_set_data(bcmpc_fitter* f, const double* states, const double* actions, const double* deltas,
+                       int64_t n);
+/* `iterations` steps; step i uses batch_sizes[i] rows, indices concatenated in `indices`;
+ * losses (optional, host, [iterations]) = each step's loss before its update */
+int bcmpc_fit_run(bcmpc_fitter* f, const int64_t* indices, const int32_t* batch_sizes, int32_t iterations,
+                  float* losses);
+const char* bcmpc_fit_last_error(void);
+
 /* Device stream the engine launches on (hipStream_t as void*). */
 void* bcmpc_stream(bcmpc_engine* eng);
 

@@ -660,3 +660,148 @@ def near_threshold_mask(states_paths_all: np.ndarray, delta: float = 1e-4) -> np
 def argmin_ref(costs: np.ndarray) -> int:
     """np.argmin semantics the engine must reproduce (first NaN, else first min)."""
     return int(np.argmin(costs))
+
+
+# ----------------------------------------------------------------------------
+# NNDynamicsModel.fit restatement (dynamics.py:44-52, 81-104) -- SURVEY 8f rank 4
+# ----------------------------------------------------------------------------
+# TF1 graph: loss = reduce_mean(squared_difference(delta, pred)); AdamOptimizer(lr)
+# .minimize(loss).  The gradients below are the autodiff of exactly those ops,
+# written out (TF is absent here: "parity unpinned" at the TF boundary, like the
+# MLP itself); the Adam step is TF1's ApplyAdam kernel.
+
+@dataclass
+class AdamState:
+    """tf.train.AdamOptimizer slots + the f32 beta-power variables (persist across fit calls)."""
+    m: List[np.ndarray]
+    v: List[np.ndarray]
+    beta1_power: np.float32
+    beta2_power: np.float32
+
+    @classmethod
+    def zeros_like(cls, params: Sequence[np.ndarray], beta1=0.9, beta2=0.999) -> "AdamState":
+        return cls([np.zeros_like(p, dtype=np.float32) for p in params],
+                   [np.zeros_like(p, dtype=np.float32) for p in params], np.float32(beta1), np.float32(beta2))
+
+
+def fit_params(w: MLPWeights) -> List[np.ndarray]:
+    """Trainable variables in TF creation order: per dense layer kernel, bias; per LN gamma... the
+    order only matters for bookkeeping -- [W0, b0, ..., WL, bL] + [g0, be0, ...] (LN)."""
+    ps = []
+    for k, b in zip(w.kernels, w.biases):
+        ps += [np.asarray(k, np.float32), np.asarray(b, np.float32)]
+    if w.layer_norm:
+        for g, be in zip(w.ln_gamma, w.ln_beta):
+            ps += [np.asarray(g, np.float32), np.asarray(be, np.float32)]
+    return ps
+
+
+def _split_params(ps: Sequence[np.ndarray], L: int, ln: bool):
+    ks = [ps[2 * i] for i in range(L + 1)]
+    bs = [ps[2 * i + 1] for i in range(L + 1)]
+    gs = [ps[2 * (L + 1) + 2 * i] for i in range(L)] if ln else None
+    bes = [ps[2 * (L + 1) + 2 * i + 1] for i in range(L)] if ln else None
+    return ks, bs, gs, bes
+
+
+def fit_batch(normalization, states, actions, deltas):
+    """dynamics.py:92-95: normalize(x, std, mean) = (x - mean)/(std + 1e-10) in f64, fed as f32."""
+    (mean_obs, std_obs, mean_action, std_action, _mr, _sr, _mn, _sn, mean_deltas, std_deltas) = normalization
+    ns = (np.asarray(states, np.float64) - mean_obs) / (std_obs + NORM_EPS)
+    na = (np.asarray(actions, np.float64) - mean_action) / (std_action + NORM_EPS)
+    nd = (np.asarray(deltas, np.float64) - mean_deltas) / (std_deltas + NORM_EPS)
+    x0 = np.concatenate([ns.astype(np.float32), na.astype(np.float32)], axis=1)
+    return x0, nd.astype(np.float32)
+
+
+def fit_grads(ps: Sequence[np.ndarray], L: int, act: str, ln: bool, x0: np.ndarray, t: np.ndarray,
+              dtype=np.float32):
+    """Loss and d(loss)/d(params) for one batch (f32 throughout, TF op semantics; ``dtype``
+    float64 only for the finite-difference check of the restated derivatives)."""
+    f32 = dtype
+    ks, bs, gs, bes = _split_params(ps, L, ln)
+    hs, As, means, rss = [x0], [], [], []
+    h = x0
+    for l in range(L):
+        z = h @ ks[l] + bs[l]
+        a = (np.tanh(z) if act == "tanh" else np.maximum(z, f32(0))).astype(f32)
+        As.append(a)
+        if ln:
+            mean = np.mean(a, axis=1, keepdims=True, dtype=f32)
+            var = np.mean(np.square(a - mean), axis=1, keepdims=True, dtype=f32)
+            rs = f32(1) / np.sqrt(var + f32(LN_EPS))
+            inv = rs * gs[l]
+            h = a * inv + (bes[l] - mean * inv)
+            means.append(mean)
+            rss.append(rs)
+        else:
+            h = a
+        hs.append(h)
+    p = h @ ks[L] + bs[L]
+    n = p.size
+    d = t - p
+    loss = f32(np.mean(np.square(d), dtype=f32))
+    dp = -((f32(2.0) * (f32(1.0) / f32(n))) * d)             # SquaredDifference / Mean grads
+    gk = [None] * (L + 1)
+    gb = [None] * (L + 1)
+    gg = [None] * L if ln else None
+    gbe = [None] * L if ln else None
+    gk[L] = hs[L].T @ dp
+    gb[L] = np.sum(dp, axis=0, dtype=f32)
+    dh = dp @ ks[L].T
+    for l in range(L - 1, -1, -1):
+        a = As[l]
+        if ln:
+            mean, rs = means[l], rss[l]
+            xhat = (a - mean) * rs
+            gbe[l] = np.sum(dh, axis=0, dtype=f32)
+            gg[l] = np.sum(dh * xhat, axis=0, dtype=f32)
+            F = f32(a.shape[1])
+            inv = rs * gs[l]
+            dmean = -np.sum(dh * inv, axis=1, keepdims=True, dtype=f32)
+            drs = np.sum(dh * (a - mean) * gs[l], axis=1, keepdims=True, dtype=f32)
+            dvar = f32(-0.5) * drs * rs * rs * rs
+            da = dh * inv + dmean / F + dvar * f32(2.0) * (a - mean) / F
+        else:
+            da = dh
+        dz = da * (a > 0) if act == "relu" else da * (f32(1) - a * a)
+        dz = dz.astype(f32)
+        gk[l] = hs[l].T @ dz
+        gb[l] = np.sum(dz, axis=0, dtype=f32)
+        if l > 0:
+            dh = dz @ ks[l].T
+    grads = []
+    for l in range(L + 1):
+        grads += [gk[l].astype(f32), gb[l].astype(f32)]
+    if ln:
+        for l in range(L):
+            grads += [gg[l], gbe[l]]
+    return loss, grads
+
+
+def adam_apply(ps: List[np.ndarray], grads: Sequence[np.ndarray], st: AdamState, lr: float,
+               beta1=0.9, beta2=0.999, eps=1e-8) -> None:
+    """TF1 ApplyAdam (training_ops.cc): lr_t = lr*sqrt(1-b2^t)/(1-b1^t) from the f32 beta
+    powers; m += (g-m)(1-b1); v += (g^2-v)(1-b2); w -= (m lr_t)/(sqrt(v)+eps); then the
+    powers are multiplied by beta (AdamOptimizer._finish)."""
+    f32 = np.float32
+    b1, b2 = f32(beta1), f32(beta2)
+    lr_t = f32(lr) * np.sqrt(f32(1) - st.beta2_power) / (f32(1) - st.beta1_power)
+    for i, g in enumerate(grads):
+        st.m[i] = (st.m[i] + (g - st.m[i]) * (f32(1) - b1)).astype(f32)
+        st.v[i] = (st.v[i] + (g * g - st.v[i]) * (f32(1) - b2)).astype(f32)
+        ps[i] = (ps[i] - (st.m[i] * lr_t) / (np.sqrt(st.v[i]) + f32(eps))).astype(f32)
+    st.beta1_power = f32(st.beta1_power * b1)
+    st.beta2_power = f32(st.beta2_power * b2)
+
+
+def fit(ps: List[np.ndarray], st: AdamState, L: int, act: str, ln: bool, normalization, data_states,
+        data_actions, data_deltas, batches: Sequence[np.ndarray], lr: float):
+    """dynamics.py:81-104 over explicit batch index lists; returns the per-step losses."""
+    losses = []
+    for idx in batches:
+        x0, t = fit_batch(normalization, data_states[idx], data_actions[idx], data_deltas[idx])
+        loss, grads = fit_grads(ps, L, act, ln, x0, t)
+        adam_apply(ps, grads, st, lr)
+        losses.append(loss)
+    return losses
