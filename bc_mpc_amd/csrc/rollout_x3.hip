@@ -289,10 +289,29 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
     const f4 b0 = *reinterpret_cast<const f4*>(bias + 16 * t0 + 4 * q);
     const f4 b1 = *reinterpret_cast<const f4*>(bias + 16 * (t0 + 1) + 4 * q);
     float v[8];
+    if constexpr (X3_DIAG_NOTANH) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        v[r] = tanh_x4096(fmaf(a0[r], f, b0[r]));
-        v[4 + r] = tanh_x4096(fmaf(a1[r], f, b1[r]));
+        for (int r = 0; r < 4; ++r) {
+            v[r] = tanh_x4096(fmaf(a0[r], f, b0[r]));
+            v[4 + r] = tanh_x4096(fmaf(a1[r], f, b1[r]));
+        }
+    } else {
+        // the tanh_x4096 arithmetic on element pairs: the fmas as v_pk_fma_f32 (bit-identical,
+        // half the VALU issue), exp / rcp / sign per element
+        const f2 c = {1.0f / 4096.0f, 1.0f / 4096.0f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f4& a = k < 2 ? a0 : a1;
+            const f4& b = k < 2 ? b0 : b1;
+            const int r = (k & 1) * 2;
+            const f2 z = __builtin_elementwise_fma((f2){a[r], a[r + 1]}, (f2){f, f}, (f2){b[r], b[r + 1]});
+            const f2 t = {__builtin_amdgcn_exp2f(-fabsf(z[0])), __builtin_amdgcn_exp2f(-fabsf(z[1]))};
+            const f2 d = __builtin_elementwise_fma(t, c, c);
+            const f2 rr = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+            const f2 u = __builtin_elementwise_fma(-t, rr, rr);
+            v[2 * k] = __builtin_copysignf(u[0], z[0]);
+            v[2 * k + 1] = __builtin_copysignf(u[1], z[1]);
+        }
     }
     split8(v, hi, lo);
 }
