@@ -87,3 +87,32 @@ def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optiona
     if best[0] < 0.5:
         raise ValueError("attempt to get argmin of an empty sequence")
     return float(best[1]), int(best[2]), best[3:].copy()
+
+
+def allgather_result(d_result, action_dim: int, maximize: bool = False, group=None) -> Tuple[float, int, np.ndarray]:
+    """The same exchange straight from the device: ``d_result`` is this rank's ``bcmpc_result``
+    (144 bytes: int64 index, f64 cost, f64 first_action[16]) as a uint8 CUDA tensor, written by
+    the argmin launch; the all-gather is stream-ordered after it, so there is no host round trip
+    before the collective and one device-to-host copy after it.  Every rank must hold >= 1
+    candidate (K > 0).  ``maximize``: learned reward (np.argmax, controllers.py:152)."""
+    import torch
+    import torch.distributed as dist
+    rank, ws = world(group)
+    nb = d_result.numel()
+    if ws == 1:
+        raw = d_result.cpu().numpy()
+    else:
+        src = d_result if dist.get_backend(group) == "nccl" else d_result.cpu()   # gloo: host tensors
+        out = torch.empty(ws * nb, dtype=torch.uint8, device=src.device)
+        dist.all_gather_into_tensor(out, src, group=group)
+        raw = out.cpu().numpy()
+    raw = raw.reshape(max(ws, 1), nb)
+    sign = -1.0 if maximize else 1.0
+    recs = np.zeros((raw.shape[0], 3 + action_dim), dtype=np.float64)
+    for r in range(raw.shape[0]):
+        recs[r, 0] = 1.0
+        recs[r, 1] = sign * float(raw[r, 8:16].view(np.float64)[0])
+        recs[r, 2] = float(raw[r, 0:8].view(np.int64)[0])
+        recs[r, 3:] = raw[r, 16:16 + 8 * action_dim].view(np.float64)
+    best = select(recs)
+    return float(sign * best[1]), int(best[2]), best[3:].copy()

@@ -255,12 +255,9 @@ def main():
             return cem_step(i)
         eng.rollout_async(d_state.data_ptr(), 0, d_actions.data_ptr() if d_actions is not None else None,
                           0xB0B + i, offset, d_costs.data_ptr(), None, d_res.data_ptr(), stream.cuda_stream)
-        raw = d_res.cpu().numpy()                       # D2H of the result; syncs the stream
-        best_i = int(raw[:8].view(np.int64)[0])
-        best_c = float(raw[8:16].view(np.float64)[0])
-        first = raw[16:16 + 8 * A_DIM].view(np.float64).copy()
-        sign = -1.0 if reward else 1.0                  # argmax of the reward == argmin of its negation
-        return bdist.allgather_minloc(True, sign * best_c, best_i, first, A_DIM)
+        # the min-loc exchange straight from the device result (stream-ordered after the argmin
+        # launch), then one D2H of the gathered records (argmax for the learned reward)
+        return bdist.allgather_result(d_res, A_DIM, maximize=reward)
 
     for i in range(args.warmup):
         step(i)

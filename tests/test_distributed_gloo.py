@@ -118,3 +118,38 @@ def test_two_rank_controller_matches_single_process(rng_mode):
         want.append(a.tolist())
     assert out[0][0] == want
     assert out[0][1] == float(np.random.random())   # both ranks consumed the stream like one process
+
+
+def _result_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from bc_mpc_amd import distributed as bd
+    # bcmpc_result layout: int64 index, f64 cost, f64 first_action[16]
+    costs = {0: 3.5, 1: 1.25, 2: 1.25}                  # tie between ranks 1 and 2: the lower index wins
+    raw = np.zeros(144, dtype=np.uint8)
+    raw[0:8] = np.frombuffer(np.int64(100 * rank + 7).tobytes(), np.uint8)
+    raw[8:16] = np.frombuffer(np.float64(costs[rank]).tobytes(), np.uint8)
+    raw[16:64] = np.frombuffer(np.full(6, float(rank)).tobytes(), np.uint8)
+    got = bd.allgather_result(torch.from_numpy(raw), 6)
+    got_max = bd.allgather_result(torch.from_numpy(raw), 6, maximize=True)
+    q.put((rank, got[0], got[1], got[2].tolist(), got_max[0], got_max[1]))
+    dist.destroy_process_group()
+
+
+def test_allgather_result_minloc_gloo():
+    """The device-record exchange (bench / multi-rank path): min-loc with the lowest-index tie-break,
+    argmax for the learned reward, identical on every rank."""
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_result_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, c, i, fa, cmax, imax in res:
+        assert (c, i, fa) == (1.25, 107, [1.0] * 6)
+        assert (cmax, imax) == (3.5, 7)
