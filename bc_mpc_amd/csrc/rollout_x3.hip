@@ -40,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/bcmpc.h"
 #include "device_common.h"
 #include "kernels.h"
@@ -82,10 +84,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
         }                                                               \
     } while (0)
 
-#define X3_BARRIER()                                \
-    do {                                            \
-        if constexpr (!X3_DIAG_NOBAR) __syncthreads(); \
+// X3_DIAG_NOBAR: 1 = every barrier off; or a bitmask 2 << id of single barriers to drop
+// (id 0 Bx, 1 B1, 2 slab-free, 3 slab-ready, 4 B3, 5 B4)
+#define X3_BARRIER_ID(id)                                                           \
+    do {                                                                            \
+        if constexpr (X3_DIAG_NOBAR != 1 && !((X3_DIAG_NOBAR >> ((id) + 1)) & 1)) __syncthreads(); \
     } while (0)
+#define X3_BARRIER() X3_BARRIER_ID(-1)
 
 // 2 log2(e): hidden-layer biases and result scales carry this factor, so the
 // epilogue's pre-activation is z = 2 log2(e) y with no extra multiply
@@ -410,7 +415,7 @@ void rollout_x3(const RolloutArgs a) {
     double prog_prev = 0.0;                             // SO: the half-1 owner's progress term, one step late
     // action j of candidate c at step h: the caller's [H,K,A] array (np.random.uniform,
     // controllers.py:53), Philox, or the CEM sampler
-    auto act_value = [&](int h, int64_t c, int j) -> double {
+    auto act_value = [&](int h, int64_t c, int j) __attribute__((always_inline)) -> double {
         const uint64_t g = (uint64_t)(a.cand_offset + c);
         if (a.cem_mu)
             return cem_action(a.seed, g, h, j, a.cem_iter, a.cem_mu[h * A + j], a.cem_sigma[h * A + j],
@@ -420,7 +425,7 @@ void rollout_x3(const RolloutArgs a) {
     };
     // stage X3_NCH steps' action inputs from step h0: f64 normalise (dynamics.py:110),
     // cast to f32 (TF feed); threads [0, nt) of the block
-    auto fill_actions = [&](int h0, int nt) {
+    auto fill_actions = [&](int h0, int nt) __attribute__((always_inline)) {
         const int nhs = (a.H - h0 < X3_NCH) ? a.H - h0 : X3_NCH;
         const int per = CB * A;
         for (int i = threadIdx.x; i < nhs * per; i += nt) {
@@ -444,10 +449,16 @@ void rollout_x3(const RolloutArgs a) {
     //   uh/ul   : unit 0 of the next hidden layer, issued before each epilogue
     //   oh/ol   : the output layer's first OP k-step pairs (slot 2*(pp % OP) + v = k-step
     //             w*PW+pp, tile v), issued before the last epilogue; the rest stream in
-    constexpr int OP = PW < 2 ? PW : 2;
+#ifndef X3_OP
+#define X3_OP 1             // output-layer k-step pairs prefetched before the last epilogue (2: the second pair in flight too -- measured equal, and it demotes the slots to scratch)
+#endif
+    constexpr int OP = PW < X3_OP ? PW : X3_OP;
     h8 a0h[TW], a0l[TW], uh[G], ul[G], oh[2 * OP], ol[2 * OP];
     aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);
-    auto load_out = [&](int pp, int slot) {
+    // (the slot is a compile-time constant at every call: a runtime index into oh/ol would
+    // demote the arrays to scratch memory)
+    auto load_out = [&](int pp, auto SLOTc) __attribute__((always_inline)) {
+        constexpr int slot = decltype(SLOTc)::value;
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
             const int o = (((w * PW + pp) * 2 + v) * 2) * 1024;
@@ -455,12 +466,12 @@ void rollout_x3(const RolloutArgs a) {
             ol[2 * slot + v] = fload(rso, voff, o + 1024);
         }
     };
-    auto load_next = [&](int l_next) {
+    auto load_next = [&](int l_next) __attribute__((always_inline)) {
         if (l_next < L) {
             aload_x3<G>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, w * P * TW * 2048, uh, ul);
         } else {
-#pragma unroll
-            for (int pp = 0; pp < OP; ++pp) load_out(pp, pp);
+            load_out(0, std::integral_constant<int, 0>{});
+            if constexpr (OP > 1) load_out(1, std::integral_constant<int, OP - 1>{});
         }
     };
 
@@ -491,7 +502,7 @@ void rollout_x3(const RolloutArgs a) {
             }
         }
         if constexpr (SO) {
-            X3_BARRIER();                                 // both halves' column maxima published
+            X3_BARRIER_ID(0);                             // both halves' column maxima published
             if (owner && !X3_DIAG_NOOWNER) mx = fmaxf(mx, colmax[(1 - hv0) * NC * 16 + cw * 16 + m]);
         }
         if (owner && !X3_DIAG_NOOWNER) {
@@ -526,7 +537,7 @@ void rollout_x3(const RolloutArgs a) {
             }
         }
         X3_ST(1);
-        X3_BARRIER();                                  // layer-0 input published
+        X3_BARRIER_ID(1);                              // layer-0 input published
         X3_ST(2);
 
         // ---- layer 0 [S+A -> h] ----
@@ -565,7 +576,7 @@ void rollout_x3(const RolloutArgs a) {
         // ---- hidden layers 1..L-1 [h -> h] through the slab ----
         for (int l = 1; l < L; ++l) {
             // (l == 1: the slab's last readers were the owners' partial sums, before the barrier above)
-            if (l > 1) X3_BARRIER();                   // every wave is done reading the slab
+            if (l > 1) X3_BARRIER_ID(2);               // every wave is done reading the slab
 #pragma unroll
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
@@ -573,7 +584,7 @@ void rollout_x3(const RolloutArgs a) {
                     swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
                     swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
-            X3_BARRIER();                              // layer input complete
+            X3_BARRIER_ID(3);                          // layer input complete
             X3_ST(4);
 #pragma unroll
             for (int j = 0; j < TW; ++j)
@@ -609,7 +620,10 @@ void rollout_x3(const RolloutArgs a) {
                     po[v][c] = mfma16(oh[2 * slot + v], xl[pp][c], po[v][c]);
                     po[v][c] = mfma16(ol[2 * slot + v], xh[pp][c], po[v][c]);
                 }
-            if (pp + OP < PW) load_out(pp + OP, slot);
+            if (pp + OP < PW) {
+                if (slot == 0) load_out(pp + OP, std::integral_constant<int, 0>{});
+                else load_out(pp + OP, std::integral_constant<int, OP - 1>{});
+            }
         }
         __builtin_amdgcn_sched_barrier(0);              // (not hoisted above the MFMAs' operand waits)
         aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);                     // next step's layer 0
@@ -617,12 +631,12 @@ void rollout_x3(const RolloutArgs a) {
         // they stage the next chunk's action inputs while the others finish
         if (owner && (h + 1) % X3_NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * (SO ? 2 * NC : NC));
         X3_ST(7);
-        X3_BARRIER();                                  // every wave is done reading the slab
+        X3_BARRIER_ID(4);                              // every wave is done reading the slab
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
             for (int c = 0; c < NC; ++c) slab[((w * 2 + v) * NC + c) * 64 + lane] = po[v][c];
-        X3_BARRIER();                                  // partials complete
+        X3_BARRIER_ID(5);                              // partials complete
         X3_ST(8);
         if (!owner || X3_DIAG_NOOWNER) continue;
 

@@ -2,7 +2,7 @@
 # Build A/B variants of libbcmpc.so into build/variants/ (selected at run time via BCMPC_LIB).
 # usage: tools/build_variants.sh [-x] "name:-DFLAG=1 ..." ...
 #   default: flags apply to rollout.hip + rollout_grp.hip (f32 kernels)
-#   -x     : flags apply to rollout_x3.hip only, built for hidden 512 / NC 4 (-DX3_ONLY=512)
+#   -x     : flags apply to rollout_x3.hip only, built for one width / NC ($X3W, default 512; $X3NC, default 4)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/variants
@@ -20,7 +20,7 @@ for spec in "$@"; do
     src=bc_mpc_amd/csrc/_x3_$name.hip
   fi
   if [ $X3 = 1 ]; then
-    ( $H $flags -DX3_ONLY=512 -c $src -o build/variants/rollout_x3_$name.o &&
+    ( $H -DX3_ONLY=${X3W:-512} -DX3_ONLY_NC=${X3NC:-4} $flags -c $src -o build/variants/rollout_x3_$name.o &&
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
           build/rollout.o build/rollout_grp.o build/cem.o build/fit.o build/variants/rollout_x3_$name.o build/variants/capi.o ) &
   else
