@@ -116,6 +116,7 @@ struct bcmpc_engine {
     bool split = false;                // BCMPC_PREC_SPLIT_F16 (rollout_x3)
     int nc = 0;                        // split kernel: 16-candidate columns per workgroup
     float winv[BCMPC_MAX_LAYERS + 1]{};  // split kernel: 1 / operand scales per layer
+    float pwinv[BCMPC_MAX_LAYERS + 1]{}; // ... and per fused-policy layer
     bool reward = false;               // BCMPC_MODEL_REWARD (NNDynamicsRewardModel)
     hipStream_t stream = nullptr;
     // device buffers
@@ -190,9 +191,9 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     const bool split = c.precision == BCMPC_PREC_SPLIT_F16;
     if (split) {
         // f16 operands need bounded hidden activations (tanh) and the plain delta net
-        if (c.activation != BCMPC_ACT_TANH || c.layer_norm || reward || c.policy_hidden > 0)
+        if (c.activation != BCMPC_ACT_TANH || c.layer_norm || reward)
             return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports the tanh NNDynamicsModel without "
-                                               "LayerNorm or fused policy in this build (use FP32)");
+                                               "LayerNorm in this build (use FP32)");
         if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLIT4))
             return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4 kernels");
     } else if (c.kernel >= BCMPC_KERNEL_SPLIT1) {
@@ -226,10 +227,12 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (c.policy_hidden > 128 || c.policy_layers < 1 || c.policy_layers > BCMPC_MAX_LAYERS)
             { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy: hidden must be in [1,128], layers in [1,8]"); }
         if (c.state_dim < 16) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines need state_dim >= 16"); }
-        if (e->HP < 128 || e->HP > 512) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines support dynamics hidden 65..512"); }
+        if (e->HP < 128 || e->HP > (split ? 1024 : 512))
+            { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines support dynamics hidden 65..512 (split: ..1024)"); }
         if (c.policy_mode != BCMPC_POLICY_EXPLORE && c.policy_mode != BCMPC_POLICY_STOCHASTIC)
             { delete e; return fail(BCMPC_ERR_ARG, "unknown policy_mode"); }
-        if (c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4 && c.kernel != BCMPC_KERNEL_GROUP8)
+        if (!split && c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4 &&
+            c.kernel != BCMPC_KERNEL_GROUP8)
             { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "policy engines run on the group4 / group8 kernels"); }
         if (c.kernel == BCMPC_KERNEL_AUTO) kern = BCMPC_KERNEL_GROUP4;
         e->PHP = 128;
@@ -243,14 +246,19 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                : c.kernel == BCMPC_KERNEL_SPLIT4 ? 4 : 0;
         const int nwx = x3_waves(e->HP);
         auto fits = [&](int n) {
-            return n <= nwx && n <= x3_max_nc(e->HP) && x3_lds(e->HP, c.n_layers, n, c.action_dim) <= 160 * 1024;
+            return n <= nwx && n <= x3_max_nc(e->HP) && (e->PL == 0 || x3_policy_ok(e->HP, n)) &&
+                   x3_lds(e->HP, c.n_layers, n, c.action_dim, e->PL, e->PHP) <= 160 * 1024;
         };
         if (nc == 0) {
             nc = 1;
             for (int n : {4, 2})
                 if (fits(n) && cols >= (int64_t)n * 256) { nc = n; break; }
         }
-        if (!fits(nc)) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "split kernel does not fit this shape"); }
+        if (!fits(nc)) {
+            delete e;
+            return fail(BCMPC_ERR_UNSUPPORTED, e->PL ? "split kernel with a fused policy needs dynamics hidden 449..1024"
+                                                     : "split kernel does not fit this shape");
+        }
         e->split = true;
         e->nc = nc;
         e->kernel = nc == 1 ? BCMPC_KERNEL_SPLIT1 : nc == 2 ? BCMPC_KERNEL_SPLIT2 : BCMPC_KERNEL_SPLIT4;
@@ -467,15 +475,35 @@ int bcmpc_set_policy(bcmpc_engine* e, const bcmpc_policy* p, uint64_t version) {
         if (!p->kernels[l] || !p->biases[l]) return fail(BCMPC_ERR_ARG, "null policy kernel/bias pointer");
     HIP_TRY(hipSetDevice(c.device));
     std::vector<float> hw(e->pw_floats, 0.f);
-    const int tb = TP / e->nw;
-    pack_layer(p->kernels[0], S, ph, 2, TP, tb, hw.data() + e->pw_off[0]);
-    for (int l = 1; l < PL; ++l) pack_layer(p->kernels[l], ph, ph, TP, TP, tb, hw.data() + e->pw_off[l]);
     int rowmap[16];
     for (int n = 0; n < 16; ++n) {
         const int j = n - (S - 16);                     // action j sits at output-tile row S-16+j
         rowmap[n] = (j >= 0 && j < A) ? j : -1;
     }
-    pack_out_rows(p->kernels[PL], ph, A, TP, rowmap, hw.data() + e->pw_off[PL]);
+    if (e->split) {
+        // one tile per wave (TWp = 1); same byte sizes as the f32 layout.  Input scales:
+        // obz (|z| <= 5) x 2^11, hidden tanh x 2^12
+        _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
+        const int PP = PHP / 32;
+        for (int l = 0; l < PL; ++l) {
+            const int in = l == 0 ? S : ph;
+            const float sw = x3_scale(p->kernels[l], (size_t)in * ph);
+            pack_x3_layer(p->kernels[l], in, ph, l == 0 ? 1 : PP, TP, 1, sw, hh + 2 * e->pw_off[l]);
+            e->pwinv[l] = (1.0f / sw) * (l == 0 ? 1.0f / 2048.0f : 1.0f / 4096.0f);
+        }
+        std::vector<float> wo((size_t)ph * 16, 0.f);    // output kernel with its columns at rows S-16+j
+        for (int k = 0; k < ph; ++k)
+            for (int n = 0; n < 16; ++n)
+                if (rowmap[n] >= 0) wo[(size_t)k * 16 + n] = p->kernels[PL][(size_t)k * A + rowmap[n]];
+        const float sw = x3_scale(p->kernels[PL], (size_t)ph * A);
+        pack_x3_layer(wo.data(), ph, 16, PP, 1, 1, sw, hh + 2 * e->pw_off[PL]);
+        e->pwinv[PL] = (1.0f / sw) * (1.0f / 4096.0f);
+    } else {
+        const int tb = TP / e->nw;
+        pack_layer(p->kernels[0], S, ph, 2, TP, tb, hw.data() + e->pw_off[0]);
+        for (int l = 1; l < PL; ++l) pack_layer(p->kernels[l], ph, ph, TP, TP, tb, hw.data() + e->pw_off[l]);
+        pack_out_rows(p->kernels[PL], ph, A, TP, rowmap, hw.data() + e->pw_off[PL]);
+    }
     std::vector<float> hb((size_t)PL * PHP + kPolParams, 0.f);
     for (int l = 0; l < PL; ++l) std::memcpy(hb.data() + (size_t)l * PHP, p->biases[l], sizeof(float) * ph);
     float* pm = hb.data() + (size_t)PL * PHP;           // [obmean 32][obstd 32][logstd 16][outbias 16]
@@ -591,6 +619,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.act_out_steps = 1;
     }
     for (int l = 0; l <= c.n_layers; ++l) a.winv[l] = e->winv[l];
+    for (int l = 0; l <= e->PL; ++l) a.pwinv[l] = e->pwinv[l];
     if (cem) {
         if (e->kernel == BCMPC_KERNEL_SOLO || e->PL > 0)
             return fail(BCMPC_ERR_UNSUPPORTED, "CEM runs on group-kernel engines without a policy");

@@ -107,6 +107,16 @@ __device__ __forceinline__ f4 bias_act(const f4 acc, const float* __restrict__ b
 }
 
 // ---------------------------------------------------------- dense layers ---
+// Standard normal from two Philox uniforms (Box-Muller, f32): the stochastic
+// policy branch (DiagGaussianPd.sample = mean + std * N(0,1), ppo_bc_policy.py:85)
+__device__ __forceinline__ float rng_normal(uint64_t seed, uint64_t g, int h, int j) {
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)h, 0x80000000u | (uint32_t)j};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float u1 = ((float)(c[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
+    return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
 // Raw buffer load of one 16-B weight fragment: voffset = lane*16 (VGPR),
 // soffset = fragment position (SGPR).  Reads past the layer's num_records
 // return 0 (hardware range check), so the prefetch may run off the end.

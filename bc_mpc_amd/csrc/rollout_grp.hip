@@ -337,16 +337,6 @@ __device__ __forceinline__ void prefetch_layer0(f4 (&ring)[T / NW], const f4* w0
     for (int j = 0; j < TW; ++j) ring[j] = wload(rs0, lane * 16, (w * 2 + 0) * TW * 1024 + j * 1024);
 }
 
-// Standard normal from two Philox uniforms (Box-Muller, f32): the stochastic
-// policy branch (DiagGaussianPd.sample = mean + std * N(0,1), ppo_bc_policy.py:85)
-__device__ __forceinline__ float rng_normal(uint64_t seed, uint64_t g, int h, int j) {
-    uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)h, 0x80000000u | (uint32_t)j};
-    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const float u1 = ((float)(c[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
-    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
-    return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
-}
-
 // Dynamics-net shape facts shared by the kernel and its launcher.
 //   RW = false: NNDynamicsModel, L hidden layers of HP, output [HP -> S]
 //   RW = true : NNDynamicsRewardModel, trunk HP + heads 2*HP, output [2HP -> S+1]

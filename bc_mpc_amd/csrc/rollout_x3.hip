@@ -340,15 +340,16 @@ __host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
     return NW >= 16 ? 4 : (NW >= 8 || HP <= 512) ? 2 : 1;
 }
 
-// LDS carve-up: consts | biases (L*HP + 32) | column factors NC*16 | column max [2][NC*16] |
-// penalty counts [2][NC*16] | action inputs
-// X3_NCH*16NC*A (16-B aligned) | layer-0 slab NC*2 KiB | slab (P+1)*NC*2 KiB
+// LDS carve-up: consts | biases (L*HP + 32) | policy biases + params (PL*PHP + kPolParams) |
+// column factors NC*16 | column max [2][NC*16] | penalty counts [2][NC*16] | action inputs
+// X3_NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab (P+1)*NC*2 KiB
 __host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
-__host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A) {
-    return param_bytes(L, HP) + NC * 16 * 4 * 5 + x3_xa_bytes(NC, A) + NC * 2048 + (HP / 32 + 1) * NC * 2048;
+__host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, int PL = 0, int PHP = 0) {
+    return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
+           NC * 2048 + (HP / 32 + 1) * NC * 2048;
 }
 
-template <int HP, int NC, int NW>
+template <int HP, int NC, int NW, int PHP>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(x3_waves_per_eu(HP, NC, NW), 8)))
 void rollout_x3(const RolloutArgs a) {
     constexpr int T = HP / 16;          // hidden tiles
@@ -360,6 +361,10 @@ void rollout_x3(const RolloutArgs a) {
     static_assert(TW % 2 == 0 && TW * NW == T, "each wave must own whole tile pairs");
     static_assert(NC <= NW, "one owner wave per column");
     static_assert(P >= NW, "the output-layer partials reuse the slab");
+    // fused policy (MPCcontrollerPolicyNet): one policy tile per wave, split ownership
+    constexpr int PPn = PHP / 32;                       // policy hidden k-steps
+    static_assert(PHP == 0 || (PHP / 16 == NW && 2 * NC <= NW && PPn + NW / 2 <= P + 1),
+                  "policy: one hidden tile per wave, two state waves per column, partials in the slab");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
@@ -386,11 +391,19 @@ void rollout_x3(const RolloutArgs a) {
         for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kTanhK;
     float* const Bout = Bl + L * HP;
     for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[L][i];
-    float* colf = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP));
+    float* const Pb = Bout + 32;                        // policy: [PL][PHP] hidden biases (x 2 log2 e), params
+    const int PL = a.pL;
+    if constexpr (PHP > 0) {
+        for (int l = 0; l < PL; ++l)
+            for (int i = threadIdx.x; i < PHP; i += blockDim.x) Pb[l * PHP + i] = a.pb[l][i] * kTanhK;
+        for (int i = threadIdx.x; i < kPolParams; i += blockDim.x) Pb[PL * PHP + i] = a.pparams[i];
+    }
+    float* colf = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP) +
+                                           pol_param_bytes(PHP > 0 ? PL : 0, PHP));
     float* colmax = colf + NC * 16;                     // [half][NC*16]: per-half column max (split owners)
     int* penbuf = reinterpret_cast<int*>(colmax + 2 * NC * 16);   // [step & 1][NC*16] penalty counts
     float* xa = reinterpret_cast<float*>(penbuf + 2 * NC * 16);   // [X3_NCH][CB][A] normalised action inputs
-    f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + x3_xa_bytes(NC, A));
+    f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)));
     f4* slab = slab0 + NC * 2 * 64;
     __syncthreads();
 
@@ -437,7 +450,7 @@ void rollout_x3(const RolloutArgs a) {
             xa[(hh * CB + kl) * A + j] = xv;
         }
     };
-    fill_actions(0, 64 * NW);
+    if constexpr (PHP == 0) fill_actions(0, 64 * NW);
     __syncthreads();
     const int voff = lane * 16;
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
@@ -454,7 +467,7 @@ void rollout_x3(const RolloutArgs a) {
 #endif
     constexpr int OP = PW < X3_OP ? PW : X3_OP;
     h8 a0h[TW], a0l[TW], uh[G], ul[G], oh[2 * OP], ol[2 * OP];
-    aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);
+    if constexpr (PHP == 0) aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);
     // (the slot is a compile-time constant at every call: a runtime index into oh/ol would
     // demote the arrays to scratch memory)
     auto load_out = [&](int pp, auto SLOTc) __attribute__((always_inline)) {
@@ -475,9 +488,163 @@ void rollout_x3(const RolloutArgs a) {
         }
     };
 
+    // ---- fused policy (MlpPolicy.act, ppo_bc_policy.py:54-88; mixing controllers.py:196-206) ----
+    // Same split-f16 arithmetic: obz = clip((f32(ob) - mean) / std, -5, 5) carried x 2^11, tanh
+    // hidden layers x 2^12.  Wave w owns policy tile w of every hidden layer (its 16 neurons are
+    // half w&1 of k-step w/2 of the next layer's input); the output layer (one 16-row tile,
+    // action j at row S-16+j) is K-split over the waves, partials summed in fixed order by the
+    // half-1 owners, whose lanes hold exactly the action dims.
+    auto policy_step = [&](int h, double (&pact)[4]) __attribute__((always_inline)) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        const float* pm = Pb + PL * PHP;                // [obmean 32][obstd 32][logstd 16][out bias 16]
+        const bool actor = owner && hv0 == 1;
+        const __amdgpu_buffer_rsrc_t pr0 = layer_rsrc(a.pw[0], a.pwbytes[0]);
+        h8 ah = fload(pr0, voff, (w * 2 + 0) * 1024), al = fload(pr0, voff, (w * 2 + 1) * 1024);
+        double uu[4] = {0.0, 0.0, 0.0, 0.0};            // explore draws (controllers.py:191), issued early
+        if (actor && a.pol_mode != BCMPC_POLICY_STOCHASTIC) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = 16 + 4 * q + r - S;
+                if (valid && j >= 0 && j < A && a.actions)   // the caller's array (no CEM with a policy)
+                    uu[r] = a.actions[((int64_t)h * a.K + cand) * A + j];
+            }
+        }
+        if (owner) {
+            float z[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * hv0 + 4 * q + r;
+                float v = 0.f;
+                if (d < S) {
+                    v = ((float)s[0][r] - pm[d]) / pm[32 + d];
+                    v = fminf(fmaxf(v, -5.0f), 5.0f);
+                }
+                z[r] = v * 2048.0f;
+            }
+            h2 h01, l01, h23, l23;
+            split2(z[0], z[1], h01, l01);
+            split2(z[2], z[3], h23, l23);
+            reinterpret_cast<h4*>(slab0 + (cw * 2 + 0) * 64 + lane)[hv0] = (h4){h01[0], h01[1], h23[0], h23[1]};
+            reinterpret_cast<h4*>(slab0 + (cw * 2 + 1) * 64 + lane)[hv0] = (h4){l01[0], l01[1], l23[0], l23[1]};
+        }
+        X3_BARRIER();                                   // policy input published
+        f4 pacc[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const h8 bh = sread(slab0 + (c * 2 + 0) * 64 + lane), bl = sread(slab0 + (c * 2 + 1) * 64 + lane);
+            pacc[c] = mfma16(ah, bh, (f4){0.f, 0.f, 0.f, 0.f});
+            pacc[c] = mfma16(ah, bl, pacc[c]);
+            pacc[c] = mfma16(al, bh, pacc[c]);
+        }
+        h4 xh[NC], xl[NC];                              // this wave's tile of the current layer
+        auto epi = [&](float f, const float* bias) __attribute__((always_inline)) {
+            const f4 b = *reinterpret_cast<const f4*>(bias + 16 * w + 4 * q);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = tanh_x4096(fmaf(pacc[c][r], f, b[r]));
+                h2 h01, l01, h23, l23;
+                split2(v[0], v[1], h01, l01);
+                split2(v[2], v[3], h23, l23);
+                xh[c] = (h4){h01[0], h01[1], h23[0], h23[1]};
+                xl[c] = (h4){l01[0], l01[1], l23[0], l23[1]};
+            }
+        };
+        h8 nh[PPn > 0 ? PPn : 1], nl[PPn > 0 ? PPn : 1];
+        auto load_layer = [&](int l) __attribute__((always_inline)) {
+            const __amdgpu_buffer_rsrc_t rs = layer_rsrc(a.pw[l], a.pwbytes[l]);
+            if (l < PL) {
+#pragma unroll
+                for (int p = 0; p < PPn; ++p) {
+                    nh[p] = fload(rs, voff, ((w * PPn + p) * 2 + 0) * 1024);
+                    nl[p] = fload(rs, voff, ((w * PPn + p) * 2 + 1) * 1024);
+                }
+            } else {                                    // output layer: k-step w/2 of its single tile
+                nh[0] = fload(rs, voff, ((w >> 1) * 2 + 0) * 1024);
+                nl[0] = fload(rs, voff, ((w >> 1) * 2 + 1) * 1024);
+            }
+        };
+        load_layer(1);
+        epi(a.pwinv[0] * kTanhK, Pb);
+        for (int l = 1; l < PL; ++l) {
+            if (l > 1) X3_BARRIER();                    // every wave is done reading the slab
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                reinterpret_cast<h4*>(slab + sidx<NC>(w >> 1, c, 0, lane))[w & 1] = xh[c];
+                reinterpret_cast<h4*>(slab + sidx<NC>(w >> 1, c, 1, lane))[w & 1] = xl[c];
+            }
+            X3_BARRIER();                               // layer input complete
+#pragma unroll
+            for (int c = 0; c < NC; ++c) pacc[c] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int p = 0; p < PPn; ++p)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const h8 bh = sread(slab + sidx<NC>(p, c, 0, lane)), bl = sread(slab + sidx<NC>(p, c, 1, lane));
+                    pacc[c] = mfma16(nh[p], bh, pacc[c]);
+                    pacc[c] = mfma16(nh[p], bl, pacc[c]);
+                    pacc[c] = mfma16(nl[p], bh, pacc[c]);
+                }
+            load_layer(l + 1);
+            epi(a.pwinv[l] * kTanhK, Pb + l * PHP);
+        }
+        // output layer, K-split: this wave's 16 neurons are one half of a k-step B fragment
+        f4* part = slab + sidx<NC>(PPn, 0, 0, 0);      // [NW][NC] partial tiles, past the hidden input
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            h8 bh = (h8)(_Float16)0.0f, bl = (h8)(_Float16)0.0f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                bh[(w & 1) * 4 + i] = xh[c][i];
+                bl[(w & 1) * 4 + i] = xl[c][i];
+            }
+            f4 po = mfma16(nh[0], bh, (f4){0.f, 0.f, 0.f, 0.f});
+            po = mfma16(nh[0], bl, po);
+            po = mfma16(nl[0], bh, po);
+            part[(w * NC + c) * 64 + lane] = po;
+        }
+        X3_BARRIER();                                   // partials complete
+        if (!actor) return;
+        f4 o = part[(0 * NC + cw) * 64 + lane];
+#pragma unroll
+        for (int g = 1; g < NW; ++g) o += part[(g * NC + cw) * 64 + lane];   // fixed summation order
+        const float fo_p = a.pwinv[PL];
+        const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
+        if (!a.actions && a.pol_mode != BCMPC_POLICY_STOCHASTIC) {   // Philox draws, computed in place
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = 16 + 4 * q + r - S;
+                if (valid && j >= 0 && j < A) uu[r] = rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int j = 16 + 4 * q + r - S;
+            if (j < 0 || j >= A) continue;
+            const float mean = o[r] * fo_p + pm[80 + 4 * q + r];       // dense bias (f32)
+            if (a.pol_mode == BCMPC_POLICY_STOCHASTIC) {
+                const float sd = expf(pm[64 + j]);
+                pact[r] = (double)(mean + sd * rng_normal(a.seed ^ 0x9E3779B97F4A7C15ull, gcand, h, j));
+            } else {
+                // (1 - explore) * mean in f32 (NumPy keeps the f32 dtype), + explore * U in f64
+                const float t1 = (float)(1.0 - a.explore) * mean;
+                pact[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, uu[r]));
+            }
+            if (a.act_out && h < a.act_out_steps && valid)          // action_paths (controllers.py:213)
+                a.act_out[((int64_t)h * a.K + cand) * A + j] = pact[r];
+        }
+    };
+
     uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.H; ++h) {
+        double pact[4] = {0.0, 0.0, 0.0, 0.0};            // policy actions of dims 16 + 4q + r (half-1 owners)
+        if constexpr (PHP > 0) {
+            policy_step(h, pact);
+            // (with a policy the layer-0 fragments are fetched after it: registers)
+            aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);
+        }
         X3_ST(0);
         float xin[4 * NHV];                               // layer-0 input slots 4*(hv0+k) + r
         float mx = 0.f;
@@ -490,8 +657,16 @@ void rollout_x3(const RolloutArgs a) {
                 for (int r = 0; r < 4; ++r) {
                     const int d = 16 * (hv0 + k) + 4 * q + r;
                     float xv = 0.f;
-                    if (d < S) xv = (float)div_rn(__dsub_rn(s[k][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
-                    else if (d < S + A) xv = xr[d - S];
+                    if (d < S) {
+                        xv = (float)div_rn(__dsub_rn(s[k][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
+                    } else if (d < S + A) {
+                        if constexpr (PHP > 0) {              // the policy's action (dynamics.py:110)
+                            const int j = d - S;
+                            xv = (float)div_rn(__dsub_rn(pact[r], C[2 * 32 + j]), C[3 * 32 + j], C[9 * 32 + j]);
+                        } else {
+                            xv = xr[d - S];
+                        }
+                    }
                     xin[4 * k + r] = xv;
                 }
 #pragma unroll
@@ -626,10 +801,11 @@ void rollout_x3(const RolloutArgs a) {
             }
         }
         __builtin_amdgcn_sched_barrier(0);              // (not hoisted above the MFMAs' operand waits)
-        aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);                     // next step's layer 0
+        if constexpr (PHP == 0) aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);   // next step's layer 0
         // the owners reach this point first (the older waves win the MFMA arbitration):
         // they stage the next chunk's action inputs while the others finish
-        if (owner && (h + 1) % X3_NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * (SO ? 2 * NC : NC));
+        if constexpr (PHP == 0)
+            if (owner && (h + 1) % X3_NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * (SO ? 2 * NC : NC));
         X3_ST(7);
         X3_BARRIER_ID(4);                              // every wave is done reading the slab
 #pragma unroll
@@ -713,22 +889,24 @@ void rollout_x3(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
-template <int HP, int NC, int NW>
+template <int HP, int NC, int NW, int PHP = 0>
 static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
     if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1) > 160 * 1024) {
         (void)a; (void)st;
         return hipErrorInvalidValue;
     } else {
+        if (PHP > 0 && (a.pL < 1 || a.phidden_padded != PHP)) return hipErrorInvalidValue;
         static bool attr_set = false;
         if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW>,
+            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW, PHP>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
             attr_set = true;
         }
-        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, a.L, a.A);
+        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, a.L, a.A, PHP > 0 ? a.pL : 0, PHP);
+        if (lds > 160 * 1024) return hipErrorInvalidValue;
         const int64_t blocks = (a.K + 16 * NC - 1) / (16 * NC);
-        hipLaunchKernelGGL((rollout_x3<HP, NC, NW>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
+        hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
         return hipGetLastError();
     }
 }
@@ -754,17 +932,43 @@ int x3_max_nc(int hidden_padded) {
 #endif
 }
 
-size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim) {
-    return (size_t)x3_lds_bytes_rt(hidden_padded, nc, n_layers, action_dim);
+// fused policy: one 128-wide policy tile per wave of an 8-wave group
+bool x3_policy_ok(int hidden_padded, int nc) {
+#ifdef X3_ONLY
+    (void)hidden_padded; (void)nc;
+    return false;
+#else
+    return x3_waves(hidden_padded) == 8 && 2 * nc <= 8 && hidden_padded >= 512;
+#endif
+}
+
+size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int policy_layers, int policy_hidden_padded) {
+    return (size_t)x3_lds_bytes_rt(hidden_padded, nc, n_layers, action_dim, policy_layers, policy_hidden_padded);
 }
 
 template <int NC>
 static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
 #ifdef X3_ONLY          // variant builds (tools/build_variants.sh): one width, NC = 4 only
     if constexpr (NC == X3_ONLY_NC)
-        return hidden_padded == X3_ONLY ? launch_x3_t<X3_ONLY, X3_ONLY_NC, X3_NW512>(a, st) : hipErrorInvalidValue;
+        return hidden_padded == X3_ONLY && a.pL == 0 ? launch_x3_t<X3_ONLY, X3_ONLY_NC, X3_NW512>(a, st)
+                                                     : hipErrorInvalidValue;
     return hipErrorInvalidValue;
 #else
+    if (a.pL > 0) {
+        if (a.phidden_padded != 128) return hipErrorInvalidValue;
+        switch (hidden_padded) {
+            case 512:
+                if constexpr (X3_NW512 == 8) return launch_x3_t<512, NC, 8, 128>(a, st);
+                return hipErrorInvalidValue;
+            case 768:
+                if constexpr (NC <= 2) return launch_x3_t<768, NC, 8, 128>(a, st);
+                return hipErrorInvalidValue;
+            case 1024:
+                if constexpr (NC <= 2) return launch_x3_t<1024, NC, 8, 128>(a, st);
+                return hipErrorInvalidValue;
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (hidden_padded) {
         case 64: return launch_x3_t<64, NC, 2>(a, st);
         case 128: return launch_x3_t<128, NC, 4>(a, st);

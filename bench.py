@@ -125,7 +125,8 @@ def main():
                     help="hbm: [H,K,A] f64 actions resident in HBM (parity mode input); device: in-kernel Philox")
     ap.add_argument("--precision", default=os.environ.get("BCMPC_PRECISION", "auto"), choices=["auto", "fp32", "split"],
                     help="fp32: f32 MFMA (rollout_grp); split: f32-accurate hi/lo f16 MFMA (rollout_x3, tanh "
-                         "NNDynamicsModel without LayerNorm/policy); auto: split where it applies, else fp32")
+                         "NNDynamicsModel without LayerNorm; with a fused policy: hidden 449..1024); auto: split "
+                         "where it applies, else fp32")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -155,7 +156,8 @@ def main():
     wl = WORKLOADS[args.workload]
     K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
     if args.precision == "auto":
-        args.precision = "split" if (act == "tanh" and not wl.get("reward") and not wl.get("policy")) else "fp32"
+        args.precision = "split" if (act == "tanh" and not wl.get("reward")
+                                     and (not wl.get("policy") or 448 < hidden <= 1024)) else "fp32"
     offset = rank * K
 
     # synthetic inputs: glorot kernels, 0.1 N biases, synthetic stats/state
@@ -198,7 +200,8 @@ def main():
         pol_arrays = (pks, pbs, mean_obs.astype(np.float32), (std_obs + 0.05).astype(np.float32),
                       np.full(A_DIM, -0.5, np.float32))
         eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, policy_hidden=ph,
-                            policy_layers=pl, policy_mode=wl.get("policy_mode", "explore"), cost=cost, model=model)
+                            policy_layers=pl, policy_mode=wl.get("policy_mode", "explore"), cost=cost, model=model,
+                            precision=args.precision)
         eng.set_policy(PolicySpec(*pol_arrays), wl["explore"], 1)
     else:
         eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, cost=cost, model=model,

@@ -294,20 +294,31 @@ def _policy_env(g):
     return Env()
 
 
+def _split_policy_ok(hidden, act, ln):
+    return act == "tanh" and not ln and 448 < hidden <= 1024
+
+
+@pytest.mark.parametrize("kernel", ["fp32", "split1", "split2", "split4"])
 @pytest.mark.parametrize("name", golden_names("policy"))
-def test_policy_engine_matches_reference_fixture(name):
-    """MPCcontrollerPolicyNet (self_exp=False) fused into the group kernel vs the reference run."""
+def test_policy_engine_matches_reference_fixture(name, kernel):
+    """MPCcontrollerPolicyNet (self_exp=False) fused into the group kernel (fp32) or the split
+    kernel (policy MLP in split-f16 too) vs the reference run; same tolerances."""
     from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
     g = Golden(name)
     w, p = g.weights, g.policy
+    if kernel != "fp32" and not _split_policy_ok(w.hidden, w.activation, w.layer_norm):
+        pytest.skip("split kernel with a policy: tanh dynamics without LayerNorm, hidden 449..1024")
+    kw = dict(precision="fp32") if kernel == "fp32" else dict(kernel=kernel)
     eng = RolloutEngine(g.S, g.A, w.hidden, w.n_layers, w.activation, w.layer_norm, g.H, g.K,
-                        policy_hidden=p.hidden, policy_layers=p.n_layers, policy_mode="explore")
+                        policy_hidden=p.hidden, policy_layers=p.n_layers, policy_mode="explore", **kw)
+    if kernel != "fp32":
+        assert eng.info()["kernel"] == kernel
     eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), g.norm, 1)
     eng.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), g.meta["explore"], 1)
     rs = np.random.RandomState(g.meta["seed"])
     expl = rs.uniform(g.low, g.high, size=[g.H, g.K, g.A])
     res = eng.get_action(g.state, expl, return_costs=True)
-    assert_costs_close(res.costs, g.costs, g.near, f"{name}")
+    assert_costs_close(res.costs, g.costs, g.near, f"{name}/{kernel}")
     fa = eng.first_actions()
     err = np.abs(fa - g.z["first_actions"])
     print(f"[{name}] max|dfirst_action|={err.max():.3e}")
@@ -364,3 +375,88 @@ def test_policy_stochastic_mode_is_deterministic_and_shard_invariant():
     mean = orc.NumpyPolicy(p).mean(np.tile(state, [K, 1])).astype(np.float64)
     z = (a1 - mean) / np.exp(p.logstd.astype(np.float64))
     assert abs(z.mean()) < 0.1 and abs(z.std() - 1.0) < 0.1
+
+
+@pytest.mark.parametrize("mode", ["explore", "stochastic"])
+@pytest.mark.parametrize("hidden,PL,ph", [(500, 2, 128), (1000, 2, 64), (512, 1, 100)])
+def test_split_policy_matches_fp32_engine(hidden, PL, ph, mode):
+    """The split kernel's fused policy against the fp32 group/solo kernel at scale: same f64
+    explore draws / Philox normals, costs and step-0 actions within the f32 tolerance
+    (the two engines differ only in the f32 summation order / split rounding)."""
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    K, H = 3000, 8
+    w = orc.synthetic_weights(20, 6, hidden, 2, "tanh", False, seed_base=77)
+    p = orc.synthetic_policy(20, 6, ph, PL, seed=5)
+    norm = orc.synthetic_normalization()
+    state = orc.synthetic_state(norm)
+    expl = np.random.RandomState(3).uniform(-1, 1, (H, K, 6))
+    out = {}
+    if hidden > 512:                     # the fp32 kernels fuse a policy up to hidden 512: the oracle
+        if mode == "stochastic":
+            pytest.skip("device Philox normals: no host restatement beyond the fp32 engine")
+        dyn, pol = orc.NumpyDynamics(w, norm), orc.NumpyPolicy(p)
+        a0, i0, c0 = orc.policy_get_action(dyn, pol, state, H, K, -np.ones(6), np.ones(6), 0.3,
+                                           rng=np.random.RandomState(3))
+        e = RolloutEngine(20, 6, hidden, 2, "tanh", False, H, K, policy_hidden=ph, policy_layers=PL,
+                          policy_mode=mode, precision="split")
+        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh"), norm, 1)
+        e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.3, 1)
+        r = e.get_action(state, expl, return_costs=True)
+        first = (1 - 0.3) * pol.act(np.tile(state, [K, 1]), stochastic=False)[0] + 0.3 * expl[0]
+        err = np.abs(e.first_actions() - first)
+        print(f"[split policy {hidden}/{PL}x{ph} vs oracle] max|dfirst|={err.max():.3e}")
+        assert (err <= 2e-6).all()
+        d = np.abs(r.costs - c0)
+        tol = 10 * (ATOL + RTOL * np.abs(c0))
+        flip = np.abs(d - 10.0 * np.round(d / 10.0)) <= tol
+        print(f"   max|dcost|={d.max():.3e} over_tol={(d > tol).sum()} flips={(flip & (d > tol)).sum()}")
+        assert ((d <= tol) | flip).all() and (flip & (d > tol)).sum() <= K // 500
+        e.close()
+        return
+    for prec in ("fp32", "split"):
+        e = RolloutEngine(20, 6, hidden, 2, "tanh", False, H, K, policy_hidden=ph, policy_layers=PL,
+                          policy_mode=mode, precision=prec)
+        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh"), norm, 1)
+        e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.3, 1)
+        if prec == "split":
+            assert e.info()["kernel"].startswith("split")
+        r = e.get_action(state, expl, seed=9, return_costs=True)
+        out[prec] = (r, e.first_actions())
+        e.close()
+    (r32, a32), (rsp, asp) = out["fp32"], out["split"]
+    err = np.abs(asp - a32)
+    print(f"[split policy {hidden}/{PL}x{ph} {mode}] max|dfirst|={err.max():.3e}")
+    assert (err <= 2e-6).all()
+    d = np.abs(rsp.costs - r32.costs)
+    tol = 10 * (ATOL + RTOL * np.abs(r32.costs))
+    flip = np.abs(d - 10.0 * np.round(d / 10.0)) <= tol          # a +-10 penalty threshold crossed
+    print(f"   max|dcost|={d.max():.3e} over_tol={(d > tol).sum()} flips={(flip & (d > tol)).sum()}")
+    assert ((d <= tol) | flip).all() and (flip & (d > tol)).sum() <= K // 500
+    assert rsp.best_index == int(np.argmin(rsp.costs))
+
+
+def test_split_policy_shard_invariant():
+    """Candidate sharding (cand_offset) leaves the split kernel's stochastic policy bit-identical."""
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    K, H = 2048, 5
+    w = orc.synthetic_weights(20, 6, 500, 2, "tanh", False)
+    p = orc.synthetic_policy(20, 6, 128, 2)
+    norm = orc.synthetic_normalization()
+    state = orc.synthetic_state(norm)
+
+    def mk(k):
+        e = RolloutEngine(20, 6, 500, 2, "tanh", False, H, k, policy_hidden=128, policy_layers=2,
+                          policy_mode="stochastic", kernel="split2")
+        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh"), norm, 1)
+        e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.5, 1)
+        return e
+    full = mk(K)
+    r1 = full.get_action(state, None, seed=42, return_costs=True)
+    r2 = full.get_action(state, None, seed=42, return_costs=True)
+    assert np.array_equal(r1.costs, r2.costs)
+    half = mk(K // 2)
+    ra = half.get_action(state, None, seed=42, cand_offset=0, return_costs=True)
+    rb = half.get_action(state, None, seed=42, cand_offset=K // 2, return_costs=True)
+    assert np.array_equal(np.concatenate([ra.costs, rb.costs]), r1.costs)
