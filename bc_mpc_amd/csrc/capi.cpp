@@ -115,6 +115,7 @@ struct bcmpc_engine {
     int pack_tb = 4;                   // output tiles per packed block of layers 0..L-1
     bool split = false;                // BCMPC_PREC_SPLIT_F16 (rollout_x3)
     int nc = 0;                        // split kernel: 16-candidate columns per workgroup
+    int nwl = 0;                       // packed weight layers (RolloutArgs.w entries)
     float winv[BCMPC_MAX_LAYERS + 1]{};  // split kernel: 1 / operand scales per layer
     float pwinv[BCMPC_MAX_LAYERS + 1]{}; // ... and per fused-policy layer
     bool reward = false;               // BCMPC_MODEL_REWARD (NNDynamicsRewardModel)
@@ -191,9 +192,11 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     const bool split = c.precision == BCMPC_PREC_SPLIT_F16;
     if (split) {
         // f16 operands need bounded hidden activations (tanh) and the plain delta net
-        if (c.activation != BCMPC_ACT_TANH || c.layer_norm || reward)
-            return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports the tanh NNDynamicsModel without "
-                                               "LayerNorm in this build (use FP32)");
+        if (c.activation != BCMPC_ACT_TANH || c.layer_norm)
+            return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports tanh nets without LayerNorm "
+                                               "in this build (use FP32)");
+        if (reward && c.state_dim < 16)
+            return fail(BCMPC_ERR_UNSUPPORTED, "split reward engines need state_dim >= 16 (reward row in tile 1)");
         if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLIT4))
             return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4 kernels");
     } else if (c.kernel >= BCMPC_KERNEL_SPLIT1) {
@@ -218,7 +221,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     if (reward) {
         // two-head net: 4-wave groups (16 head tiles per wave, spill-free at 2 waves/SIMD; the
         // 8-wave layout needs ~135 registers and spills at 4 waves/SIMD -- measured 2.5% slower)
-        if (c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4 && c.kernel != BCMPC_KERNEL_GROUP8)
+        if (!split && c.kernel != BCMPC_KERNEL_AUTO && c.kernel != BCMPC_KERNEL_GROUP4 &&
+            c.kernel != BCMPC_KERNEL_GROUP8)
             { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "reward engines run on the group4 / group8 kernels"); }
         if (c.kernel == BCMPC_KERNEL_AUTO) kern = BCMPC_KERNEL_GROUP4;
     }
@@ -247,7 +251,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         const int nwx = x3_waves(e->HP);
         auto fits = [&](int n) {
             return n <= nwx && n <= x3_max_nc(e->HP) && (e->PL == 0 || x3_policy_ok(e->HP, n)) &&
-                   x3_lds(e->HP, c.n_layers, n, c.action_dim, e->PL, e->PHP) <= 160 * 1024;
+                   x3_lds(e->HP, reward ? 3 : c.n_layers, n, c.action_dim, e->PL, e->PHP) <= 160 * 1024;
         };
         if (nc == 0) {
             nc = 1;
@@ -282,7 +286,21 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->T / nw;   // split: output tiles per wave
     const int L = c.n_layers, T = e->T;
     size_t off = 0, boff = 0;
-    if (reward) {
+    e->nwl = reward ? 3 : L + 1;
+    if (reward && split) {
+        // split layout: trunk, delta head hidden (dense_1), delta out (dense_2), reward head
+        // hidden (dense_3), reward out (dense_4, one 16-row tile); 512 floats = one 2-KiB fragment pair
+        const int P = T / 2;
+        e->w_off[0] = off; off += (size_t)T * 512;
+        e->w_off[1] = off; off += (size_t)T * P * 512;
+        e->w_off[2] = off; off += (size_t)2 * P * 512;
+        e->w_off[3] = off; off += (size_t)T * P * 512;
+        e->w_off[4] = off; off += (size_t)P * 512;
+        e->nwl = 5;
+        // biases: trunk | delta head | reward head | out (rows 0..S-1 dense_2, row S dense_4)
+        e->b_off[0] = 0; e->b_off[1] = e->HP; e->b_off[2] = 2 * e->HP; e->b_off[3] = 3 * e->HP;
+        boff = 3 * e->HP + 32;
+    } else if (reward) {
         // [S+A -> h] trunk, [h -> 2h] both heads' hidden layers, [2h -> S+1] block-diagonal output
         e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;
         e->w_off[1] = off; off += (size_t)2 * T * T * 64 * 4;
@@ -386,7 +404,32 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
     const int tb = e->pack_tb;
     std::vector<float> hb(rw ? 3 * (size_t)HP + 32 : (size_t)L * HP + 32, 0.f);
     std::vector<float> hln(2 * (size_t)NLN * HP, 0.f);
-    if (e->split) {
+    if (e->split && rw) {
+        _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
+        const int P = T / 2;
+        const float s0 = x3_scale(w->kernels[0], (size_t)(S + A) * h);
+        pack_x3_layer(w->kernels[0], S + A, h, 1, T, tb, s0, hh + 2 * e->w_off[0]);
+        e->winv[0] = 1.0f / s0;
+        const float sd = x3_scale(w->kernels[1], (size_t)h * h), sr = x3_scale(w->kernels[3], (size_t)h * h);
+        pack_x3_layer(w->kernels[1], h, h, P, T, tb, sd, hh + 2 * e->w_off[1]);
+        pack_x3_layer(w->kernels[3], h, h, P, T, tb, sr, hh + 2 * e->w_off[3]);
+        e->winv[1] = (1.0f / sd) / 4096.0f;
+        e->winv[3] = (1.0f / sr) / 4096.0f;
+        // both output kernels feed one accumulator: one scale (the smaller of the two)
+        const float so = std::min(x3_scale(w->kernels[2], (size_t)h * S), x3_scale(w->kernels[4], (size_t)h));
+        pack_x3_layer(w->kernels[2], h, S, P, 2, 2, so, hh + 2 * e->w_off[2]);
+        std::vector<float> wr((size_t)h * 16, 0.f);      // dense_4 at row S of the second output tile
+        for (int k = 0; k < h; ++k) wr[(size_t)k * 16 + (S - 16)] = w->kernels[4][k];
+        pack_x3_layer(wr.data(), h, 16, P, 1, 1, so, hh + 2 * e->w_off[4]);
+        e->winv[2] = e->winv[4] = (1.0f / so) / 4096.0f;
+        std::memcpy(hb.data() + e->b_off[0], w->biases[0], sizeof(float) * h);
+        std::memcpy(hb.data() + e->b_off[1], w->biases[1], sizeof(float) * h);
+        std::memcpy(hb.data() + e->b_off[2], w->biases[3], sizeof(float) * h);
+        std::memcpy(hb.data() + e->b_off[3], w->biases[2], sizeof(float) * S);
+        hb[e->b_off[3] + S] = w->biases[4][0];
+        e->mean_reward = w->mean_reward[0];
+        e->std_reward = w->std_reward[0];
+    } else if (e->split) {
         // same sizes as the f32 layout (4 bytes per weight: two halves)
         _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
         const int P = T / 2;
@@ -576,12 +619,12 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     if (c.cost != BCMPC_COST_NONE && !d_costs) return fail(BCMPC_ERR_ARG, "the fused objective needs a costs buffer");
     if (d_result && c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "argmin needs the fused cost");
     RolloutArgs a{};
-    for (int l = 0; l <= c.n_layers; ++l) {
-        const size_t end = l < c.n_layers ? e->w_off[l + 1] : e->w_floats;
+    for (int l = 0; l < e->nwl; ++l) {
+        const size_t end = l + 1 < e->nwl ? e->w_off[l + 1] : e->w_floats;
         a.wbytes[l] = (int32_t)((end - e->w_off[l]) * sizeof(float));
         a.w[l] = reinterpret_cast<const float __attribute__((ext_vector_type(4)))*>(e->d_w + e->w_off[l]);
-        a.b[l] = e->d_b + e->b_off[l];
     }
+    for (int l = 0; l < (e->split && e->reward ? 4 : e->nwl); ++l) a.b[l] = e->d_b + e->b_off[l];
     if (e->reward) {   // trunk LN, then the two heads' LN params side by side (2*HP)
         a.lng[0] = e->d_ln;               a.lng[1] = e->d_ln + e->HP;
         a.lnb[0] = e->d_ln + 3 * e->HP;   a.lnb[1] = e->d_ln + 4 * e->HP;
@@ -618,7 +661,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.act_out = e->d_first;
         a.act_out_steps = 1;
     }
-    for (int l = 0; l <= c.n_layers; ++l) a.winv[l] = e->winv[l];
+    for (int l = 0; l < e->nwl; ++l) a.winv[l] = e->winv[l];
     for (int l = 0; l <= e->PL; ++l) a.pwinv[l] = e->pwinv[l];
     if (cem) {
         if (e->kernel == BCMPC_KERNEL_SOLO || e->PL > 0)

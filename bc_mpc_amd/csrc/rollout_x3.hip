@@ -349,7 +349,7 @@ __host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, 
            NC * 2048 + (HP / 32 + 1) * NC * 2048;
 }
 
-template <int HP, int NC, int NW, int PHP>
+template <int HP, int NC, int NW, int PHP, bool RW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(x3_waves_per_eu(HP, NC, NW), 8)))
 void rollout_x3(const RolloutArgs a) {
     constexpr int T = HP / 16;          // hidden tiles
@@ -383,14 +383,18 @@ void rollout_x3(const RolloutArgs a) {
     const int64_t cand = cand0 + 16 * cw + m;
     const bool valid = owner && cand < a.K;
     const int S = a.S, A = a.A, L = a.L;
+    // RW (NNDynamicsRewardModel, dynamics.py:150-177): weights [trunk, delta head, delta out,
+    // reward head, reward out], biases [trunk, delta head, reward head | out]
+    const int LB = RW ? 3 : L;                          // hidden bias rows
+    const int LO = RW ? 2 : L;                          // the (delta) output layer
 
     double* C = reinterpret_cast<double*>(lds);
     float* Bl = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kConstRows * kConstCols * 8);
     for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
-    for (int l = 0; l < L; ++l)
+    for (int l = 0; l < LB; ++l)
         for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kTanhK;
-    float* const Bout = Bl + L * HP;
-    for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[L][i];
+    float* const Bout = Bl + LB * HP;
+    for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[LB][i];
     float* const Pb = Bout + 32;                        // policy: [PL][PHP] hidden biases (x 2 log2 e), params
     const int PL = a.pL;
     if constexpr (PHP > 0) {
@@ -398,7 +402,7 @@ void rollout_x3(const RolloutArgs a) {
             for (int i = threadIdx.x; i < PHP; i += blockDim.x) Pb[l * PHP + i] = a.pb[l][i] * kTanhK;
         for (int i = threadIdx.x; i < kPolParams; i += blockDim.x) Pb[PL * PHP + i] = a.pparams[i];
     }
-    float* colf = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + param_bytes(L, HP) +
+    float* colf = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + param_bytes(LB, HP) +
                                            pol_param_bytes(PHP > 0 ? PL : 0, PHP));
     float* colmax = colf + NC * 16;                     // [half][NC*16]: per-half column max (split owners)
     int* penbuf = reinterpret_cast<int*>(colmax + 2 * NC * 16);   // [step & 1][NC*16] penalty counts
@@ -454,8 +458,8 @@ void rollout_x3(const RolloutArgs a) {
     __syncthreads();
     const int voff = lane * 16;
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
-    const __amdgpu_buffer_rsrc_t rso = layer_rsrc(a.w[L], a.wbytes[L]);
-    const float fo = a.winv[L];
+    const __amdgpu_buffer_rsrc_t rso = layer_rsrc(a.w[LO], a.wbytes[LO]);
+    const float fo = a.winv[LO];
 
     // Operand sets in flight ahead of their MFMAs (issued before the preceding VALU phase):
     //   a0h/a0l : layer-0 fragments of the NEXT step (issued after the output MFMAs)
@@ -738,7 +742,10 @@ void rollout_x3(const RolloutArgs a) {
                 for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0l[j], bh[c], acc[j][c]);
             }
         }
-        load_next(1);
+        if constexpr (RW)                                  // the reward head runs first
+            aload_x3<G>(layer_rsrc(a.w[3], a.wbytes[3]), voff, w * P * TW * 2048, uh, ul);
+        else
+            load_next(1);
         h8 xh[PW][NC], xl[PW][NC];                        // this wave's activations of the current layer
 #pragma unroll
         for (int pp = 0; pp < PW; ++pp)
@@ -748,8 +755,67 @@ void rollout_x3(const RolloutArgs a) {
                          xh[pp][c], xl[pp][c]);
         X3_ST(3);
 
+        f4 po1[NC];                                       // RW: the reward row's output partial (tile 1)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) po1[c] = (f4){0.f, 0.f, 0.f, 0.f};
+        if constexpr (RW) {
+            // ---- both heads read the trunk's output from one slab (no barrier between them) ----
+#pragma unroll
+            for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
+                    swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
+                }
+            X3_BARRIER_ID(3);                          // trunk output complete
+            // reward head [h -> h] (dense_3), then its output row (dense_4) from registers
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
+            mm_x3<TW, NC, P, G>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab, acc, lane, uh, ul);
+            aload_x3<G>(layer_rsrc(a.w[1], a.wbytes[1]), voff, w * P * TW * 2048, uh, ul);   // delta head unit 0
+            h8 rh[PW], rl[PW];
+            {
+                const __amdgpu_buffer_rsrc_t rsr = layer_rsrc(a.w[4], a.wbytes[4]);
+#pragma unroll
+                for (int pp = 0; pp < PW; ++pp) {
+                    rh[pp] = fload(rsr, voff, ((w * PW + pp) * 2 + 0) * 1024);
+                    rl[pp] = fload(rsr, voff, ((w * PW + pp) * 2 + 1) * 1024);
+                }
+            }
+            const float fr = a.winv[3] * kTanhK;
+#pragma unroll
+            for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], fr, Bl + 2 * HP, w * TW + 2 * pp, q, xh[pp][c],
+                             xl[pp][c]);
+#pragma unroll
+            for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    po1[c] = mfma16(rh[pp], xh[pp][c], po1[c]);
+                    po1[c] = mfma16(rh[pp], xl[pp][c], po1[c]);
+                    po1[c] = mfma16(rl[pp], xh[pp][c], po1[c]);
+                }
+            // delta head [h -> h] (dense_1)
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
+            mm_x3<TW, NC, P, G>(layer_rsrc(a.w[1], a.wbytes[1]), w * P * TW * 2048, slab, acc, lane, uh, ul);
+            load_next(L);                                  // delta out (L == 2)
+            const float fd = a.winv[1] * kTanhK;
+#pragma unroll
+            for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], fd, Bl + HP, w * TW + 2 * pp, q, xh[pp][c],
+                             xl[pp][c]);
+        }
         // ---- hidden layers 1..L-1 [h -> h] through the slab ----
-        for (int l = 1; l < L; ++l) {
+        for (int l = 1; l < (RW ? 1 : L); ++l) {
             // (l == 1: the slab's last readers were the owners' partial sums, before the barrier above)
             if (l > 1) X3_BARRIER_ID(2);               // every wave is done reading the slab
 #pragma unroll
@@ -783,7 +849,7 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
-            for (int c = 0; c < NC; ++c) po[v][c] = (f4){0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < NC; ++c) po[v][c] = v == 1 ? po1[c] : (f4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int pp = 0; pp < PW; ++pp) {
             const int slot = pp % OP;
@@ -844,6 +910,22 @@ void rollout_x3(const RolloutArgs a) {
                 }
             }
         }
+        if constexpr (RW) {
+            // ---- learned reward (dynamics.py:236) * gamma**h, running sum (controllers.py:139,150):
+            //      output row S (tile 1: S >= 16) in lane row q = (S & 15) >> 2, register S & 3 ----
+            const int kS = 1 - hv0;                       // the half-1 slot of this owner's state
+            if (kS < NHV && q == ((S & 15) >> 2)) {
+                float o_s = 0.f;
+#pragma unroll
+                for (int k = 0; k < NHV; ++k)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (k == kS && r == (S & 3)) o_s = o[k][r];
+                const float nr = fmaf(o_s, fo, Bout[S]);                   // BiasAdd (f32)
+                const double rw = __dadd_rn(__dmul_rn((double)nr, a.std_reward), a.mean_reward);
+                cost = __dadd_rn(cost, __dmul_rn(rw, a.gpow[h]));
+            }
+        }
         if (a.cost == BCMPC_COST_CHEETAH) {
             // score = pen - (s'17 - s17) / 0.01 (cost_functions.py:28), summed in step order (:59-63)
             if constexpr (SO) {
@@ -881,7 +963,8 @@ void rollout_x3(const RolloutArgs a) {
             cost = __dadd_rn(cost, __dsub_rn(pen, prog_prev));
         }
     }
-    if (a.costs && valid && q == 0 && (SO ? hv0 == 1 : true)) a.costs[cand] = cost;   // the cost holder
+    // the cost holder: half 1, lane row 0 (cheetah) / the reward row's lanes (RW)
+    if (a.costs && valid && q == (RW ? (S & 15) >> 2 : 0) && (SO ? hv0 == 1 : true)) a.costs[cand] = cost;
     if constexpr (X3_STAMP) {
         if (a.stamps && lane == 0)
             for (int k = 0; k < 10; ++k) a.stamps[((size_t)blockIdx.x * NW + w) * 10 + k] = ph_[k];
@@ -889,7 +972,7 @@ void rollout_x3(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
-template <int HP, int NC, int NW, int PHP = 0>
+template <int HP, int NC, int NW, int PHP = 0, bool RW = false>
 static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
     if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1) > 160 * 1024) {
         (void)a; (void)st;
@@ -898,15 +981,16 @@ static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
         if (PHP > 0 && (a.pL < 1 || a.phidden_padded != PHP)) return hipErrorInvalidValue;
         static bool attr_set = false;
         if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW, PHP>,
+            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW, PHP, RW>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
             attr_set = true;
         }
-        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, a.L, a.A, PHP > 0 ? a.pL : 0, PHP);
+        if (RW != (a.model == BCMPC_MODEL_REWARD) || (RW && (a.L != 2 || a.S < 16))) return hipErrorInvalidValue;
+        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, RW ? 3 : a.L, a.A, PHP > 0 ? a.pL : 0, PHP);
         if (lds > 160 * 1024) return hipErrorInvalidValue;
         const int64_t blocks = (a.K + 16 * NC - 1) / (16 * NC);
-        hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
+        hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP, RW>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
         return hipGetLastError();
     }
 }
@@ -954,6 +1038,20 @@ static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStrea
                                                      : hipErrorInvalidValue;
     return hipErrorInvalidValue;
 #else
+    if (a.model == BCMPC_MODEL_REWARD) {      // NNDynamicsRewardModel (hidden <= 512)
+        if (a.pL > 0) {
+            if constexpr (X3_NW512 == 8)
+                if (hidden_padded == 512 && a.phidden_padded == 128) return launch_x3_t<512, NC, 8, 128, true>(a, st);
+            return hipErrorInvalidValue;
+        }
+        switch (hidden_padded) {
+            case 64: return launch_x3_t<64, NC, 2, 0, true>(a, st);
+            case 128: return launch_x3_t<128, NC, 4, 0, true>(a, st);
+            case 256: return launch_x3_t<256, NC, 4, 0, true>(a, st);
+            case 512: return launch_x3_t<512, NC, X3_NW512, 0, true>(a, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (a.pL > 0) {
         if (a.phidden_padded != 128) return hipErrorInvalidValue;
         switch (hidden_padded) {

@@ -156,8 +156,8 @@ def main():
     wl = WORKLOADS[args.workload]
     K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
     if args.precision == "auto":
-        args.precision = "split" if (act == "tanh" and not wl.get("reward")
-                                     and (not wl.get("policy") or 448 < hidden <= 1024)) else "fp32"
+        top = 512 if wl.get("reward") else 1024
+        args.precision = "split" if (act == "tanh" and (not wl.get("policy") or 448 < hidden <= top)) else "fp32"
     offset = rank * K
 
     # synthetic inputs: glorot kernels, 0.1 N biases, synthetic stats/state

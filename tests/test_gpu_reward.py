@@ -73,11 +73,20 @@ class _Env:
         self.observation_space = obs
 
 
-@pytest.mark.parametrize("kernel", ["group4", "group8"])
+def _skip_split(g, kernel):
+    if kernel.startswith("split"):
+        if g.weights.layer_norm:
+            pytest.skip("split precision: nets without LayerNorm")
+        if kernel == "split4" and g.weights.hidden <= 64:
+            pytest.skip("split4 needs >= 4 waves (hidden > 64)")
+
+
+@pytest.mark.parametrize("kernel", ["group4", "group8", "split1", "split2", "split4"])
 @pytest.mark.parametrize("name", REWARD)
 def test_reward_engine_matches_reference_fixture(name, kernel):
     from bc_mpc_amd.engine import RolloutEngine
     g = RewardGolden(name)
+    _skip_split(g, kernel)
     eng = RolloutEngine(g.S, g.A, g.weights.hidden, 2, "tanh", g.weights.layer_norm, g.H, g.K, device=0,
                         cost="reward", model="reward", kernel=kernel)
     assert eng.info()["kernel"] == kernel
@@ -236,3 +245,35 @@ def test_reward_errors():
     with pytest.raises(Exception):
         delta.set_discount(0.9)
     del orc
+
+
+@pytest.mark.parametrize("mode", ["explore", "stochastic"])
+def test_split_policy_reward_matches_fp32_engine(mode):
+    """MPCcontrollerPolicyNetReward at hidden 500 (the run.sh recipe's net): the split kernel
+    (reward heads + fused policy in split-f16) against the fp32 group kernel on the same draws."""
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    S, A, K, H, h = 20, 6, 3000, 8, 500
+    norm = orc.synthetic_normalization(S, A, seed=5, reward=True)
+    w = orc.synthetic_reward_weights(S, A, h, False, seed_base=123)
+    p = orc.synthetic_policy(S, A, 128, 2, seed=9)
+    state = orc.synthetic_state(norm, seed=6)
+    expl = np.random.RandomState(4).uniform(-1, 1, (H, K, A))
+    out = {}
+    for prec in ("fp32", "split"):
+        e = RolloutEngine(S, A, h, 2, "tanh", False, H, K, cost="reward", model="reward", precision=prec,
+                          policy_hidden=128, policy_layers=2, policy_mode=mode)
+        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh", model="reward"), norm, 1)
+        e.set_discount(0.99)
+        e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.5, 1)
+        if prec == "split":
+            assert e.info()["kernel"].startswith("split")
+        r = e.get_action(state, expl, seed=13, return_costs=True)
+        out[prec] = (r, e.first_actions())
+        e.close()
+    (r32, a32), (rsp, asp) = out["fp32"], out["split"]
+    err = np.abs(asp - a32)
+    print(f"[split polrew {mode}] max|dfirst|={err.max():.3e}")
+    assert (err <= 2e-6).all()
+    assert_rewards_close(rsp.costs, r32.costs, f"split polrew {mode}")
+    assert rsp.best_index == int(np.argmax(rsp.costs))
