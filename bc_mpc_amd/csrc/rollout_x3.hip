@@ -236,23 +236,50 @@ __device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, in
 // flight while unit u's MFMAs run; set 0 arrives holding unit 0, loaded by the
 // caller before its epilogue and clobbered here); the layer input from the slab,
 // each k-step's B fragments read once at its first unit.
-template <int TW, int NC, int P, int G>
+//
+// OWN: the k-steps run in the order k0 = w*PW, w*PW+1, ... (mod P), and the first PW
+// -- the ones this wave produced and already wrote to the slab itself -- need no
+// other wave: bar() (the "layer input complete" barrier) runs after their MFMAs are
+// issued, overlapping them with the slower waves' epilogues.  (A wave reads its own
+// LDS writes in program order: no barrier.)
+template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, typename Bar = void (*)()>
 __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
-                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G]) {
+                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr) {
     constexpr int NG = TW / G;
     static_assert(NG * G == TW && (NG == 1 || NG == 2), "one or two units per k-step");
     static_assert((P * NG) % 2 == 0, "ping-pong over unit pairs");
     constexpr int NU = P * NG;
+    // units fed from registers (whole ping-pong pairs only; otherwise the rotated order from the slab)
+    constexpr int NOWN = (OWN && (PW * NG) % 2 == 0) ? PW * NG : 0;
+    static_assert(NU - NOWN >= 2, "a slab pair remains");
     constexpr int STEPB = TW * 2048;
     const int voff = lane * 16;
-    auto uoff = [&](int u) { return wbase + (u / NG) * STEPB + (u % NG) * G * 2048; };
+    auto kstep = [&](int u) {                           // k-step of unit u
+        const int p = u / NG + k0;
+        return p >= P ? p - P : p;
+    };
+    auto uoff = [&](int u) { return wbase + kstep(u) * STEPB + (u % NG) * G * 2048; };
     // unit u (even) is (k-step u/NG, group 0); unit u+1 is group 1 of the same
     // k-step (NG = 2) or the next k-step (NG = 1)
     constexpr int G1 = NG == 2 ? 1 : 0;
     h8 s1h[G], s1l[G], bh[NC], bl[NC];
+    if constexpr (OWN) {
+#pragma unroll
+        for (int u = 0; u < NOWN; u += 2) {
+            aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
+            __builtin_amdgcn_sched_barrier(0);
+            bread_x3<NC>(slab, kstep(u), lane, bh, bl);
+            unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
+            aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (NG == 1) bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
+            unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
+        }
+        bar();
+    }
     // (the last pair is peeled so that every load in the loop is unconditional: a
     // conditional load would make the compiler drain vmcnt to 0 at the merge)
-    if constexpr (NG == 1 && X3_BSTREAM) {
+    if constexpr (NG == 1 && X3_BSTREAM && !OWN) {
         for (int u = 0; u < NU - 2; u += 2) {
             aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
             __builtin_amdgcn_sched_barrier(0);      // keep the loads ahead of the MFMAs they overlap
@@ -268,21 +295,21 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
         (void)bh; (void)bl;
         return;
     }
-    for (int u = 0; u < NU - 2; u += 2) {
+    for (int u = NOWN; u < NU - 2; u += 2) {
         aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
         __builtin_amdgcn_sched_barrier(0);          // keep the loads ahead of the MFMAs they overlap
-        bread_x3<NC>(slab, u / NG, lane, bh, bl);
+        bread_x3<NC>(slab, kstep(u), lane, bh, bl);
         unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
         aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NG == 1) bread_x3<NC>(slab, u + 1, lane, bh, bl);
+        if constexpr (NG == 1) bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
         unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
     }
     aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
     __builtin_amdgcn_sched_barrier(0);
-    bread_x3<NC>(slab, (NU - 2) / NG, lane, bh, bl);
+    bread_x3<NC>(slab, kstep(NU - 2), lane, bh, bl);
     unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-    if constexpr (NG == 1) bread_x3<NC>(slab, NU - 1, lane, bh, bl);
+    if constexpr (NG == 1) bread_x3<NC>(slab, kstep(NU - 1), lane, bh, bl);
     unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
 }
 
@@ -330,6 +357,9 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
 // tiles per streamed operand unit: a whole k-step up to 4 tiles per wave, else half
 __host__ __device__ constexpr int x3_group(int TW) { return TW <= 4 ? TW : TW / 2; }
 
+#ifndef X3_OWN                   // hidden layers start with the k-steps the wave produced itself
+#define X3_OWN 1
+#endif
 #ifndef X3_NCH
 #define X3_NCH 4                 // steps of layer-0 action inputs staged in LDS per fill
 #endif
@@ -342,11 +372,11 @@ __host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
 
 // LDS carve-up: consts | biases (L*HP + 32) | policy biases + params (PL*PHP + kPolParams) |
 // column factors NC*16 | column max [2][NC*16] | penalty counts [2][NC*16] | action inputs
-// X3_NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab (P+1)*NC*2 KiB
+// X3_NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab P*NC*2 KiB
 __host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
 __host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, int PL = 0, int PHP = 0) {
     return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
-           NC * 2048 + (HP / 32 + 1) * NC * 2048;
+           NC * 2048 + (HP / 32) * NC * 2048;
 }
 
 template <int HP, int NC, int NW, int PHP, bool RW>
@@ -363,7 +393,7 @@ void rollout_x3(const RolloutArgs a) {
     static_assert(P >= NW, "the output-layer partials reuse the slab");
     // fused policy (MPCcontrollerPolicyNet): one policy tile per wave, split ownership
     constexpr int PPn = PHP / 32;                       // policy hidden k-steps
-    static_assert(PHP == 0 || (PHP / 16 == NW && 2 * NC <= NW && PPn + NW / 2 <= P + 1),
+    static_assert(PHP == 0 || (PHP / 16 == NW && 2 * NC <= NW && PPn + NW / 2 <= P),
                   "policy: one hidden tile per wave, two state waves per column, partials in the slab");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
@@ -457,6 +487,7 @@ void rollout_x3(const RolloutArgs a) {
     if constexpr (PHP == 0) fill_actions(0, 64 * NW);
     __syncthreads();
     const int voff = lane * 16;
+    const int kown = X3_OWN ? w * PW : 0;               // first k-step of this wave's hidden-layer sweep
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
     const __amdgpu_buffer_rsrc_t rso = layer_rsrc(a.w[LO], a.wbytes[LO]);
     const float fo = a.winv[LO];
@@ -485,7 +516,7 @@ void rollout_x3(const RolloutArgs a) {
     };
     auto load_next = [&](int l_next) __attribute__((always_inline)) {
         if (l_next < L) {
-            aload_x3<G>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, w * P * TW * 2048, uh, ul);
+            aload_x3<G>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, w * P * TW * 2048 + kown * TW * 2048, uh, ul);
         } else {
             load_out(0, std::integral_constant<int, 0>{});
             if constexpr (OP > 1) load_out(1, std::integral_constant<int, OP - 1>{});
@@ -743,7 +774,7 @@ void rollout_x3(const RolloutArgs a) {
             }
         }
         if constexpr (RW)                                  // the reward head runs first
-            aload_x3<G>(layer_rsrc(a.w[3], a.wbytes[3]), voff, w * P * TW * 2048, uh, ul);
+            aload_x3<G>(layer_rsrc(a.w[3], a.wbytes[3]), voff, w * P * TW * 2048 + kown * TW * 2048, uh, ul);
         else
             load_next(1);
         h8 xh[PW][NC], xl[PW][NC];                        // this wave's activations of the current layer
@@ -767,13 +798,17 @@ void rollout_x3(const RolloutArgs a) {
                     swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
                     swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
-            X3_BARRIER_ID(3);                          // trunk output complete
             // reward head [h -> h] (dense_3), then its output row (dense_4) from registers
 #pragma unroll
             for (int j = 0; j < TW; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
-            mm_x3<TW, NC, P, G>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab, acc, lane, uh, ul);
+            {
+                auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // trunk output complete
+                mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab, acc,
+                                                     lane, uh, ul, kown, ready);
+                if constexpr (!X3_OWN) ready();
+            }
             aload_x3<G>(layer_rsrc(a.w[1], a.wbytes[1]), voff, w * P * TW * 2048, uh, ul);   // delta head unit 0
             h8 rh[PW], rl[PW];
             {
@@ -825,13 +860,16 @@ void rollout_x3(const RolloutArgs a) {
                     swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
                     swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
-            X3_BARRIER_ID(3);                          // layer input complete
+            auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // layer input complete
             X3_ST(4);
 #pragma unroll
             for (int j = 0; j < TW; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
-            mm_x3<TW, NC, P, G>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane, uh, ul);
+            // own k-steps first: this wave's slab writes need no barrier
+            mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane,
+                                                 uh, ul, kown, ready);
+            if constexpr (!X3_OWN) ready();
             X3_ST(5);
             load_next(l + 1);
             const float f = a.winv[l] * kTanhK;
