@@ -96,14 +96,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // epilogue's pre-activation is z = 2 log2(e) y with no extra multiply
 constexpr float kTanhK = 2.8853900817779268f;
 
-// tanh(y) * 2^12 from z = 2 log2(e) y: 4096 (1 - t) / (1 + t), t = 2^-|z| = e^{-2|y|},
-// sign restored (6 VALU ops, two of them transcendental).  Absolute error ~1e-7
-// (x 4096) near 0, a few ulp elsewhere; NaN propagates, +-inf -> +-4096.
+// tanh(y) * 2^12 from z = 2 log2(e) y: 4096 - 8192 / (1 + e), e = 2^z = e^{2y} (4 VALU
+// ops, two of them transcendental; no sign handling: e = inf -> 4096, e = 0 -> -4096).
+// Absolute error ~1e-7 (x 4096) near 0, a few ulp elsewhere; NaN propagates.
 __device__ __forceinline__ float tanh_x4096(float z) {
     if constexpr (X3_DIAG_NOTANH) return z * 1024.0f;
-    const float t = __builtin_amdgcn_exp2f(-fabsf(z));
-    const float r = __builtin_amdgcn_rcpf(fmaf(t, 1.0f / 4096.0f, 1.0f / 4096.0f));
-    return __builtin_copysignf(fmaf(-t, r, r), z);
+    const float r = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z) + 1.0f);
+    return fmaf(-8192.0f, r, 4096.0f);
 }
 
 // (a, b) -> packed f16 hi = RNE(a, b) and lo = RNE(a - hi, b - hi): v_cvt_pk_f16_f32,
@@ -328,21 +327,20 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
             v[4 + r] = tanh_x4096(fmaf(a1[r], f, b1[r]));
         }
     } else {
-        // the tanh_x4096 arithmetic on element pairs: the fmas as v_pk_fma_f32 (bit-identical,
-        // half the VALU issue), exp / rcp / sign per element
-        const f2 c = {1.0f / 4096.0f, 1.0f / 4096.0f};
+        // the tanh_x4096 arithmetic on element pairs: fma / add / fma as packed f32 ops
+        // (bit-identical, half the VALU issue), exp / rcp per element
+        const f2 one = {1.0f, 1.0f}, m8k = {-8192.0f, -8192.0f}, p4k = {4096.0f, 4096.0f};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const f4& a = k < 2 ? a0 : a1;
             const f4& b = k < 2 ? b0 : b1;
             const int r = (k & 1) * 2;
             const f2 z = __builtin_elementwise_fma((f2){a[r], a[r + 1]}, (f2){f, f}, (f2){b[r], b[r + 1]});
-            const f2 t = {__builtin_amdgcn_exp2f(-fabsf(z[0])), __builtin_amdgcn_exp2f(-fabsf(z[1]))};
-            const f2 d = __builtin_elementwise_fma(t, c, c);
+            const f2 d = (f2){__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])} + one;
             const f2 rr = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-            const f2 u = __builtin_elementwise_fma(-t, rr, rr);
-            v[2 * k] = __builtin_copysignf(u[0], z[0]);
-            v[2 * k + 1] = __builtin_copysignf(u[1], z[1]);
+            const f2 u = __builtin_elementwise_fma(m8k, rr, p4k);
+            v[2 * k] = u[0];
+            v[2 * k + 1] = u[1];
         }
     }
     split8(v, hi, lo);
