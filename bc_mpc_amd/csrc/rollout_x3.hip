@@ -312,6 +312,65 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
 }
 
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// A hidden layer in two tile halves (X3_HALF): half 0 (tiles [0, TW/2)) over all k-steps,
+// then half 1 with epi(n) -- half 0's epilogue, the caller's VALU -- issued after each of
+// its unit pairs n, so that the tanh / split work runs under this wave's own MFMAs instead
+// of after them.  Units are (half, k-step) with G = TW/2 tiles; k-steps in the rotated
+// order k0, k0+1, ... (mod P), the first PW of half 0 from the wave's own slab rows before
+// bar() (see mm_x3).  Every k-step's B fragments are read once per half.
+template <int TW, int NC, int P, int PW, bool OWN, typename Bar, typename Epi>
+__device__ __forceinline__ void mm_x3h(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
+                                       int lane, h8 (&s0h)[TW / 2], h8 (&s0l)[TW / 2], int k0, Bar bar, Epi epi) {
+    constexpr int G = TW / 2;
+    constexpr int STEPB = TW * 2048;
+    constexpr int NOWN = OWN ? PW : 0;
+    static_assert(P % 2 == 0 && NOWN % 2 == 0 && NOWN < P, "unit pairs");
+    const int voff = lane * 16;
+    auto kstep = [&](int i) {
+        const int p = i + k0;
+        return p >= P ? p - P : p;
+    };
+    auto uoff = [&](int u) {
+        const int half = u >= P ? 1 : 0;
+        return wbase + kstep(u - half * P) * STEPB + half * G * 2048;
+    };
+    h8 s1h[G], s1l[G], bh[NC], bl[NC];
+    auto pair0 = [&](int u) __attribute__((always_inline)) {     // half-0 units u, u+1
+        aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
+        __builtin_amdgcn_sched_barrier(0);
+        bread_x3<NC>(slab, kstep(u), lane, bh, bl);
+        unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
+        aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
+        __builtin_amdgcn_sched_barrier(0);
+        bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
+        unit_x3<TW, NC, G>(s1h, s1l, bh, bl, 0, acc);
+    };
+#pragma unroll
+    for (int u = 0; u < NOWN; u += 2) pair0(u);
+    if constexpr (OWN) bar();
+    for (int u = NOWN; u < P; u += 2) pair0(u);
+    static_for<0, P / 2>([&](auto nn) __attribute__((always_inline)) {
+        constexpr int n = decltype(nn)::value;
+        aload_x3<G>(rs, voff, uoff(P + 2 * n + 1), s1h, s1l, true);
+        __builtin_amdgcn_sched_barrier(0);
+        bread_x3<NC>(slab, kstep(2 * n), lane, bh, bl);
+        unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 1, acc);
+        if constexpr (2 * n + 2 < P) aload_x3<G>(rs, voff, uoff(P + 2 * n + 2), s0h, s0l, true);
+        __builtin_amdgcn_sched_barrier(0);
+        bread_x3<NC>(slab, kstep(2 * n + 1), lane, bh, bl);
+        unit_x3<TW, NC, G>(s1h, s1l, bh, bl, 1, acc);
+        epi(nn);
+    });
+}
+
 // Epilogue of one tile pair (k-step) for one column: BiasAdd (f32, after undoing
 // the operand scales; f and the LDS biases carry the 2 log2(e) factor), tanh,
 // x 2^12, split.
@@ -352,8 +411,17 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
 #ifndef X3_ONLY_NC
 #define X3_ONLY_NC 4
 #endif
+#ifndef X3_HALF                  // hidden layers in two tile halves, half 0's epilogue under half 1's MFMAs
+#define X3_HALF 0                // (measured 8% slower at cfg3: every k-step's B read twice, half-size units)
+#endif
+#ifndef X3_PRIO                  // 1: s_setprio 1 for the second-dispatched half of the waves
+#define X3_PRIO 0
+#endif
+// hidden layers split into tile halves where each half holds whole tile pairs
+__host__ __device__ constexpr bool x3_half(int TW) { return X3_HALF && TW % 4 == 0; }
 // tiles per streamed operand unit: a whole k-step up to 4 tiles per wave, else half
-__host__ __device__ constexpr int x3_group(int TW) { return TW <= 4 ? TW : TW / 2; }
+// (a tile half with X3_HALF)
+__host__ __device__ constexpr int x3_group(int TW) { return x3_half(TW) ? TW / 2 : TW <= 4 ? TW : TW / 2; }
 
 #ifndef X3_OWN                   // hidden layers start with the k-steps the wave produced itself
 #define X3_OWN 1
@@ -669,6 +737,8 @@ void rollout_x3(const RolloutArgs a) {
         }
     };
 
+    if constexpr (X3_PRIO == 1)
+        if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
     uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.H; ++h) {
@@ -864,19 +934,47 @@ void rollout_x3(const RolloutArgs a) {
             for (int j = 0; j < TW; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
-            // own k-steps first: this wave's slab writes need no barrier
-            mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane,
-                                                 uh, ul, kown, ready);
-            if constexpr (!X3_OWN) ready();
-            X3_ST(5);
-            load_next(l + 1);
             const float f = a.winv[l] * kTanhK;
+            if constexpr (x3_half(TW)) {
+                // half 0's epilogue (PW/2 tile pairs x NC columns) spread over half 1's unit pairs
+                constexpr int NJ = PW / 2 * NC, NP = P / 2;
+                auto epi0 = [&](auto nn) __attribute__((always_inline)) {
+                    constexpr int n = decltype(nn)::value;
+                    static_for<0, NJ>([&](auto jj) __attribute__((always_inline)) {
+                        constexpr int j = decltype(jj)::value;
+                        constexpr int at = NJ < NP ? 1 + j * (NP - 1) / NJ : j * NP / NJ;
+                        if constexpr (at == n) {
+                            constexpr int pp = j / NC, c = j % NC;
+                            epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q,
+                                     xh[pp][c], xl[pp][c]);
+                        }
+                    });
+                };
+                mm_x3h<TW, NC, P, PW, X3_OWN != 0>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc,
+                                                   lane, uh, ul, kown, ready, epi0);
+                if constexpr (!X3_OWN) ready();
+                X3_ST(5);
+                load_next(l + 1);
 #pragma unroll
-            for (int pp = 0; pp < PW; ++pp)
+                for (int pp = PW / 2; pp < PW; ++pp)
 #pragma unroll
-                for (int c = 0; c < NC; ++c)
-                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
-                             xl[pp][c]);
+                    for (int c = 0; c < NC; ++c)
+                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
+                                 xl[pp][c]);
+            } else {
+                // own k-steps first: this wave's slab writes need no barrier
+                mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc,
+                                                     lane, uh, ul, kown, ready);
+                if constexpr (!X3_OWN) ready();
+                X3_ST(5);
+                load_next(l + 1);
+#pragma unroll
+                for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c)
+                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
+                                 xl[pp][c]);
+            }
         }
         X3_ST(6);
 
