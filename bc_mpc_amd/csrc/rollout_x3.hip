@@ -203,6 +203,29 @@ __device__ __forceinline__ void unit_x3s(const h8 (&ah)[G], const h8 (&al)[G], c
 #ifndef X3_BSTREAM
 #define X3_BSTREAM 0
 #endif
+#ifndef X3_BROLL                 // B fragments of the next k-step read column by column as the current
+#define X3_BROLL 0               // unit's MFMAs release them (measured 3% slower at cfg3)
+#endif
+
+// unit_x3 with a rolling B prefetch: once column c's three passes are issued, its B
+// registers are reloaded with column c of k-step knext (NEXT)
+template <int TW, int NC, int G, bool NEXT>
+__device__ __forceinline__ void unit_x3r(const h8 (&ah)[G], const h8 (&al)[G], h8 (&bh)[NC], h8 (&bl)[NC], int g,
+                                         f4 (&acc)[TW][NC], const f4* slab, int knext, int lane) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bh[c], acc[g * G + j][c]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bl[c], acc[g * G + j][c]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(al[j], bh[c], acc[g * G + j][c]);
+        if constexpr (NEXT) {
+            bh[c] = sread(slab + sidx<NC>(knext, c, 0, lane));
+            bl[c] = sread(slab + sidx<NC>(knext, c, 1, lane));
+        }
+    }
+}
 
 template <int NC>
 __device__ __forceinline__ void bread_x3(const f4* slab, int p, int lane, h8 (&bh)[NC], h8 (&bl)[NC]) {
@@ -275,6 +298,23 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
             unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
         }
         bar();
+    }
+    if constexpr (NG == 1 && X3_BROLL) {
+        // (OWN: the own units above read their own B; the rolling chain starts after bar())
+        bread_x3<NC>(slab, kstep(NOWN), lane, bh, bl);
+        for (int u = NOWN; u < NU - 2; u += 2) {
+            aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
+            __builtin_amdgcn_sched_barrier(0);
+            unit_x3r<TW, NC, G, true>(s0h, s0l, bh, bl, 0, acc, slab, kstep(u + 1), lane);
+            aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
+            __builtin_amdgcn_sched_barrier(0);
+            unit_x3r<TW, NC, G, true>(s1h, s1l, bh, bl, 0, acc, slab, kstep(u + 2), lane);
+        }
+        aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
+        __builtin_amdgcn_sched_barrier(0);
+        unit_x3r<TW, NC, G, true>(s0h, s0l, bh, bl, 0, acc, slab, kstep(NU - 1), lane);
+        unit_x3r<TW, NC, G, false>(s1h, s1l, bh, bl, 0, acc, slab, 0, lane);
+        return;
     }
     // (the last pair is peeled so that every load in the loop is unconditional: a
     // conditional load would make the compiler drain vmcnt to 0 at the merge)
