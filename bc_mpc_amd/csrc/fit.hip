@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -120,12 +121,16 @@ static hipError_t gemm(const float* A, const float* B, float* C, const float* bi
 // ---------------------------------------------------------------- gather ---
 // X0[b] = [(s - mean_obs)/(std_obs+1e-10), (a - mean_act)/(std_act+1e-10)] (f32),
 // T[b] = (delta - mean_d)/(std_d+1e-10) (f32); f64 arithmetic as numpy (dynamics.py:73-75, 92-95)
+// The batch of iteration *iter is idx_base[iter * stride ...] (stride 0: the caller offset the base),
+// so one launch sequence serves every iteration of a graph.
 __global__ void fit_gather(const double* __restrict__ st, const double* __restrict__ ac,
-                           const double* __restrict__ de, const int64_t* __restrict__ idx, const double* __restrict__ nc,
+                           const double* __restrict__ de, const int64_t* __restrict__ idx_base, int stride,
+                           const int32_t* __restrict__ iter, const double* __restrict__ nc,
                            float* __restrict__ X0, float* __restrict__ T, int B, int S, int A) {
     const int IN = S + A;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B * (IN + S)) return;
+    const int64_t* idx = idx_base + (int64_t)(*iter) * stride;
     const int b = i / (IN + S), c = i % (IN + S);
     const int64_t r = idx[b];
     if (c < S) {
@@ -213,18 +218,23 @@ __global__ void fit_act_bwd(const float* __restrict__ dH, float* __restrict__ dZ
 }
 
 // column sums: out[f] = sum_r X[r][f] (bias grads); with Aact: out2[f] = sum_r X[r][f] * xhat[r][f]
-// where xhat = (A - mean_r) rs_r (LN gamma grads; out = beta grads).  Block = 64 columns x 16
-// row groups (rows strided by 16), partials combined in row-group order (deterministic).
-__global__ __launch_bounds__(1024) void fit_colsum(const float* __restrict__ X, float* __restrict__ out, int B,
-                                                   int F, const float* __restrict__ Aact,
-                                                   const float* __restrict__ mean_in,
-                                                   const float* __restrict__ rs_in, float* __restrict__ out2) {
-    __shared__ float p1[16][64], p2[16][64];
+// where xhat = (A - mean_r) rs_r (LN gamma grads; out = beta grads).  Grid = 64-column blocks x RB
+// row chunks (enough blocks to fill the chip at batch 512); block = 64 columns x 4 row groups.
+// Each block leaves its chunk's partials in part[chunk][F]; the last block of a column block to
+// finish (ticket counter) adds the chunks in chunk order: deterministic in one launch.
+constexpr int kColChunks = 16;
+__global__ __launch_bounds__(256) void fit_colsum(const float* __restrict__ X, float* __restrict__ out, int B, int F,
+                                                  const float* __restrict__ Aact, const float* __restrict__ mean_in,
+                                                  const float* __restrict__ rs_in, float* __restrict__ out2,
+                                                  float* __restrict__ part, unsigned* __restrict__ tickets) {
+    __shared__ float p1[4][64], p2[4][64];
     const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int f = blockIdx.x * 64 + c;
+    const int nchunk = gridDim.y, chunk = blockIdx.y;
+    const int r0 = (int)(((int64_t)B * chunk) / nchunk), r1 = (int)(((int64_t)B * (chunk + 1)) / nchunk);
     float s = 0.f, s2 = 0.f;
     if (f < F)
-        for (int r = g; r < B; r += 16) {
+        for (int r = r0 + g; r < r1; r += 4) {
             const float x = X[(size_t)r * F + f];
             s += x;
             if (out2) s2 += x * (Aact[(size_t)r * F + f] - mean_in[r]) * rs_in[r];
@@ -233,16 +243,42 @@ __global__ __launch_bounds__(1024) void fit_colsum(const float* __restrict__ X, 
     p2[g][c] = s2;
     __syncthreads();
     if (g == 0 && f < F) {
+        part[(size_t)chunk * 2 * F + f] = p1[0][c] + p1[1][c] + p1[2][c] + p1[3][c];
+        part[(size_t)chunk * 2 * F + F + f] = p2[0][c] + p2[1][c] + p2[2][c] + p2[3][c];
+    }
+    // publish (agent-scope release once per block, then the ticket; cdna_hip_programming.md
+    // "In-launch split-K reduction"): correct for any spread of the chunks over XCDs
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        p1[0][0] = t == (unsigned)nchunk - 1 ? 1.f : 0.f;     // "last" through the existing LDS array
+        if (t == (unsigned)nchunk - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (p1[0][0] == 0.f) return;
+    if (g == 0 && f < F) {
         float t = 0.f, t2 = 0.f;
-        for (int k = 0; k < 16; ++k) { t += p1[k][c]; t2 += p2[k][c]; }
+        for (int k = 0; k < nchunk; ++k) {
+            t += part[(size_t)k * 2 * F + f];
+            t2 += part[(size_t)k * 2 * F + F + f];
+        }
         out[f] = t;
         if (out2) out2[f] = t2;
     }
+    if (threadIdx.x == 0) tickets[blockIdx.x] = 0;       // ready for the next launch (stream order)
 }
 
 // loss = mean((T - P)^2) (one block), dP = -((2 * (1/N)) * (T - P))
 __global__ __launch_bounds__(1024) void fit_loss(const float* __restrict__ P, const float* __restrict__ T,
-                                                 float* __restrict__ dP, float* __restrict__ loss, int n) {
+                                                 float* __restrict__ dP, float* __restrict__ loss_base,
+                                                 const int32_t* __restrict__ iter, int n) {
+    float* loss = loss_base + *iter;
     __shared__ float red[16];
     const float inv = 1.0f / (float)n;
     float s = 0.f;
@@ -261,17 +297,29 @@ __global__ __launch_bounds__(1024) void fit_loss(const float* __restrict__ P, co
     }
 }
 
-// TF1 ApplyAdam over the flat parameter vector
+// TF1 ApplyAdam over the flat parameter vector; lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t)
+// in f32 from the device beta powers bp[2] (correctly rounded, as the host expression)
 __global__ void fit_adam(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
-                         const float* __restrict__ g, int64_t n, float lr_t, float b1, float b2, float eps) {
+                         const float* __restrict__ g, int64_t n, const float* __restrict__ bp, float lr, float b1,
+                         float b2, float eps) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const float lr_t = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.0f, bp[1]))), __fsub_rn(1.0f, bp[0]));
     const float gi = g[i];
     const float mi = m[i] + (gi - m[i]) * (1.0f - b1);
     const float vi = v[i] + (gi * gi - v[i]) * (1.0f - b2);
     m[i] = mi;
     v[i] = vi;
     w[i] = w[i] - (mi * lr_t) / (sqrtf(vi) + eps);
+}
+
+// end of an iteration: beta powers *= beta (TF1 _finish), iteration counter + 1
+__global__ void fit_step_end(int32_t* __restrict__ iter, float* __restrict__ bp, float b1, float b2) {
+    if (threadIdx.x == 0) {
+        bp[0] = __fmul_rn(bp[0], b1);
+        bp[1] = __fmul_rn(bp[1], b2);
+        *iter += 1;
+    }
 }
 
 }  // namespace bcmpc
@@ -303,7 +351,16 @@ struct bcmpc_fitter {
     double *d_st = nullptr, *d_ac = nullptr, *d_de = nullptr, *d_nc = nullptr;
     int64_t n_data = 0, data_cap = 0;
     int64_t* d_idx = nullptr; int64_t idx_cap = 0;
-    float beta1_power = 0.f, beta2_power = 0.f;   // TF1 Adam accumulators (f32 variables)
+    float beta1_power = 0.f, beta2_power = 0.f;   // TF1 Adam accumulators (f32 variables), host mirror
+    int32_t* d_iter = nullptr;                    // iteration counter of the running fit (device)
+    float* d_bp = nullptr;                        // [beta1_power, beta2_power] (device)
+    float* d_cpart = nullptr;                     // column-sum chunk partials [kColChunks][2][max width]
+    unsigned* d_tickets = nullptr;                // column-sum completion tickets (one per 64 columns)
+    // one captured graph of a whole uniform-batch run, reused while its shape and buffers match
+    hipGraphExec_t graph = nullptr;
+    int32_t graph_iters = 0, graph_b = 0;
+    const void* graph_idx = nullptr;
+    const void* graph_loss = nullptr;
     int64_t step = 0;
     bool has_weights = false;
 };
@@ -352,10 +409,15 @@ int bcmpc_fit_create(const bcmpc_fit_config* c, bcmpc_fitter** out) {
               al((void**)&f->d_mean, L * B * 4) && al((void**)&f->d_rs, L * B * 4) && al((void**)&f->d_dh, B * H * 4) &&
               al((void**)&f->d_dz, B * H * 4) &&
               al((void**)&f->d_split, (f->split_floats = 8 * (size_t)std::max(f->IN, f->h) * std::max(f->h, f->S)) * 4) &&
-              al((void**)&f->d_nc, kConstRows * kConstCols * 8);
+              al((void**)&f->d_nc, kConstRows * kConstCols * 8) && al((void**)&f->d_iter, 4) &&
+              al((void**)&f->d_bp, 8) &&
+              al((void**)&f->d_cpart, (size_t)kColChunks * 2 * std::max(f->h, f->S) * 4) &&
+              al((void**)&f->d_tickets, 64 * 4);
     if (!ok) { bcmpc_fit_destroy(f); return ffail(BCMPC_ERR_HIP, "device allocation failed"); }
     (void)hipMemset(f->d_m, 0, off * 4);
     (void)hipMemset(f->d_v, 0, off * 4);
+    (void)hipMemset(f->d_g, 0, off * 4);
+    (void)hipMemset(f->d_tickets, 0, 64 * 4);     // (the LN slots of a net without LayerNorm stay 0: no update)
     f->beta1_power = c->beta1;
     f->beta2_power = c->beta2;
     *out = f;
@@ -365,7 +427,8 @@ int bcmpc_fit_create(const bcmpc_fit_config* c, bcmpc_fitter** out) {
 int bcmpc_fit_destroy(bcmpc_fitter* f) {
     if (!f) return BCMPC_OK;
     if (f->stream) (void)hipStreamSynchronize(f->stream);
-    for (void* p : {(void*)f->d_w, (void*)f->d_m, (void*)f->d_v, (void*)f->d_g, (void*)f->d_x0, (void*)f->d_t,
+    if (f->graph) (void)hipGraphExecDestroy(f->graph);
+    for (void* p : {(void*)f->d_iter, (void*)f->d_bp, (void*)f->d_cpart, (void*)f->d_tickets, (void*)f->d_w, (void*)f->d_m, (void*)f->d_v, (void*)f->d_g, (void*)f->d_x0, (void*)f->d_t,
                     (void*)f->d_p, (void*)f->d_dp, (void*)f->d_act, (void*)f->d_hln, (void*)f->d_mean,
                     (void*)f->d_rs, (void*)f->d_dh, (void*)f->d_dz, (void*)f->d_loss, (void*)f->d_st,
                     (void*)f->d_ac, (void*)f->d_de, (void*)f->d_nc, (void*)f->d_idx, (void*)f->d_split})
@@ -456,7 +519,7 @@ int bcmpc_fit_set_data(bcmpc_fitter* f, const double* states, const double* acti
     return BCMPC_OK;
 }
 
-static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int B, float* d_loss) {
+static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int stride, int B, float* d_loss) {
     hipStream_t st = f->stream;
     const int S = f->S, IN = f->IN, L = f->L, h = f->h, act = f->cfg.activation, ln = f->cfg.layer_norm;
     const size_t BH = (size_t)f->Bmax * h;
@@ -465,7 +528,7 @@ static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int B, float* d_
 #define FIT_TRY(x) do { if ((x) != hipSuccess) return ffail(BCMPC_ERR_HIP, #x); } while (0)
     const int ng = B * (IN + S);
     hipLaunchKernelGGL(fit_gather, dim3((ng + 255) / 256), dim3(256), 0, st, f->d_st, f->d_ac, f->d_de, d_idx,
-                       f->d_nc, f->d_x0, f->d_t, B, S, f->A);
+                       stride, f->d_iter, f->d_nc, f->d_x0, f->d_t, B, S, f->A);
     FIT_TRY(hipGetLastError());
     // ---- forward ----
     const dim3 rows((B + 3) / 4), rthreads(256);
@@ -480,21 +543,23 @@ static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int B, float* d_
     }
     const float* HL = ln ? f->d_hln + (L - 1) * BH : f->d_act + (L - 1) * BH;
     FIT_TRY((gemm<false, false>(HL, W + f->w_off[L], f->d_p, W + f->b_off[L], B, S, h, h, S, S, st)));
-    hipLaunchKernelGGL(fit_loss, dim3(1), dim3(1024), 0, st, f->d_p, f->d_t, f->d_dp, d_loss, B * S);
+    hipLaunchKernelGGL(fit_loss, dim3(1), dim3(1024), 0, st, f->d_p, f->d_t, f->d_dp, d_loss, f->d_iter, B * S);
     FIT_TRY(hipGetLastError());
     // ---- backward ----
     // output layer: dW_L = H_L^T dP, db_L = colsum dP, dH = dP W_L^T
     FIT_TRY((gemm<true, false>(HL, f->d_dp, G + f->w_off[L], nullptr, h, S, B, h, S, S, st, f->d_split,
                                f->split_floats)));
-    hipLaunchKernelGGL(fit_colsum, dim3((S + 63) / 64), dim3(1024), 0, st, f->d_dp, G + f->b_off[L], B, S, nullptr,
-                       nullptr, nullptr, nullptr);
+    const int nch = std::max(1, std::min(kColChunks, B / 32));
+    hipLaunchKernelGGL(fit_colsum, dim3((S + 63) / 64, nch), dim3(256), 0, st, f->d_dp, G + f->b_off[L], B, S, nullptr,
+                       nullptr, nullptr, nullptr, f->d_cpart, f->d_tickets);
     FIT_TRY(hipGetLastError());
     FIT_TRY((gemm<false, true>(f->d_dp, W + f->w_off[L], f->d_dh, nullptr, B, h, S, S, S, h, st)));
     for (int l = L - 1; l >= 0; --l) {
         const float* Aact = f->d_act + l * BH;
         if (ln)   // LN grads: beta = colsum dH, gamma = colsum dH * xhat
-            hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64), dim3(1024), 0, st, f->d_dh, G + f->be_off[l], B, h,
-                               Aact, f->d_mean + l * f->Bmax, f->d_rs + l * f->Bmax, G + f->g_off[l]);
+            hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64, nch), dim3(256), 0, st, f->d_dh, G + f->be_off[l], B,
+                               h, Aact, f->d_mean + l * f->Bmax, f->d_rs + l * f->Bmax, G + f->g_off[l], f->d_cpart,
+                               f->d_tickets);
         hipLaunchKernelGGL(fit_act_bwd, rows, rthreads, 0, st, f->d_dh, f->d_dz, Aact, f->d_mean + l * f->Bmax,
                            f->d_rs + l * f->Bmax, W + f->g_off[l], B, h, act, ln);
         FIT_TRY(hipGetLastError());
@@ -502,26 +567,20 @@ static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int B, float* d_
         const int in = l == 0 ? IN : h;
         FIT_TRY((gemm<true, false>(Hin, f->d_dz, G + f->w_off[l], nullptr, in, h, B, in, h, h, st, f->d_split,
                                    f->split_floats)));
-        hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64), dim3(1024), 0, st, f->d_dz, G + f->b_off[l], B, h,
-                           nullptr, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64, nch), dim3(256), 0, st, f->d_dz, G + f->b_off[l], B, h,
+                           nullptr, nullptr, nullptr, nullptr, f->d_cpart, f->d_tickets);
         FIT_TRY(hipGetLastError());
         if (l > 0) FIT_TRY((gemm<false, true>(f->d_dz, W + f->w_off[l], f->d_dh, nullptr, B, in, h, h, h, in, st)));
     }
-    if (!ln)   // the LN slots of a model without LayerNorm are not variables: no update
-        for (int l = 0; l < L; ++l) {
-            FIT_TRY(hipMemsetAsync(G + f->g_off[l], 0, (size_t)h * 4, st));
-            FIT_TRY(hipMemsetAsync(G + f->be_off[l], 0, (size_t)h * 4, st));
-        }
+    // (without LayerNorm the LN slots of G are never written: zero since create, no update)
     // ---- Adam (TF1 ApplyAdam; beta powers are f32 variables updated after the step) ----
     const float b1 = f->cfg.beta1, b2 = f->cfg.beta2;
-    const float lr_t = f->cfg.learning_rate * std::sqrt(1.0f - f->beta2_power) / (1.0f - f->beta1_power);
     const int64_t n = (int64_t)f->n_params;
-    hipLaunchKernelGGL(fit_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, f->d_m, f->d_v, G, n, lr_t,
-                       b1, b2, f->cfg.epsilon);
+    hipLaunchKernelGGL(fit_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, f->d_m, f->d_v, G, n,
+                       f->d_bp, f->cfg.learning_rate, b1, b2, f->cfg.epsilon);
     FIT_TRY(hipGetLastError());
-    f->beta1_power *= b1;
-    f->beta2_power *= b2;
-    ++f->step;
+    hipLaunchKernelGGL(fit_step_end, dim3(1), dim3(64), 0, st, f->d_iter, f->d_bp, b1, b2);
+    FIT_TRY(hipGetLastError());
 #undef FIT_TRY
     return BCMPC_OK;
 }
@@ -557,11 +616,53 @@ int bcmpc_fit_run(bcmpc_fitter* f, const int64_t* indices, const int32_t* batch_
             return ffail(BCMPC_ERR_HIP, "loss buffer allocation failed");
         f->loss_cap = iterations;
     }
-    int64_t pos = 0;
-    for (int i = 0; i < iterations; ++i) {
-        const int rc = fit_iteration(f, f->d_idx + pos, batch_sizes[i], f->d_loss + i);
-        if (rc != BCMPC_OK) return rc;
-        pos += batch_sizes[i];
+    // device iteration state: counter 0, the host mirror's beta powers
+    const float bp[2] = {f->beta1_power, f->beta2_power};
+    if (hipMemsetAsync(f->d_iter, 0, 4, f->stream) != hipSuccess ||
+        hipMemcpyAsync(f->d_bp, bp, 8, hipMemcpyHostToDevice, f->stream) != hipSuccess)
+        return ffail(BCMPC_ERR_HIP, "iteration state upload failed");
+    bool uniform = iterations > 0;
+    for (int i = 1; i < iterations; ++i) uniform = uniform && batch_sizes[i] == batch_sizes[0];
+    const char* ge = std::getenv("BCMPC_FIT_GRAPH");
+    const bool use_graph = uniform && !(ge && ge[0] == '0');
+    if (use_graph) {
+        // the whole run as one graph (~20 launches per iteration otherwise dominate a 512-row step)
+        if (!(f->graph && f->graph_iters == iterations && f->graph_b == batch_sizes[0] && f->graph_idx == f->d_idx &&
+              f->graph_loss == f->d_loss)) {
+            if (f->graph) (void)hipGraphExecDestroy(f->graph);
+            f->graph = nullptr;
+            if (hipStreamBeginCapture(f->stream, hipStreamCaptureModeThreadLocal) != hipSuccess)
+                return ffail(BCMPC_ERR_HIP, "graph capture failed to start");
+            int rc = BCMPC_OK;
+            for (int i = 0; i < iterations && rc == BCMPC_OK; ++i)
+                rc = fit_iteration(f, f->d_idx, batch_sizes[0], batch_sizes[0], f->d_loss);
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(f->stream, &g);
+            if (rc != BCMPC_OK || ec != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc != BCMPC_OK ? rc : ffail(BCMPC_ERR_HIP, "graph capture failed");
+            }
+            const hipError_t ei = hipGraphInstantiate(&f->graph, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ei != hipSuccess) { f->graph = nullptr; return ffail(BCMPC_ERR_HIP, "graph instantiation failed"); }
+            f->graph_iters = iterations;
+            f->graph_b = batch_sizes[0];
+            f->graph_idx = f->d_idx;
+            f->graph_loss = f->d_loss;
+        }
+        if (hipGraphLaunch(f->graph, f->stream) != hipSuccess) return ffail(BCMPC_ERR_HIP, "graph launch failed");
+    } else {
+        int64_t pos = 0;
+        for (int i = 0; i < iterations; ++i) {
+            const int rc = fit_iteration(f, f->d_idx + pos, 0, batch_sizes[i], f->d_loss);
+            if (rc != BCMPC_OK) return rc;
+            pos += batch_sizes[i];
+        }
+    }
+    for (int i = 0; i < iterations; ++i) {       // host mirror of the device beta powers (same f32 products)
+        f->beta1_power *= f->cfg.beta1;
+        f->beta2_power *= f->cfg.beta2;
+        ++f->step;
     }
     if (losses && iterations > 0 &&
         hipMemcpyAsync(losses, f->d_loss, (size_t)iterations * 4, hipMemcpyDeviceToHost, f->stream) != hipSuccess)

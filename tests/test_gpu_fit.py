@@ -99,3 +99,39 @@ def test_model_fit_dropin_updates_weights_and_engine():
     ps = orc.fit_params(w)
     want = orc.fit(ps, orc.AdamState.zeros_like(ps), 2, "relu", True, norm, states, actions, deltas, batches, 1e-3)
     assert np.isclose(loss, want[-1], rtol=1e-3)
+
+
+def test_fit_graph_and_launch_paths_identical(monkeypatch):
+    """A uniform-batch run executes as one captured graph; ragged batches (and BCMPC_FIT_GRAPH=0)
+    launch per iteration.  Same kernels, same device iteration state: bit-identical results."""
+    from bc_mpc_amd.engine import MLPSpec
+    from bc_mpc_amd.fit import GPUFitter
+    w = orc.synthetic_weights(20, 6, 128, 2, "relu", True, seed_base=3)
+    norm, states, actions, deltas = _data(1500)
+    rs = np.random.RandomState(4)
+    batches = [rs.choice(1500, 256, replace=False) for _ in range(12)]
+    out = []
+    for graph in ("1", "0"):
+        monkeypatch.setenv("BCMPC_FIT_GRAPH", graph)
+        f = GPUFitter(20, 6, 128, 2, "relu", True, 256, 1e-3, device=0)
+        f.set_params(MLPSpec(w.kernels, w.biases, "relu", w.ln_gamma, w.ln_beta), norm)
+        f.set_data(states, actions, deltas)
+        l1 = f.run(batches[:8])
+        l2 = f.run(batches[8:])                   # a second run continues the Adam state
+        out.append((np.concatenate([l1, l2]), f.get_params()))
+        f.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    for a, b in zip(out[0][1], out[1][1]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    # ragged batches take the launch path and still match the oracle
+    ps = orc.fit_params(w)
+    ragged = [rs.choice(1500, n, replace=False) for n in (256, 100, 256, 7)]
+    monkeypatch.setenv("BCMPC_FIT_GRAPH", "1")
+    f = GPUFitter(20, 6, 128, 2, "relu", True, 256, 1e-3, device=0)
+    f.set_params(MLPSpec(w.kernels, w.biases, "relu", w.ln_gamma, w.ln_beta), norm)
+    f.set_data(states, actions, deltas)
+    got = f.run(ragged)
+    want = orc.fit(ps, orc.AdamState.zeros_like(ps), 2, "relu", True, norm, states, actions, deltas, ragged, 1e-3)
+    assert np.allclose(got, want, rtol=1e-4, atol=0)
+    f.close()
