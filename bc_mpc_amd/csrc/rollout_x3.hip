@@ -457,6 +457,9 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
 #ifndef X3_PRIO                  // 1: s_setprio 1 for the second-dispatched half of the waves
 #define X3_PRIO 0
 #endif
+#ifndef X3_STAGGER               // diagnostic: odd workgroups start X3_STAGGER x 8k cycles late
+#define X3_STAGGER 0
+#endif
 // hidden layers split into tile halves where each half holds whole tile pairs
 __host__ __device__ constexpr bool x3_half(int TW) { return X3_HALF && TW % 4 == 0; }
 // tiles per streamed operand unit: a whole k-step up to 4 tiles per wave, else half
@@ -779,6 +782,9 @@ void rollout_x3(const RolloutArgs a) {
 
     if constexpr (X3_PRIO == 1)
         if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if constexpr (X3_STAGGER > 0)                     // diagnostic: de-phase alternate workgroups
+        if (blockIdx.x & 1)
+            for (int i = 0; i < X3_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
     uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.H; ++h) {
