@@ -5,7 +5,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-s
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
 OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/cem.o build/fit.o build/capi.o
-HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h
+HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h $(SRC)/argmin_common.h
 
 all: $(LIB)
 

@@ -1,0 +1,35 @@
+// argmin_common.h -- the np.argmin result record (controllers.py:82-85), shared by the
+// two-launch argmin (rollout.hip) and the split kernel's fused tail (rollout_x3.hip).
+#pragma once
+#include "device_common.h"
+#include "kernels.h"
+
+namespace bcmpc {
+
+// Writes out->{best_index, best_cost, first_action} for the winning (cost, index) record
+// (maximize: the record holds -cost).  CEM merge: np.argmin over the iteration-major
+// concatenation keeps the earlier best on ties.
+__device__ __forceinline__ void argmin_write(const ArgminArgs& a, Best best) {
+    bcmpc_result* out = a.out;
+    if (a.merge) {
+        const double prev = out->best_cost;
+        const Best ex{a.maximize ? -prev : prev, out->best_index - a.pos_base};
+        if (!better(best, ex)) return;
+    }
+    out->best_index = (a.merge || a.cem_mu ? a.pos_base : a.cand_offset) + best.i;
+    out->best_cost = a.maximize ? -best.c : best.c;
+    for (int j = 0; j < BCMPC_MAX_ACTION; ++j) out->first_action[j] = 0.0;
+    if (best.i < a.K) {
+        const uint64_t g = (uint64_t)(a.cand_offset + best.i);
+        for (int j = 0; j < a.A; ++j) {
+            const double lo = a.consts[6 * 32 + j], hi = a.consts[7 * 32 + j];
+            out->first_action[j] =
+                a.act_out ? a.act_out[best.i * a.A + j]     // policy-mixed actions (controllers.py:233-235)
+                : a.cem_mu ? cem_action(a.seed, g, 0, j, a.cem_iter, a.cem_mu[j], a.cem_sigma[j], lo, hi)
+                : a.actions ? a.actions[best.i * a.A + j]   // action_paths[0, i*, :] (controllers.py:84-85)
+                          : rng_action(a.seed, g, 0, j, lo, hi);
+        }
+    }
+}
+
+}  // namespace bcmpc

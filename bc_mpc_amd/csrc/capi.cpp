@@ -132,6 +132,8 @@ struct bcmpc_engine {
     bcmpc_result* d_result = nullptr;
     double* d_amin_c = nullptr;         // argmin scratch: per-block best
     int64_t* d_amin_i = nullptr;
+    size_t amin_cap = 0;                // records the scratch holds
+    unsigned* d_amin_ticket = nullptr;  // fused argmin (split kernel): last-workgroup ticket
     bcmpc_result* h_result = nullptr;   // pinned
     double h_consts[kConstRows * kConstCols]{};
     uint64_t version = 0;
@@ -324,8 +326,12 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         hipMalloc(&e->d_state, BCMPC_MAX_STATE * sizeof(double)) != hipSuccess ||
         hipMalloc(&e->d_costs, std::max<int64_t>(1, c.num_paths) * sizeof(double)) != hipSuccess ||
         hipMalloc(&e->d_result, sizeof(bcmpc_result)) != hipSuccess ||
-        hipMalloc(&e->d_amin_c, kArgminParts * sizeof(double)) != hipSuccess ||
-        hipMalloc(&e->d_amin_i, kArgminParts * sizeof(int64_t)) != hipSuccess ||
+        // (the split kernel's fused argmin keeps one record per workgroup)
+        hipMalloc(&e->d_amin_c, (e->amin_cap = std::max<size_t>(kArgminParts, (size_t)(c.num_paths + 15) / 16)) *
+                                    sizeof(double)) != hipSuccess ||
+        hipMalloc(&e->d_amin_i, e->amin_cap * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc(&e->d_amin_ticket, sizeof(unsigned)) != hipSuccess ||
+        hipMemset(e->d_amin_ticket, 0, sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&e->h_result, sizeof(bcmpc_result), hipHostMallocDefault) != hipSuccess) {
         g_last_error = "device allocation failed";
         return cleanup(BCMPC_ERR_HIP);
@@ -371,7 +377,8 @@ int bcmpc_destroy(bcmpc_engine* e) {
     for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
                     (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
-                    (void*)e->d_count, (void*)e->d_amin_c, (void*)e->d_amin_i})
+                    (void*)e->d_count, (void*)e->d_amin_c, (void*)e->d_amin_i,
+                    (void*)e->d_amin_ticket})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
     for (auto& ev : e->ev)
@@ -670,6 +677,30 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.cem_sigma = cem->sigma;
         a.cem_iter = cem->iter;
     }
+    ArgminArgs m{};
+    if (d_result) {
+        m.costs = d_costs; m.actions = d_actions; m.consts = e->d_consts; m.out = d_result;
+        m.act_out = e->PL > 0 ? e->d_first : nullptr;
+        m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
+        m.maximize = c.cost == BCMPC_COST_REWARD;
+        m.scratch_c = e->d_amin_c;
+        m.scratch_i = e->d_amin_i;
+        m.nparts = argmin_parts(c.num_paths);
+        if (cem) {
+            m.cem_mu = cem->mu; m.cem_sigma = cem->sigma; m.cem_iter = cem->iter;
+            m.merge = cem->merge; m.pos_base = cem->pos_base;
+        }
+    }
+    // BCMPC_FUSED_ARGMIN=1: the split kernel reduces np.argmin in its own tail (one launch per
+    // get_action).  Off by default: the tail's ticket + acquire cost ~6 us in-kernel, as much as the
+    // two argmin launches it replaces, and p50 did not move (cfg1/cfg2/run.sh recipe)
+    const char* fa = std::getenv("BCMPC_FUSED_ARGMIN");
+    const bool fused = e->split && d_result && fa && fa[0] == '1';
+    if (fused) {
+        a.fused_argmin = 1;
+        a.amin = m;
+        a.amin_ticket = e->d_amin_ticket;
+    }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
     if (e->split) {
         // diagnostics: X3_STAMP builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
@@ -711,21 +742,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         HIP_TRY(launch_rollout_grp(a, e->HP, kern_waves(e->kernel), st));
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[1], st));
-    if (d_result) {
-        ArgminArgs m{};
-        m.costs = d_costs; m.actions = d_actions; m.consts = e->d_consts; m.out = d_result;
-        m.act_out = e->PL > 0 ? e->d_first : nullptr;
-        m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
-        m.maximize = c.cost == BCMPC_COST_REWARD;
-        m.scratch_c = e->d_amin_c;
-        m.scratch_i = e->d_amin_i;
-        m.nparts = argmin_parts(c.num_paths);
-        if (cem) {
-            m.cem_mu = cem->mu; m.cem_sigma = cem->sigma; m.cem_iter = cem->iter;
-            m.merge = cem->merge; m.pos_base = cem->pos_base;
-        }
-        HIP_TRY(launch_argmin(m, st));
-    }
+    if (d_result && !fused) HIP_TRY(launch_argmin(m, st));
     if (record_events) HIP_TRY(hipEventRecord(e->ev[2], st));
     e->timed = d_result != nullptr;
     return BCMPC_OK;

@@ -14,6 +14,27 @@ namespace bcmpc {
 constexpr int kConstRows = 10;
 constexpr int kConstCols = 32;
 
+struct ArgminArgs {
+    const double* costs;
+    const double* act_out;   // [.][K][A] actions written by the rollout (policy mode) or nullptr
+    const double* actions;   // [H][K][A] or nullptr
+    const double* consts;
+    bcmpc_result* out;
+    uint64_t seed;
+    int64_t cand_offset;
+    int64_t K;
+    int32_t A;
+    int32_t maximize;        // np.argmax (learned reward, controllers.py:152) instead of np.argmin
+    // CEM: first action regenerated from the sampler; merge with the running best by stream position
+    const double* cem_mu;
+    const double* cem_sigma;
+    int32_t cem_iter;
+    int32_t merge;           // keep out's previous best unless strictly better (np.argmin over iterations)
+    int64_t pos_base;        // position of candidate 0 in the concatenated stream (iter * K_global + offset)
+    double* scratch_c;       // [kArgminParts] per-block best (argmin_partial -> argmin_final)
+    int64_t* scratch_i;
+    int32_t nparts;          // argmin_parts(K)
+};
 struct RolloutArgs {
     const float __attribute__((ext_vector_type(4)))* w[BCMPC_MAX_LAYERS + 1];  // packed kernels
     int32_t wbytes[BCMPC_MAX_LAYERS + 1];    // packed bytes per layer (buffer num_records)
@@ -52,6 +73,12 @@ struct RolloutArgs {
     float winv[BCMPC_MAX_LAYERS + 1];
     float pwinv[BCMPC_MAX_LAYERS + 1];       // the same for the fused policy's layers
     uint64_t* stamps;                        // diagnostics (X3_STAMP builds): [blocks][NW][10] phase cycles
+    // split kernel: np.argmin fused into the launch's tail (fused_argmin != 0): every workgroup
+    // leaves its best (cost, index) in amin.scratch_c/i[blockIdx.x], the last to finish (ticket)
+    // reduces them and writes amin.out like argmin_final
+    int32_t fused_argmin;
+    unsigned* amin_ticket;
+    ArgminArgs amin;
 };
 
 struct SelectArgs {                          // top-E of (cost, index) pairs, NaN last, ties -> lower index
@@ -76,27 +103,6 @@ struct RefitArgs {                           // per-(h, j) elite mean / std, smo
 };
 constexpr int kPolParams = 96;
 
-struct ArgminArgs {
-    const double* costs;
-    const double* act_out;   // [.][K][A] actions written by the rollout (policy mode) or nullptr
-    const double* actions;   // [H][K][A] or nullptr
-    const double* consts;
-    bcmpc_result* out;
-    uint64_t seed;
-    int64_t cand_offset;
-    int64_t K;
-    int32_t A;
-    int32_t maximize;        // np.argmax (learned reward, controllers.py:152) instead of np.argmin
-    // CEM: first action regenerated from the sampler; merge with the running best by stream position
-    const double* cem_mu;
-    const double* cem_sigma;
-    int32_t cem_iter;
-    int32_t merge;           // keep out's previous best unless strictly better (np.argmin over iterations)
-    int64_t pos_base;        // position of candidate 0 in the concatenated stream (iter * K_global + offset)
-    double* scratch_c;       // [kArgminParts] per-block best (argmin_partial -> argmin_final)
-    int64_t* scratch_i;
-    int32_t nparts;          // argmin_parts(K)
-};
 constexpr int kArgminParts = 256;
 int argmin_parts(int64_t K);
 

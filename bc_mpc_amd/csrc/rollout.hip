@@ -36,6 +36,7 @@
 #include "../../include/bcmpc.h"
 #include "kernels.h"
 #include "device_common.h"
+#include "argmin_common.h"
 
 namespace bcmpc {
 
@@ -359,28 +360,7 @@ __global__ __launch_bounds__(256) void argmin_final(const ArgminArgs a) {
         if (better(c, best)) best = c;
     }
     best = block_best(best, sc, si);
-    if (threadIdx.x == 0) {
-        bcmpc_result* out = a.out;
-        if (a.merge) {        // CEM: np.argmin over the iteration-major concatenation; keep the earlier best on ties
-            const double prev = out->best_cost;
-            const Best ex{a.maximize ? -prev : prev, out->best_index - a.pos_base};
-            if (!better(best, ex)) return;
-        }
-        out->best_index = (a.merge || a.cem_mu ? a.pos_base : a.cand_offset) + best.i;
-        out->best_cost = a.maximize ? -best.c : best.c;
-        for (int j = 0; j < BCMPC_MAX_ACTION; ++j) out->first_action[j] = 0.0;
-        if (best.i < a.K) {
-            const uint64_t g = (uint64_t)(a.cand_offset + best.i);
-            for (int j = 0; j < a.A; ++j) {
-                const double lo = a.consts[6 * 32 + j], hi = a.consts[7 * 32 + j];
-                out->first_action[j] =
-                    a.act_out ? a.act_out[best.i * a.A + j]     // policy-mixed actions (controllers.py:233-235)
-                    : a.cem_mu ? cem_action(a.seed, g, 0, j, a.cem_iter, a.cem_mu[j], a.cem_sigma[j], lo, hi)
-                    : a.actions ? a.actions[best.i * a.A + j]   // action_paths[0, i*, :] (controllers.py:84-85)
-                              : rng_action(a.seed, g, 0, j, lo, hi);
-            }
-        }
-    }
+    if (threadIdx.x == 0) argmin_write(a, best);
 }
 
 // ------------------------------------------------------------ launchers ----

@@ -45,6 +45,7 @@
 #include "../../include/bcmpc.h"
 #include "device_common.h"
 #include "kernels.h"
+#include "argmin_common.h"
 
 namespace bcmpc {
 
@@ -776,7 +777,8 @@ void rollout_x3(const RolloutArgs a) {
                 pact[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, uu[r]));
             }
             if (a.act_out && h < a.act_out_steps && valid)          // action_paths (controllers.py:213)
-                a.act_out[((int64_t)h * a.K + cand) * A + j] = pact[r];
+                __hip_atomic_store(&a.act_out[((int64_t)h * a.K + cand) * A + j], pact[r], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);       // (sc1: read by the fused argmin)
         }
     };
 
@@ -1144,10 +1146,70 @@ void rollout_x3(const RolloutArgs a) {
         }
     }
     // the cost holder: half 1, lane row 0 (cheetah) / the reward row's lanes (RW)
-    if (a.costs && valid && q == (RW ? (S & 15) >> 2 : 0) && (SO ? hv0 == 1 : true)) a.costs[cand] = cost;
+    const bool holder = valid && q == (RW ? (S & 15) >> 2 : 0) && (SO ? hv0 == 1 : true);
+    if (a.costs && holder) a.costs[cand] = cost;
     if constexpr (X3_STAMP) {
         if (a.stamps && lane == 0)
             for (int k = 0; k < 10; ++k) a.stamps[((size_t)blockIdx.x * NW + w) * 10 + k] = ph_[k];
+    }
+    if (a.fused_argmin) {
+        // ---- np.argmin / argmax (controllers.py:82,152) fused: this workgroup's best, then the
+        //      last workgroup to finish reduces every workgroup's record (ticket; the agent-scope
+        //      release / acquire recipe of cdna_hip_programming.md "In-launch split-K reduction") ----
+        const ArgminArgs& m = a.amin;
+        Best best{__builtin_inf(), INT64_MAX};
+        if (holder) best = Best{m.maximize ? -cost : cost, cand};
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const Best o{__shfl_xor(best.c, off), __shfl_xor(best.i, off)};
+            if (better(o, best)) best = o;
+        }
+        double* rc = reinterpret_cast<double*>(slab);          // (the slab is free after the last step)
+        int64_t* ri = reinterpret_cast<int64_t*>(rc + 16);
+        __syncthreads();
+        if (lane == 0) { rc[w] = best.c; ri[w] = best.i; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < NW; ++k) {
+                const Best o{rc[k], ri[k]};
+                if (better(o, best)) best = o;
+            }
+            // write-through (sc1) record stores need no release fence; the policy's act_out rows
+            // are stored the same way (cdna_hip_programming.md, in-launch reduction, sc1 form)
+            __hip_atomic_store(&m.scratch_c[blockIdx.x], best.c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&m.scratch_i[blockIdx.x], best.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned t = __hip_atomic_fetch_add(a.amin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = t == gridDim.x - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            ri[16] = last ? 1 : 0;
+        }
+        __syncthreads();
+        if (ri[16] == 0) return;
+        best = Best{__builtin_inf(), INT64_MAX};
+        for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+            const Best o{m.scratch_c[b], m.scratch_i[b]};
+            if (better(o, best)) best = o;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const Best o{__shfl_xor(best.c, off), __shfl_xor(best.i, off)};
+            if (better(o, best)) best = o;
+        }
+        __syncthreads();
+        if (lane == 0) { rc[w] = best.c; ri[w] = best.i; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < NW; ++k) {
+                const Best o{rc[k], ri[k]};
+                if (better(o, best)) best = o;
+            }
+            argmin_write(m, best);
+            *a.amin_ticket = 0;                        // ready for the next launch (stream order)
+        }
     }
 }
 
