@@ -460,3 +460,37 @@ def test_split_policy_shard_invariant():
     ra = half.get_action(state, None, seed=42, cand_offset=0, return_costs=True)
     rb = half.get_action(state, None, seed=42, cand_offset=K // 2, return_costs=True)
     assert np.array_equal(np.concatenate([ra.costs, rb.costs]), r1.costs)
+
+
+@pytest.mark.parametrize("model", ["delta", "policy", "reward"])
+def test_fused_argmin_tail_matches_launches(model, monkeypatch):
+    """BCMPC_FUSED_ARGMIN=1 (the split kernel reduces np.argmin in its own tail) returns exactly
+    what the two argmin launches return: index, cost, first action (policy: the mixed action)."""
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    K, H = 5000, 6
+    rew = model == "reward"
+    norm = orc.synthetic_normalization(20, 6, seed=5, reward=rew)
+    w = orc.synthetic_reward_weights(20, 6, 500, False, seed_base=9) if rew else orc.synthetic_weights(20, 6, 500, 2)
+    state = orc.synthetic_state(norm, seed=6)
+    expl = np.random.RandomState(8).uniform(-1, 1, (H, K, 6))
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("BCMPC_FUSED_ARGMIN", fused)
+        kw = dict(cost="reward", model="reward") if rew else {}
+        if model == "policy":
+            kw.update(policy_hidden=128, policy_layers=2)
+        e = RolloutEngine(20, 6, 500, 2, "tanh", False, H, K, precision="split", **kw)
+        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh", model="reward" if rew else "delta"), norm, 1)
+        if rew:
+            e.set_discount(0.99)
+        if model == "policy":
+            p = orc.synthetic_policy(20, 6, 128, 2)
+            e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.5, 1)
+        r1 = e.get_action(state, expl, return_costs=True)
+        r2 = e.get_action(state, None, seed=77, cand_offset=123, return_costs=True)   # device RNG, offset
+        out.append((r1, r2))
+        e.close()
+    for a, b in zip(out[0], out[1]):
+        assert a.best_index == b.best_index and a.best_cost == b.best_cost
+        assert np.array_equal(a.first_action, b.first_action) and np.array_equal(a.costs, b.costs)
