@@ -90,6 +90,79 @@ __global__ __launch_bounds__(256) void gemm_f32(const float* __restrict__ A, con
     }
 }
 
+// The same contract on the f32 matrix cores: one wave per 32 x 32 tile of C (2 x 2
+// v_mfma_f32_16x16x4_f32 tiles), operands straight from global memory (L1/L2-resident at
+// these sizes), K in steps of 4 with the next step's fragments in flight.  Fragment layouts:
+// A 16x4: lane l holds A[l&15][l>>4]; B 4x16: B[l>>4][l&15]; D 16x16: D[4(l>>4)+r][l&15].
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <bool TA, bool TB>
+__global__ __launch_bounds__(64) void gemm_mfma(const float* __restrict__ A, const float* __restrict__ B,
+                                                float* __restrict__ C, const float* __restrict__ bias, int M, int N,
+                                                int K, int lda, int ldb, int ldc, int kc) {
+    const int lane = threadIdx.x;
+    const int r16 = lane & 15, k4 = lane >> 4;
+    const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+    const int kb = blockIdx.z * kc, ke = kb + kc < K ? kb + kc : K;
+    auto lda_ = [&](int m, int k) -> float {
+        if (m >= M || k >= ke) return 0.f;
+        return TA ? A[(size_t)k * lda + m] : A[(size_t)m * lda + k];
+    };
+    auto ldb_ = [&](int k, int n) -> float {
+        if (n >= N || k >= ke) return 0.f;
+        return TB ? B[(size_t)n * ldb + k] : B[(size_t)k * ldb + n];
+    };
+    f4v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f4v){0.f, 0.f, 0.f, 0.f};
+    // K in chunks of 8 steps (32): the next chunk's 32 fragments are loaded while this one's
+    // 32 MFMAs run (one global-load latency per chunk, not per step)
+    constexpr int CH = 8;
+    float a0[CH], a1[CH], b0[CH], b1[CH];
+    auto load = [&](int k) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+            const int kk = k + 4 * s + k4;
+            a0[s] = lda_(m0 + r16, kk);
+            a1[s] = lda_(m0 + 16 + r16, kk);
+            b0[s] = ldb_(kk, n0 + r16);
+            b1[s] = ldb_(kk, n0 + 16 + r16);
+        }
+    };
+    load(kb);
+    for (int k = kb; k < ke; k += 4 * CH) {
+        float c0[CH], c1[CH], d0[CH], d1[CH];
+#pragma unroll
+        for (int s = 0; s < CH; ++s) { c0[s] = a0[s]; c1[s] = a1[s]; d0[s] = b0[s]; d1[s] = b1[s]; }
+        if (k + 4 * CH < ke) load(k + 4 * CH);
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+            acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(c0[s], d0[s], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(c0[s], d1[s], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(c1[s], d0[s], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(c1[s], d1[s], acc[1][1], 0, 0, 0);
+        }
+    }
+    float* Cz = C + (size_t)blockIdx.z * M * ldc;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + 16 * j + r16;
+            if (n >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + 16 * i + 4 * k4 + r;
+                if (m < M) Cz[(size_t)m * ldc + n] = (bias && gridDim.z == 1) ? acc[i][j][r] + bias[n] : acc[i][j][r];
+            }
+        }
+}
+
+#ifndef FIT_MFMA
+#define FIT_MFMA 1
+#endif
+
 __global__ void gemm_reduce(const float* __restrict__ part, float* __restrict__ C, const float* __restrict__ bias,
                             int M, int N, int ldc, int nz) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -110,8 +183,12 @@ static hipError_t gemm(const float* A, const float* B, float* C, const float* bi
         while (nz < 8 && tiles * nz < 256 && K / (nz * 2) >= 64 && (size_t)nz * 2 * M * ldc <= scratch_floats) nz *= 2;
     const int kc = ((K + nz - 1) / nz + 31) / 32 * 32;
     dim3 grid((N + 31) / 32, (M + 31) / 32, nz);
-    hipLaunchKernelGGL((gemm_f32<TA, TB>), grid, dim3(256), 0, st, A, B, nz > 1 ? scratch : C, bias, M, N, K, lda,
-                       ldb, ldc, kc);
+    if (FIT_MFMA)
+        hipLaunchKernelGGL((gemm_mfma<TA, TB>), grid, dim3(64), 0, st, A, B, nz > 1 ? scratch : C, bias, M, N, K,
+                           lda, ldb, ldc, kc);
+    else
+        hipLaunchKernelGGL((gemm_f32<TA, TB>), grid, dim3(256), 0, st, A, B, nz > 1 ? scratch : C, bias, M, N, K,
+                           lda, ldb, ldc, kc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nz == 1) return e;
     hipLaunchKernelGGL(gemm_reduce, dim3((M * N + 255) / 256), dim3(256), 0, st, scratch, C, bias, M, N, ldc, nz);
@@ -242,17 +319,17 @@ __global__ __launch_bounds__(256) void fit_colsum(const float* __restrict__ X, f
     p1[g][c] = s;
     p2[g][c] = s2;
     __syncthreads();
-    if (g == 0 && f < F) {
-        part[(size_t)chunk * 2 * F + f] = p1[0][c] + p1[1][c] + p1[2][c] + p1[3][c];
-        part[(size_t)chunk * 2 * F + F + f] = p2[0][c] + p2[1][c] + p2[2][c] + p2[3][c];
+    if (g == 0 && f < F) {      // write-through (sc1) partials: no release fence needed
+        __hip_atomic_store(&part[(size_t)chunk * 2 * F + f], p1[0][c] + p1[1][c] + p1[2][c] + p1[3][c],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&part[(size_t)chunk * 2 * F + F + f], p2[0][c] + p2[1][c] + p2[2][c] + p2[3][c],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // publish (agent-scope release once per block, then the ticket; cdna_hip_programming.md
-    // "In-launch split-K reduction"): correct for any spread of the chunks over XCDs
+    // publish: stores complete, then the ticket (cdna_hip_programming.md "In-launch split-K
+    // reduction", sc1 form); correct for any spread of the chunks over XCDs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned t = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         p1[0][0] = t == (unsigned)nchunk - 1 ? 1.f : 0.f;     // "last" through the existing LDS array
         if (t == (unsigned)nchunk - 1) {
@@ -277,8 +354,10 @@ __global__ __launch_bounds__(256) void fit_colsum(const float* __restrict__ X, f
 // loss = mean((T - P)^2) (one block), dP = -((2 * (1/N)) * (T - P))
 __global__ __launch_bounds__(1024) void fit_loss(const float* __restrict__ P, const float* __restrict__ T,
                                                  float* __restrict__ dP, float* __restrict__ loss_base,
-                                                 const int32_t* __restrict__ iter, int n) {
-    float* loss = loss_base + *iter;
+                                                 int32_t* __restrict__ iter, float* __restrict__ bp, float b1,
+                                                 float b2, int n) {
+    const int it = *iter;
+    float* loss = loss_base + it;
     __shared__ float red[16];
     const float inv = 1.0f / (float)n;
     float s = 0.f;
@@ -294,6 +373,13 @@ __global__ __launch_bounds__(1024) void fit_loss(const float* __restrict__ P, co
         float t = 0.f;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
         *loss = t * inv;
+        // the previous iteration's end (TF1 _finish: beta powers *= beta), then the counter;
+        // the iteration's Adam (after this kernel) reads bp = beta^(it+1)
+        if (it > 0) {
+            bp[0] = __fmul_rn(bp[0], b1);
+            bp[1] = __fmul_rn(bp[1], b2);
+        }
+        *iter = it + 1;
     }
 }
 
@@ -313,14 +399,6 @@ __global__ void fit_adam(float* __restrict__ w, float* __restrict__ m, float* __
     w[i] = w[i] - (mi * lr_t) / (sqrtf(vi) + eps);
 }
 
-// end of an iteration: beta powers *= beta (TF1 _finish), iteration counter + 1
-__global__ void fit_step_end(int32_t* __restrict__ iter, float* __restrict__ bp, float b1, float b2) {
-    if (threadIdx.x == 0) {
-        bp[0] = __fmul_rn(bp[0], b1);
-        bp[1] = __fmul_rn(bp[1], b2);
-        *iter += 1;
-    }
-}
 
 }  // namespace bcmpc
 
@@ -543,7 +621,8 @@ static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int stride, int 
     }
     const float* HL = ln ? f->d_hln + (L - 1) * BH : f->d_act + (L - 1) * BH;
     FIT_TRY((gemm<false, false>(HL, W + f->w_off[L], f->d_p, W + f->b_off[L], B, S, h, h, S, S, st)));
-    hipLaunchKernelGGL(fit_loss, dim3(1), dim3(1024), 0, st, f->d_p, f->d_t, f->d_dp, d_loss, f->d_iter, B * S);
+    hipLaunchKernelGGL(fit_loss, dim3(1), dim3(1024), 0, st, f->d_p, f->d_t, f->d_dp, d_loss, f->d_iter, f->d_bp,
+                       f->cfg.beta1, f->cfg.beta2, B * S);
     FIT_TRY(hipGetLastError());
     // ---- backward ----
     // output layer: dW_L = H_L^T dP, db_L = colsum dP, dH = dP W_L^T
@@ -579,8 +658,7 @@ static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int stride, int 
     hipLaunchKernelGGL(fit_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, f->d_m, f->d_v, G, n,
                        f->d_bp, f->cfg.learning_rate, b1, b2, f->cfg.epsilon);
     FIT_TRY(hipGetLastError());
-    hipLaunchKernelGGL(fit_step_end, dim3(1), dim3(64), 0, st, f->d_iter, f->d_bp, b1, b2);
-    FIT_TRY(hipGetLastError());
+
 #undef FIT_TRY
     return BCMPC_OK;
 }
