@@ -265,9 +265,14 @@ __device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, in
 // other wave: bar() (the "layer input complete" barrier) runs after their MFMAs are
 // issued, overlapping them with the slower waves' epilogues.  (A wave reads its own
 // LDS writes in program order: no barrier.)
-template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, typename Bar = void (*)()>
+struct NoWait {
+    __device__ void operator()(int) const {}
+};
+// wt(p): called before the slab's k-step p is first read (X3_FLAGS: wait for its producer)
+template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, typename Bar = void (*)(), typename Wt = NoWait>
 __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
-                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr) {
+                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr,
+                                      Wt wt = {}) {
     constexpr int NG = TW / G;
     static_assert(NG * G == TW && (NG == 1 || NG == 2), "one or two units per k-step");
     static_assert((P * NG) % 2 == 0, "ping-pong over unit pairs");
@@ -338,18 +343,26 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     for (int u = NOWN; u < NU - 2; u += 2) {
         aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
         __builtin_amdgcn_sched_barrier(0);          // keep the loads ahead of the MFMAs they overlap
+        wt(kstep(u));
         bread_x3<NC>(slab, kstep(u), lane, bh, bl);
         unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
         aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NG == 1) bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
+        if constexpr (NG == 1) {
+            wt(kstep(u + 1));
+            bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
+        }
         unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
     }
     aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
     __builtin_amdgcn_sched_barrier(0);
+    wt(kstep(NU - 2));
     bread_x3<NC>(slab, kstep(NU - 2), lane, bh, bl);
     unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-    if constexpr (NG == 1) bread_x3<NC>(slab, kstep(NU - 1), lane, bh, bl);
+    if constexpr (NG == 1) {
+        wt(kstep(NU - 1));
+        bread_x3<NC>(slab, kstep(NU - 1), lane, bh, bl);
+    }
     unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
 }
 
@@ -458,6 +471,10 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
 #ifndef X3_PRIO                  // 1: s_setprio 1 for the second-dispatched half of the waves
 #define X3_PRIO 0
 #endif
+#ifndef X3_FLAGS                 // hidden-layer input hand-off by per-wave LDS flags instead of a barrier
+#define X3_FLAGS 0                // (measured 1.3% slower at cfg3: the polls cost more than the barrier skew they save)
+#endif
+static_assert(!X3_FLAGS || (!X3_BROLL && !X3_BSTREAM && !X3_HALF), "the flag hand-off waits in the plain slab loop only");
 #ifndef X3_STAGGER               // diagnostic: odd workgroups start X3_STAGGER x 8k cycles late
 #define X3_STAGGER 0
 #endif
@@ -485,7 +502,7 @@ __host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
 // X3_NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab P*NC*2 KiB
 __host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
 __host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, int PL = 0, int PHP = 0) {
-    return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
+    return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + 64 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
            NC * 2048 + (HP / 32) * NC * 2048;
 }
 
@@ -546,7 +563,8 @@ void rollout_x3(const RolloutArgs a) {
                                            pol_param_bytes(PHP > 0 ? PL : 0, PHP));
     float* colmax = colf + NC * 16;                     // [half][NC*16]: per-half column max (split owners)
     int* penbuf = reinterpret_cast<int*>(colmax + 2 * NC * 16);   // [step & 1][NC*16] penalty counts
-    float* xa = reinterpret_cast<float*>(penbuf + 2 * NC * 16);   // [X3_NCH][CB][A] normalised action inputs
+    int* flg = penbuf + 2 * NC * 16;                    // [16] per-wave hand-off flags (X3_FLAGS)
+    float* xa = reinterpret_cast<float*>(flg + 16);     // [X3_NCH][CB][A] normalised action inputs
     f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)));
     f4* slab = slab0 + NC * 2 * 64;
     __syncthreads();
@@ -595,7 +613,31 @@ void rollout_x3(const RolloutArgs a) {
         }
     };
     if constexpr (PHP == 0) fill_actions(0, 64 * NW);
+    for (int i = threadIdx.x; i < 16; i += blockDim.x) flg[i] = 0;
     __syncthreads();
+    // X3_FLAGS: wave w's k-steps [w*PW, (w+1)*PW) of hidden layer l's input at step h are in the
+    // slab once flg[w] >= h*L + l (monotonic: no reset).  publish(): LDS writes complete
+    // (workgroup release), then the flag; wait_for(p): the producer of k-step p, polled
+    // (bounded: a missing flag cannot hang the kernel, it would only read stale rows)
+    auto publish = [&](int val) __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&flg[w], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    struct FlagWait {
+        const int* f;
+        int want, self, pw;
+        __device__ void operator()(int p) const {
+            if (p % pw != 0 || p / pw == self) return;
+            const int* q = f + p / pw;
+            for (int n = 0; n < (1 << 22); ++n) {
+                const int v = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (v >= want) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+    };
     const int voff = lane * 16;
     const int kown = X3_OWN ? w * PW : 0;               // first k-step of this wave's hidden-layer sweep
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
@@ -920,9 +962,17 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
             {
-                auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // trunk output complete
-                mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab, acc,
-                                                     lane, uh, ul, kown, ready);
+                auto ready = [&]() __attribute__((always_inline)) {  // trunk output complete
+                    if constexpr (!X3_FLAGS) X3_BARRIER_ID(3);
+                };
+                if constexpr (X3_FLAGS) {
+                    publish(h + 1);
+                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab,
+                                                         acc, lane, uh, ul, kown, ready, FlagWait{flg, h + 1, w, PW});
+                } else {
+                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab,
+                                                         acc, lane, uh, ul, kown, ready);
+                }
                 if constexpr (!X3_OWN) ready();
             }
             aload_x3<G>(layer_rsrc(a.w[1], a.wbytes[1]), voff, w * P * TW * 2048, uh, ul);   // delta head unit 0
@@ -976,7 +1026,11 @@ void rollout_x3(const RolloutArgs a) {
                     swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
                     swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
-            auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // layer input complete
+            auto ready = [&]() __attribute__((always_inline)) {      // layer input complete
+                if constexpr (!X3_FLAGS) X3_BARRIER_ID(3);
+            };
+            if constexpr (X3_FLAGS) publish(h * L + l);
+            const FlagWait fw{flg, h * L + l, w, PW};
             X3_ST(4);
 #pragma unroll
             for (int j = 0; j < TW; ++j)
@@ -1011,8 +1065,12 @@ void rollout_x3(const RolloutArgs a) {
                                  xl[pp][c]);
             } else {
                 // own k-steps first: this wave's slab writes need no barrier
-                mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc,
-                                                     lane, uh, ul, kown, ready);
+                if constexpr (X3_FLAGS)
+                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab,
+                                                         acc, lane, uh, ul, kown, ready, fw);
+                else
+                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab,
+                                                         acc, lane, uh, ul, kown, ready);
                 if constexpr (!X3_OWN) ready();
                 X3_ST(5);
                 load_next(l + 1);
