@@ -204,30 +204,6 @@ __device__ __forceinline__ void unit_x3s(const h8 (&ah)[G], const h8 (&al)[G], c
 #ifndef X3_BSTREAM
 #define X3_BSTREAM 0
 #endif
-#ifndef X3_BROLL                 // B fragments of the next k-step read column by column as the current
-#define X3_BROLL 0               // unit's MFMAs release them (measured 3% slower at cfg3)
-#endif
-
-// unit_x3 with a rolling B prefetch: once column c's three passes are issued, its B
-// registers are reloaded with column c of k-step knext (NEXT)
-template <int TW, int NC, int G, bool NEXT>
-__device__ __forceinline__ void unit_x3r(const h8 (&ah)[G], const h8 (&al)[G], h8 (&bh)[NC], h8 (&bl)[NC], int g,
-                                         f4 (&acc)[TW][NC], const f4* slab, int knext, int lane) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-#pragma unroll
-        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bh[c], acc[g * G + j][c]);
-#pragma unroll
-        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bl[c], acc[g * G + j][c]);
-#pragma unroll
-        for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(al[j], bh[c], acc[g * G + j][c]);
-        if constexpr (NEXT) {
-            bh[c] = sread(slab + sidx<NC>(knext, c, 0, lane));
-            bl[c] = sread(slab + sidx<NC>(knext, c, 1, lane));
-        }
-    }
-}
-
 template <int NC>
 __device__ __forceinline__ void bread_x3(const f4* slab, int p, int lane, h8 (&bh)[NC], h8 (&bl)[NC]) {
 #pragma unroll
@@ -265,14 +241,9 @@ __device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, in
 // other wave: bar() (the "layer input complete" barrier) runs after their MFMAs are
 // issued, overlapping them with the slower waves' epilogues.  (A wave reads its own
 // LDS writes in program order: no barrier.)
-struct NoWait {
-    __device__ void operator()(int) const {}
-};
-// wt(p): called before the slab's k-step p is first read (X3_FLAGS: wait for its producer)
-template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, typename Bar = void (*)(), typename Wt = NoWait>
+template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, typename Bar = void (*)()>
 __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
-                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr,
-                                      Wt wt = {}) {
+                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr) {
     constexpr int NG = TW / G;
     static_assert(NG * G == TW && (NG == 1 || NG == 2), "one or two units per k-step");
     static_assert((P * NG) % 2 == 0, "ping-pong over unit pairs");
@@ -305,23 +276,6 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
         }
         bar();
     }
-    if constexpr (NG == 1 && X3_BROLL) {
-        // (OWN: the own units above read their own B; the rolling chain starts after bar())
-        bread_x3<NC>(slab, kstep(NOWN), lane, bh, bl);
-        for (int u = NOWN; u < NU - 2; u += 2) {
-            aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
-            __builtin_amdgcn_sched_barrier(0);
-            unit_x3r<TW, NC, G, true>(s0h, s0l, bh, bl, 0, acc, slab, kstep(u + 1), lane);
-            aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
-            __builtin_amdgcn_sched_barrier(0);
-            unit_x3r<TW, NC, G, true>(s1h, s1l, bh, bl, 0, acc, slab, kstep(u + 2), lane);
-        }
-        aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
-        __builtin_amdgcn_sched_barrier(0);
-        unit_x3r<TW, NC, G, true>(s0h, s0l, bh, bl, 0, acc, slab, kstep(NU - 1), lane);
-        unit_x3r<TW, NC, G, false>(s1h, s1l, bh, bl, 0, acc, slab, 0, lane);
-        return;
-    }
     // (the last pair is peeled so that every load in the loop is unconditional: a
     // conditional load would make the compiler drain vmcnt to 0 at the merge)
     if constexpr (NG == 1 && X3_BSTREAM && !OWN) {
@@ -343,86 +297,19 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     for (int u = NOWN; u < NU - 2; u += 2) {
         aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
         __builtin_amdgcn_sched_barrier(0);          // keep the loads ahead of the MFMAs they overlap
-        wt(kstep(u));
         bread_x3<NC>(slab, kstep(u), lane, bh, bl);
         unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
         aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NG == 1) {
-            wt(kstep(u + 1));
-            bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
-        }
+        if constexpr (NG == 1) bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
         unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
     }
     aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
     __builtin_amdgcn_sched_barrier(0);
-    wt(kstep(NU - 2));
     bread_x3<NC>(slab, kstep(NU - 2), lane, bh, bl);
     unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-    if constexpr (NG == 1) {
-        wt(kstep(NU - 1));
-        bread_x3<NC>(slab, kstep(NU - 1), lane, bh, bl);
-    }
+    if constexpr (NG == 1) bread_x3<NC>(slab, kstep(NU - 1), lane, bh, bl);
     unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
-}
-
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
-// A hidden layer in two tile halves (X3_HALF): half 0 (tiles [0, TW/2)) over all k-steps,
-// then half 1 with epi(n) -- half 0's epilogue, the caller's VALU -- issued after each of
-// its unit pairs n, so that the tanh / split work runs under this wave's own MFMAs instead
-// of after them.  Units are (half, k-step) with G = TW/2 tiles; k-steps in the rotated
-// order k0, k0+1, ... (mod P), the first PW of half 0 from the wave's own slab rows before
-// bar() (see mm_x3).  Every k-step's B fragments are read once per half.
-template <int TW, int NC, int P, int PW, bool OWN, typename Bar, typename Epi>
-__device__ __forceinline__ void mm_x3h(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
-                                       int lane, h8 (&s0h)[TW / 2], h8 (&s0l)[TW / 2], int k0, Bar bar, Epi epi) {
-    constexpr int G = TW / 2;
-    constexpr int STEPB = TW * 2048;
-    constexpr int NOWN = OWN ? PW : 0;
-    static_assert(P % 2 == 0 && NOWN % 2 == 0 && NOWN < P, "unit pairs");
-    const int voff = lane * 16;
-    auto kstep = [&](int i) {
-        const int p = i + k0;
-        return p >= P ? p - P : p;
-    };
-    auto uoff = [&](int u) {
-        const int half = u >= P ? 1 : 0;
-        return wbase + kstep(u - half * P) * STEPB + half * G * 2048;
-    };
-    h8 s1h[G], s1l[G], bh[NC], bl[NC];
-    auto pair0 = [&](int u) __attribute__((always_inline)) {     // half-0 units u, u+1
-        aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
-        __builtin_amdgcn_sched_barrier(0);
-        bread_x3<NC>(slab, kstep(u), lane, bh, bl);
-        unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-        aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
-        __builtin_amdgcn_sched_barrier(0);
-        bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
-        unit_x3<TW, NC, G>(s1h, s1l, bh, bl, 0, acc);
-    };
-#pragma unroll
-    for (int u = 0; u < NOWN; u += 2) pair0(u);
-    if constexpr (OWN) bar();
-    for (int u = NOWN; u < P; u += 2) pair0(u);
-    static_for<0, P / 2>([&](auto nn) __attribute__((always_inline)) {
-        constexpr int n = decltype(nn)::value;
-        aload_x3<G>(rs, voff, uoff(P + 2 * n + 1), s1h, s1l, true);
-        __builtin_amdgcn_sched_barrier(0);
-        bread_x3<NC>(slab, kstep(2 * n), lane, bh, bl);
-        unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 1, acc);
-        if constexpr (2 * n + 2 < P) aload_x3<G>(rs, voff, uoff(P + 2 * n + 2), s0h, s0l, true);
-        __builtin_amdgcn_sched_barrier(0);
-        bread_x3<NC>(slab, kstep(2 * n + 1), lane, bh, bl);
-        unit_x3<TW, NC, G>(s1h, s1l, bh, bl, 1, acc);
-        epi(nn);
-    });
 }
 
 // Epilogue of one tile pair (k-step) for one column: BiasAdd (f32, after undoing
@@ -465,24 +352,14 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
 #ifndef X3_ONLY_NC
 #define X3_ONLY_NC 4
 #endif
-#ifndef X3_HALF                  // hidden layers in two tile halves, half 0's epilogue under half 1's MFMAs
-#define X3_HALF 0                // (measured 8% slower at cfg3: every k-step's B read twice, half-size units)
-#endif
 #ifndef X3_PRIO                  // 1: s_setprio 1 for the second-dispatched half of the waves
 #define X3_PRIO 0
 #endif
-#ifndef X3_FLAGS                 // hidden-layer input hand-off by per-wave LDS flags instead of a barrier
-#define X3_FLAGS 0                // (measured 1.3% slower at cfg3: the polls cost more than the barrier skew they save)
-#endif
-static_assert(!X3_FLAGS || (!X3_BROLL && !X3_BSTREAM && !X3_HALF), "the flag hand-off waits in the plain slab loop only");
 #ifndef X3_STAGGER               // diagnostic: odd workgroups start X3_STAGGER x 8k cycles late
 #define X3_STAGGER 0
 #endif
-// hidden layers split into tile halves where each half holds whole tile pairs
-__host__ __device__ constexpr bool x3_half(int TW) { return X3_HALF && TW % 4 == 0; }
 // tiles per streamed operand unit: a whole k-step up to 4 tiles per wave, else half
-// (a tile half with X3_HALF)
-__host__ __device__ constexpr int x3_group(int TW) { return x3_half(TW) ? TW / 2 : TW <= 4 ? TW : TW / 2; }
+__host__ __device__ constexpr int x3_group(int TW) { return TW <= 4 ? TW : TW / 2; }
 
 #ifndef X3_OWN                   // hidden layers start with the k-steps the wave produced itself
 #define X3_OWN 1
@@ -502,7 +379,7 @@ __host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
 // X3_NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab P*NC*2 KiB
 __host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
 __host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, int PL = 0, int PHP = 0) {
-    return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + 64 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
+    return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
            NC * 2048 + (HP / 32) * NC * 2048;
 }
 
@@ -563,8 +440,7 @@ void rollout_x3(const RolloutArgs a) {
                                            pol_param_bytes(PHP > 0 ? PL : 0, PHP));
     float* colmax = colf + NC * 16;                     // [half][NC*16]: per-half column max (split owners)
     int* penbuf = reinterpret_cast<int*>(colmax + 2 * NC * 16);   // [step & 1][NC*16] penalty counts
-    int* flg = penbuf + 2 * NC * 16;                    // [16] per-wave hand-off flags (X3_FLAGS)
-    float* xa = reinterpret_cast<float*>(flg + 16);     // [X3_NCH][CB][A] normalised action inputs
+    float* xa = reinterpret_cast<float*>(penbuf + 2 * NC * 16);   // [X3_NCH][CB][A] normalised action inputs
     f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)));
     f4* slab = slab0 + NC * 2 * 64;
     __syncthreads();
@@ -613,31 +489,7 @@ void rollout_x3(const RolloutArgs a) {
         }
     };
     if constexpr (PHP == 0) fill_actions(0, 64 * NW);
-    for (int i = threadIdx.x; i < 16; i += blockDim.x) flg[i] = 0;
     __syncthreads();
-    // X3_FLAGS: wave w's k-steps [w*PW, (w+1)*PW) of hidden layer l's input at step h are in the
-    // slab once flg[w] >= h*L + l (monotonic: no reset).  publish(): LDS writes complete
-    // (workgroup release), then the flag; wait_for(p): the producer of k-step p, polled
-    // (bounded: a missing flag cannot hang the kernel, it would only read stale rows)
-    auto publish = [&](int val) __attribute__((always_inline)) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&flg[w], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    struct FlagWait {
-        const int* f;
-        int want, self, pw;
-        __device__ void operator()(int p) const {
-            if (p % pw != 0 || p / pw == self) return;
-            const int* q = f + p / pw;
-            for (int n = 0; n < (1 << 22); ++n) {
-                const int v = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (v >= want) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
-    };
     const int voff = lane * 16;
     const int kown = X3_OWN ? w * PW : 0;               // first k-step of this wave's hidden-layer sweep
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
@@ -962,17 +814,9 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
             {
-                auto ready = [&]() __attribute__((always_inline)) {  // trunk output complete
-                    if constexpr (!X3_FLAGS) X3_BARRIER_ID(3);
-                };
-                if constexpr (X3_FLAGS) {
-                    publish(h + 1);
-                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab,
-                                                         acc, lane, uh, ul, kown, ready, FlagWait{flg, h + 1, w, PW});
-                } else {
-                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab,
-                                                         acc, lane, uh, ul, kown, ready);
-                }
+                auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // trunk output complete
+                mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[3], a.wbytes[3]), w * P * TW * 2048, slab, acc,
+                                                     lane, uh, ul, kown, ready);
                 if constexpr (!X3_OWN) ready();
             }
             aload_x3<G>(layer_rsrc(a.w[1], a.wbytes[1]), voff, w * P * TW * 2048, uh, ul);   // delta head unit 0
@@ -1026,61 +870,25 @@ void rollout_x3(const RolloutArgs a) {
                     swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
                     swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
-            auto ready = [&]() __attribute__((always_inline)) {      // layer input complete
-                if constexpr (!X3_FLAGS) X3_BARRIER_ID(3);
-            };
-            if constexpr (X3_FLAGS) publish(h * L + l);
-            const FlagWait fw{flg, h * L + l, w, PW};
+            auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // layer input complete
             X3_ST(4);
 #pragma unroll
             for (int j = 0; j < TW; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
             const float f = a.winv[l] * kTanhK;
-            if constexpr (x3_half(TW)) {
-                // half 0's epilogue (PW/2 tile pairs x NC columns) spread over half 1's unit pairs
-                constexpr int NJ = PW / 2 * NC, NP = P / 2;
-                auto epi0 = [&](auto nn) __attribute__((always_inline)) {
-                    constexpr int n = decltype(nn)::value;
-                    static_for<0, NJ>([&](auto jj) __attribute__((always_inline)) {
-                        constexpr int j = decltype(jj)::value;
-                        constexpr int at = NJ < NP ? 1 + j * (NP - 1) / NJ : j * NP / NJ;
-                        if constexpr (at == n) {
-                            constexpr int pp = j / NC, c = j % NC;
-                            epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q,
-                                     xh[pp][c], xl[pp][c]);
-                        }
-                    });
-                };
-                mm_x3h<TW, NC, P, PW, X3_OWN != 0>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc,
-                                                   lane, uh, ul, kown, ready, epi0);
-                if constexpr (!X3_OWN) ready();
-                X3_ST(5);
-                load_next(l + 1);
+            // own k-steps first: this wave's slab writes need no barrier
+            mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane,
+                                                 uh, ul, kown, ready);
+            if constexpr (!X3_OWN) ready();
+            X3_ST(5);
+            load_next(l + 1);
 #pragma unroll
-                for (int pp = PW / 2; pp < PW; ++pp)
+            for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
-                    for (int c = 0; c < NC; ++c)
-                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
-                                 xl[pp][c]);
-            } else {
-                // own k-steps first: this wave's slab writes need no barrier
-                if constexpr (X3_FLAGS)
-                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab,
-                                                         acc, lane, uh, ul, kown, ready, fw);
-                else
-                    mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab,
-                                                         acc, lane, uh, ul, kown, ready);
-                if constexpr (!X3_OWN) ready();
-                X3_ST(5);
-                load_next(l + 1);
-#pragma unroll
-                for (int pp = 0; pp < PW; ++pp)
-#pragma unroll
-                    for (int c = 0; c < NC; ++c)
-                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
-                                 xl[pp][c]);
-            }
+                for (int c = 0; c < NC; ++c)
+                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
+                             xl[pp][c]);
         }
         X3_ST(6);
 
