@@ -164,14 +164,33 @@ class MPCcontroller(Controller):
         if not fused and self.rng != "numpy":
             raise ValueError("a non-cheetah cost_fn needs rng='numpy' (actions must exist on the host)")
 
+        if K == 0:                                          # (the reference draws before failing)
+            if self.rng == "numpy":
+                self.sample_random_actions()
+            else:
+                self._next_seed()
+            raise ValueError("attempt to get argmin of an empty sequence")
+        # the reference's draw, made by the library straight into pinned memory and uploaded step
+        # by step (same values, same stream advance) unless sample_random_actions is overridden
+        if (self.rng == "numpy" and fused and hi > lo and "sample_random_actions" not in self.__dict__
+                and type(self).sample_random_actions is MPCcontroller.sample_random_actions):
+            eng = self._engine_for(spec, S, A, hi - lo, fused)
+            eng.set_weights(spec, norm, version)
+            res = eng.get_action_numpy_stream(state, self.env.action_space.low, self.env.action_space.high, K, lo,
+                                              return_costs=self.keep_costs)
+            if res is not None:
+                self.last_costs = res.costs
+                cost, index, first_g = _dist.allgather_minloc(True, res.best_cost, res.best_index, res.first_action,
+                                                              A, self._group)
+                self.last_cost, self.last_index = cost, index
+                return first_g                               # = action_paths[0, index] (controllers.py:84-85)
+
         action_paths = None
         seed = 0
         if self.rng == "numpy":
             action_paths = self.sample_random_actions()      # every rank draws the full [H, K, A]
         else:
             seed = self._next_seed()
-        if K == 0:
-            raise ValueError("attempt to get argmin of an empty sequence")
 
         valid, cost, index, first = False, float("inf"), -1, None
         if hi > lo:

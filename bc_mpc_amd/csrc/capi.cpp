@@ -12,6 +12,7 @@
 
 #include "../../include/bcmpc.h"
 #include "kernels.h"
+#include "mt19937.h"
 
 using namespace bcmpc;
 
@@ -128,6 +129,7 @@ struct bcmpc_engine {
     double* d_consts = nullptr;
     double* d_state = nullptr;
     double* d_actions = nullptr; size_t actions_cap = 0;
+    double* h_stage = nullptr; size_t stage_cap = 0;   // pinned [H, K, A] staging (bcmpc_get_action_mt19937)
     double* d_costs = nullptr;
     bcmpc_result* d_result = nullptr;
     double* d_amin_c = nullptr;         // argmin scratch: per-block best
@@ -381,6 +383,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
                     (void*)e->d_amin_ticket})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -824,6 +827,70 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
         HIP_TRY(hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     *out = *e->h_result;
+    return BCMPC_OK;
+}
+
+int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_key, int32_t* mt_pos,
+                             const double* low, const double* high, int64_t k_global, int64_t cand_offset,
+                             bcmpc_result* out, double* costs_out) {
+    if (!e || !state || !mt_key || !mt_pos || !low || !high || !out) return fail(BCMPC_ERR_ARG, "null argument");
+    const bcmpc_config& c = e->cfg;
+    if (c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "get_action needs a fused objective (cheetah cost or learned reward)");
+    if (k_global < c.num_paths || cand_offset < 0 || cand_offset + c.num_paths > k_global)
+        return fail(BCMPC_ERR_ARG, "this engine's candidates must lie inside [0, k_global)");
+    if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
+    HIP_TRY(hipSetDevice(c.device));
+    const int64_t K = c.num_paths;
+    const int A = c.action_dim, H = c.horizon;
+    const size_t row = (size_t)K * A, n = (size_t)H * row;
+    if (n > e->actions_cap) {
+        if (e->d_actions) (void)hipFree(e->d_actions);
+        e->d_actions = nullptr;
+        e->actions_cap = 0;
+        HIP_TRY(hipMalloc(&e->d_actions, n * sizeof(double)));
+        e->actions_cap = n;
+    }
+    if (n > e->stage_cap) {                       // pinned staging: the generator writes, the DMA reads
+        if (e->h_stage) (void)hipHostFree(e->h_stage);
+        e->h_stage = nullptr;
+        e->stage_cap = 0;
+        HIP_TRY(hipHostMalloc(&e->h_stage, n * sizeof(double), hipHostMallocDefault));
+        e->stage_cap = n;
+    }
+    HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
+    Mt19937 g;
+    std::memcpy(g.key, mt_key, sizeof(g.key));
+    g.pos = *mt_pos;
+    // [H, k_global, A] in C order, one step at a time: step h's slice of this shard is copied
+    // while step h+1 is drawn (the earlier copies overlap the generator)
+    for (int h = 0; h < H; ++h) {
+        mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_stage + h * row);
+        HIP_TRY(hipMemcpyAsync(e->d_actions + h * row, e->h_stage + h * row, row * sizeof(double),
+                               hipMemcpyHostToDevice, e->stream));
+    }
+    std::memcpy(mt_key, g.key, sizeof(g.key));
+    *mt_pos = g.pos;
+    int rc = rollout_impl(e, e->d_state, 0, e->d_actions, 0, cand_offset, e->d_costs, nullptr, e->d_result, e->stream);
+    if (rc != BCMPC_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream));
+    if (costs_out)
+        HIP_TRY(hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * K, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));   // (also: the staging buffer is free again)
+    *out = *e->h_result;
+    return BCMPC_OK;
+}
+
+int bcmpc_mt19937_uniform(uint32_t* mt_key, int32_t* mt_pos, const double* low, const double* high,
+                          int32_t action_dim, int64_t n_rows, double* out) {
+    if (!mt_key || !mt_pos || !low || !high || !out || action_dim < 1 || n_rows < 0)
+        return fail(BCMPC_ERR_ARG, "bad argument");
+    if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
+    Mt19937 g;
+    std::memcpy(g.key, mt_key, sizeof(g.key));
+    g.pos = *mt_pos;
+    mt_uniform_rows(g, low, high, action_dim, n_rows, 0, n_rows, out);
+    std::memcpy(mt_key, g.key, sizeof(g.key));
+    *mt_pos = g.pos;
     return BCMPC_OK;
 }
 

@@ -1,0 +1,56 @@
+// mt19937.h -- the legacy NumPy global generator on the host (internal to libbcmpc).
+//
+// MPCcontroller.sample_random_actions (controllers.py:43-55) draws
+// np.random.uniform(low, high, [H, K, A]) from NumPy's legacy RandomState:
+// MT19937 (Matsumoto & Nishimura 1998; NumPy's randomkit twist, mt19937.c) and
+// random_sample = ((w1 >> 5) * 2^26 + (w2 >> 6)) / 2^53 from two tempered words,
+// then uniform = low + (high - low) * d in f64 (mul, then add: no FMA).  This
+// restatement continues the stream from NumPy's own state (np.random.get_state())
+// and returns the advanced state, so the caller's global stream moves exactly as
+// one np.random.uniform call would move it.
+#pragma once
+#include <stdint.h>
+
+namespace bcmpc {
+
+struct Mt19937 {
+    uint32_t key[624];
+    int32_t pos;
+
+    void twist() {
+        constexpr uint32_t kUpper = 0x80000000u, kLower = 0x7fffffffu, kMatrix = 0x9908b0dfu;
+        int i = 0;
+        for (; i < 624 - 397; ++i) {
+            const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+            key[i] = key[i + 397] ^ (y >> 1) ^ (-(y & 1u) & kMatrix);
+        }
+        for (; i < 623; ++i) {
+            const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+            key[i] = key[i + 397 - 624] ^ (y >> 1) ^ (-(y & 1u) & kMatrix);
+        }
+        const uint32_t y = (key[623] & kUpper) | (key[0] & kLower);
+        key[623] = key[396] ^ (y >> 1) ^ (-(y & 1u) & kMatrix);
+        pos = 0;
+    }
+    uint32_t next32() {
+        if (pos >= 624) twist();
+        uint32_t y = key[pos++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+    double next_double() {
+        const int32_t a = (int32_t)(next32() >> 5), b = (int32_t)(next32() >> 6);
+        return (a * 67108864.0 + b) / 9007199254740992.0;
+    }
+};
+
+// n_rows rows of A uniforms (C order): out[r * A + j] = low[j] + (high[j] - low[j]) * d.
+// Rows outside [keep_lo, keep_hi) are drawn (the stream advances) but not stored; kept row r
+// lands at out[(r - keep_lo) * A + j].
+void mt_uniform_rows(Mt19937& g, const double* low, const double* high, int A, int64_t n_rows, int64_t keep_lo,
+                     int64_t keep_hi, double* out);
+
+}  // namespace bcmpc

@@ -262,6 +262,35 @@ class RolloutEngine:
         return StepResult(int(res.best_index), float(res.best_cost),
                           np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
 
+    def get_action_numpy_stream(self, state, low, high, k_global: int, cand_offset: int = 0,
+                                return_costs: bool = False) -> Optional[StepResult]:
+        """get_action on the actions ``np.random.uniform(low, high, [H, k_global, A])`` would
+        return from the global legacy stream (controllers.py:53), drawn by the library's
+        MT19937 restatement from ``np.random.get_state()`` straight into pinned memory and
+        uploaded step by step (bcmpc_get_action_mt19937); the global stream is then advanced
+        exactly as that one NumPy call advances it.  Returns None (nothing drawn) when the
+        global generator is not the legacy MT19937 or the bounds are not per-action vectors."""
+        st = np.random.get_state()
+        lo = np.asarray(low, dtype=np.float64)
+        hi = np.asarray(high, dtype=np.float64)
+        if (not isinstance(st, tuple) or st[0] != "MT19937" or lo.shape != (self.action_dim,)
+                or hi.shape != (self.action_dim,) or not np.all(np.isfinite(hi - lo))):
+            return None
+        s = _f64(state).reshape(-1)
+        if s.shape[0] != self.state_dim:
+            raise ValueError(f"state has {s.shape[0]} dims, expected {self.state_dim}")
+        key = np.array(st[1], dtype=np.uint32)
+        pos = ctypes.c_int32(int(st[2]))
+        res = _lib.Result()
+        costs = np.empty(self.num_paths, dtype=np.float64) if return_costs else None
+        _lib.check(self._lib.bcmpc_get_action_mt19937(
+            self._h, _dp(s), key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos), _dp(lo),
+            _dp(hi), ctypes.c_int64(k_global), ctypes.c_int64(cand_offset), ctypes.byref(res),
+            _dp(costs) if costs is not None else None))
+        np.random.set_state((st[0], key, pos.value, st[3], st[4]))
+        return StepResult(int(res.best_index), float(res.best_cost),
+                          np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
+
     def rollout_async(self, d_state: int, state_stride: int, d_actions: Optional[int], seed: int,
                       cand_offset: int, d_costs: Optional[int], d_traj: Optional[int],
                       d_result: Optional[int], stream: Optional[int] = None) -> None:

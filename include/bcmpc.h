@@ -209,6 +209,23 @@ int bcmpc_set_action_bounds(bcmpc_engine* eng, const double* low, const double* 
 int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actions,
                      uint64_t seed, int64_t cand_offset, bcmpc_result* out, double* costs_out);
 
+/* MPCcontroller.get_action with the reference's RNG contract (controllers.py:53): the
+ * [H, k_global, A] array np.random.uniform(low, high, size) would return is drawn on the host
+ * from NumPy's legacy MT19937 state (mt_key[624] / mt_pos as np.random.get_state() holds
+ * them; advanced in place, as the one NumPy call would advance them), step by step into
+ * pinned memory, and this shard's [cand_offset, cand_offset + K) slice of each step is
+ * copied while the next step is drawn.  Then as bcmpc_get_action; out->first_action is
+ * action_paths[0, best] of that same array.  Replaces the host-array form of
+ * bcmpc_get_action on the drop-in path (no 8*H*K*A-byte pageable copy). */
+int bcmpc_get_action_mt19937(bcmpc_engine* eng, const double* state, uint32_t* mt_key, int32_t* mt_pos,
+                             const double* low, const double* high, int64_t k_global, int64_t cand_offset,
+                             bcmpc_result* out, double* costs_out);
+
+/* Host only (no GPU): n_rows x action_dim doubles of np.random.uniform(low, high) from the
+ * legacy MT19937 state (mt_key / mt_pos in/out) -- the generator bcmpc_get_action_mt19937 uses. */
+int bcmpc_mt19937_uniform(uint32_t* mt_key, int32_t* mt_pos, const double* low, const double* high,
+                          int32_t action_dim, int64_t n_rows, double* out);
+
 /* Actions the last rollout actually used for step 0 (policy engines:
  * action_paths[0] of controllers.py:233), copied to host K x A doubles. */
 int bcmpc_first_actions(bcmpc_engine* eng, double* out);

@@ -494,3 +494,36 @@ def test_fused_argmin_tail_matches_launches(model, monkeypatch):
     for a, b in zip(out[0], out[1]):
         assert a.best_index == b.best_index and a.best_cost == b.best_cost
         assert np.array_equal(a.first_action, b.first_action) and np.array_equal(a.costs, b.costs)
+
+
+def test_dropin_numpy_stream_path_equals_host_array_path():
+    """MPCcontroller draws the reference's [H, K, A] array with the library's MT19937 restatement
+    straight into pinned memory; a subclass that overrides sample_random_actions takes the host-
+    array path.  Same costs, same action, same global-stream position afterwards."""
+    from bc_mpc_amd import MPCcontroller, cheetah_cost_fn
+    g = Golden("cfg2_2x500_tanh")
+
+    class Box:
+        low, high = g.low, g.high
+        shape = (g.A,)
+
+    class Env:
+        action_space = Box()
+
+        class observation_space:
+            shape = (g.S,)
+
+    class Slow(MPCcontroller):
+        def sample_random_actions(self):
+            return super().sample_random_actions()
+
+    out = []
+    for cls in (MPCcontroller, Slow):
+        ctrl = cls(env=Env(), dyn_model=g.dyn(), horizon=g.H, cost_fn=cheetah_cost_fn, num_simulated_paths=g.K)
+        ctrl.keep_costs = True
+        np.random.seed(g.meta["seed"])
+        a = ctrl.get_action(g.state)
+        out.append((a, ctrl.last_costs.copy(), np.random.random()))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2] == float(g.z["next_draw"])
+    assert_costs_close(out[0][1], g.costs, g.near, "numpy-stream path")
