@@ -16,7 +16,7 @@ HEADER = os.path.join(REPO, "include", "bcmpc.h")
 def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(bcmpc_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(bcmpc_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_every_declared_symbol():

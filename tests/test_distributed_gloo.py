@@ -46,6 +46,24 @@ class ShardEngine:
         i = int(np.argmin(costs))
         return StepResult(cand_offset + i, float(costs[i]), actions[0, i].copy(), costs)
 
+    def get_action_numpy_stream(self, state, low, high, k_global, cand_offset=0, return_costs=False):
+        """The engine's NumPy-stream path: the full [H, k_global, A] from the library's MT19937
+        restatement (host-only, bcmpc_mt19937_uniform), this shard's slice rolled out."""
+        import ctypes
+        from bc_mpc_amd import _lib
+        lib = _lib.load()
+        st = np.random.get_state()
+        key = np.array(st[1], dtype=np.uint32)
+        pos = ctypes.c_int32(int(st[2]))
+        lo, hi = np.asarray(low, np.float64), np.asarray(high, np.float64)
+        full = np.empty((self.H * k_global, self.A))
+        dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))   # noqa: E731
+        assert lib.bcmpc_mt19937_uniform(key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
+                                         dp(lo), dp(hi), self.A, self.H * k_global, dp(full)) == 0
+        np.random.set_state((st[0], key, pos.value, st[3], st[4]))
+        actions = np.ascontiguousarray(full.reshape(self.H, k_global, self.A)[:, cand_offset:cand_offset + self.K])
+        return self.get_action(state, actions, cand_offset=cand_offset, return_costs=return_costs)
+
     def close(self):
         pass
 
