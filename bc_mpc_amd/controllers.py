@@ -325,6 +325,23 @@ class MPCcontrollerPolicyNet(Controller):
         spec, norm, version = _weights.extract(self.dyn_model)
         _check_model(spec, self._MODEL, type(self).__name__)
         pspec, pversion = _policy.extract(self.policy_net)
+        sign = -1.0 if reward else 1.0                         # argmax(r) == argmin(-r), ties and NaN alike
+        if (K > 0 and hi > lo and "sample_random_actions" not in self.__dict__
+                and type(self).sample_random_actions is MPCcontrollerPolicyNet.sample_random_actions):
+            # the exploration draw (controllers.py:191) made by the library into pinned memory,
+            # same values and stream advance as sample_random_actions
+            eng = self._engine_for(spec, pspec, S, A, hi - lo)
+            if eng.numpy_stream_available(self.env.action_space.low, self.env.action_space.high):
+                eng.set_weights(spec, norm, version)
+                eng.set_policy(pspec, float(self.explore), pversion)
+                seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+                res = eng.get_action_numpy_stream(state, self.env.action_space.low, self.env.action_space.high, K,
+                                                  lo, return_costs=self.keep_costs, seed=seed)
+                self.last_costs = res.costs
+                cost, index, first_g = _dist.allgather_minloc(True, sign * res.best_cost, res.best_index,
+                                                              res.first_action, A, self._group)
+                self.last_cost, self.last_index = sign * cost, index
+                return first_g
         exploration = self.sample_random_actions()           # every rank draws the full [H, K, A]
         seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
         if K == 0:
@@ -338,7 +355,6 @@ class MPCcontrollerPolicyNet(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, cost, index, first = True, res.best_cost, res.best_index, res.first_action
             self.last_costs = res.costs
-        sign = -1.0 if reward else 1.0                         # argmax(r) == argmin(-r), ties and NaN alike
         cost, index, first_g = _dist.allgather_minloc(valid, sign * cost, index, first, A, self._group)
         self.last_cost, self.last_index = sign * cost, index
         return first_g                                         # copy of action_paths[0, argmin] (:233-235)

@@ -832,7 +832,7 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
 
 int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_key, int32_t* mt_pos,
                              const double* low, const double* high, int64_t k_global, int64_t cand_offset,
-                             bcmpc_result* out, double* costs_out) {
+                             uint64_t seed, bcmpc_result* out, double* costs_out) {
     if (!e || !state || !mt_key || !mt_pos || !low || !high || !out) return fail(BCMPC_ERR_ARG, "null argument");
     const bcmpc_config& c = e->cfg;
     if (c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "get_action needs a fused objective (cheetah cost or learned reward)");
@@ -870,7 +870,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     }
     std::memcpy(mt_key, g.key, sizeof(g.key));
     *mt_pos = g.pos;
-    int rc = rollout_impl(e, e->d_state, 0, e->d_actions, 0, cand_offset, e->d_costs, nullptr, e->d_result, e->stream);
+    int rc = rollout_impl(e, e->d_state, 0, e->d_actions, seed, cand_offset, e->d_costs, nullptr, e->d_result, e->stream);
     if (rc != BCMPC_OK) return rc;
     HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream));
     if (costs_out)

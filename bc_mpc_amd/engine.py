@@ -262,20 +262,28 @@ class RolloutEngine:
         return StepResult(int(res.best_index), float(res.best_cost),
                           np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
 
+    def numpy_stream_available(self, low, high) -> bool:
+        """The global generator is NumPy's legacy MT19937 and the bounds are per-action vectors
+        with a finite range (np.random.uniform would not raise)."""
+        st = np.random.get_state()
+        lo = np.asarray(low, dtype=np.float64)
+        hi = np.asarray(high, dtype=np.float64)
+        return (isinstance(st, tuple) and st[0] == "MT19937" and lo.shape == (self.action_dim,)
+                and hi.shape == (self.action_dim,) and bool(np.all(np.isfinite(hi - lo))))
+
     def get_action_numpy_stream(self, state, low, high, k_global: int, cand_offset: int = 0,
-                                return_costs: bool = False) -> Optional[StepResult]:
+                                return_costs: bool = False, seed: int = 0) -> Optional[StepResult]:
         """get_action on the actions ``np.random.uniform(low, high, [H, k_global, A])`` would
         return from the global legacy stream (controllers.py:53), drawn by the library's
         MT19937 restatement from ``np.random.get_state()`` straight into pinned memory and
         uploaded step by step (bcmpc_get_action_mt19937); the global stream is then advanced
         exactly as that one NumPy call advances it.  Returns None (nothing drawn) when the
         global generator is not the legacy MT19937 or the bounds are not per-action vectors."""
+        if not self.numpy_stream_available(low, high):
+            return None
         st = np.random.get_state()
         lo = np.asarray(low, dtype=np.float64)
         hi = np.asarray(high, dtype=np.float64)
-        if (not isinstance(st, tuple) or st[0] != "MT19937" or lo.shape != (self.action_dim,)
-                or hi.shape != (self.action_dim,) or not np.all(np.isfinite(hi - lo))):
-            return None
         s = _f64(state).reshape(-1)
         if s.shape[0] != self.state_dim:
             raise ValueError(f"state has {s.shape[0]} dims, expected {self.state_dim}")
@@ -285,7 +293,8 @@ class RolloutEngine:
         costs = np.empty(self.num_paths, dtype=np.float64) if return_costs else None
         _lib.check(self._lib.bcmpc_get_action_mt19937(
             self._h, _dp(s), key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos), _dp(lo),
-            _dp(hi), ctypes.c_int64(k_global), ctypes.c_int64(cand_offset), ctypes.byref(res),
+            _dp(hi), ctypes.c_int64(k_global), ctypes.c_int64(cand_offset), ctypes.c_uint64(seed & (2**64 - 1)),
+            ctypes.byref(res),
             _dp(costs) if costs is not None else None))
         np.random.set_state((st[0], key, pos.value, st[3], st[4]))
         return StepResult(int(res.best_index), float(res.best_cost),

@@ -214,12 +214,13 @@ int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actio
  * from NumPy's legacy MT19937 state (mt_key[624] / mt_pos as np.random.get_state() holds
  * them; advanced in place, as the one NumPy call would advance them), step by step into
  * pinned memory, and this shard's [cand_offset, cand_offset + K) slice of each step is
- * copied while the next step is drawn.  Then as bcmpc_get_action; out->first_action is
- * action_paths[0, best] of that same array.  Replaces the host-array form of
+ * copied while the next step is drawn.  Then as bcmpc_get_action (seed: the stochastic
+ * policy's Philox normals); out->first_action is action_paths[0, best] of that same array
+ * (policy engines: the mixed action, the array being the exploration draw of controllers.py:191).  Replaces the host-array form of
  * bcmpc_get_action on the drop-in path (no 8*H*K*A-byte pageable copy). */
 int bcmpc_get_action_mt19937(bcmpc_engine* eng, const double* state, uint32_t* mt_key, int32_t* mt_pos,
                              const double* low, const double* high, int64_t k_global, int64_t cand_offset,
-                             bcmpc_result* out, double* costs_out);
+                             uint64_t seed, bcmpc_result* out, double* costs_out);
 
 /* Host only (no GPU): n_rows x action_dim doubles of np.random.uniform(low, high) from the
  * legacy MT19937 state (mt_key / mt_pos in/out) -- the generator bcmpc_get_action_mt19937 uses. */

@@ -46,7 +46,10 @@ class ShardEngine:
         i = int(np.argmin(costs))
         return StepResult(cand_offset + i, float(costs[i]), actions[0, i].copy(), costs)
 
-    def get_action_numpy_stream(self, state, low, high, k_global, cand_offset=0, return_costs=False):
+    def numpy_stream_available(self, low, high):
+        return True
+
+    def get_action_numpy_stream(self, state, low, high, k_global, cand_offset=0, return_costs=False, seed=0):
         """The engine's NumPy-stream path: the full [H, k_global, A] from the library's MT19937
         restatement (host-only, bcmpc_mt19937_uniform), this shard's slice rolled out."""
         import ctypes
