@@ -533,18 +533,35 @@ void rollout_x3(const RolloutArgs a) {
     // half w&1 of k-step w/2 of the next layer's input); the output layer (one 16-row tile,
     // action j at row S-16+j) is K-split over the waves, partials summed in fixed order by the
     // half-1 owners, whose lanes hold exactly the action dims.
+#ifndef X3_POLDIAG                // timing only (results wrong): 1 no hidden->hidden layer, 2 no explore
+#define X3_POLDIAG 0              // loads, 3 no partial sum / mixing, 4 no obz division
+#endif
     auto policy_step = [&](int h, double (&pact)[4]) __attribute__((always_inline)) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         const float* pm = Pb + PL * PHP;                // [obmean 32][obstd 32][logstd 16][out bias 16]
         const bool actor = owner && hv0 == 1;
+        // every layer's fragments of the first two layers and the output layer are requested
+        // here, so one L2 latency (under the owners' obz and the first barrier) covers them
         const __amdgpu_buffer_rsrc_t pr0 = layer_rsrc(a.pw[0], a.pwbytes[0]);
         h8 ah = fload(pr0, voff, (w * 2 + 0) * 1024), al = fload(pr0, voff, (w * 2 + 1) * 1024);
+        h8 nh[PPn > 0 ? PPn : 1], nl[PPn > 0 ? PPn : 1];
+        auto load_layer = [&](int l) __attribute__((always_inline)) {
+            const __amdgpu_buffer_rsrc_t rs = layer_rsrc(a.pw[l], a.pwbytes[l]);
+#pragma unroll
+            for (int p = 0; p < PPn; ++p) {
+                nh[p] = fload(rs, voff, ((w * PPn + p) * 2 + 0) * 1024);
+                nl[p] = fload(rs, voff, ((w * PPn + p) * 2 + 1) * 1024);
+            }
+        };
+        if (PL > 1) load_layer(1);
+        const __amdgpu_buffer_rsrc_t pro = layer_rsrc(a.pw[PL], a.pwbytes[PL]);    // output: k-step w/2
+        const h8 oh = fload(pro, voff, ((w >> 1) * 2 + 0) * 1024), ol = fload(pro, voff, ((w >> 1) * 2 + 1) * 1024);
         double uu[4] = {0.0, 0.0, 0.0, 0.0};            // explore draws (controllers.py:191), issued early
         if (actor && a.pol_mode != BCMPC_POLICY_STOCHASTIC) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int j = 16 + 4 * q + r - S;
-                if (valid && j >= 0 && j < A && a.actions)   // the caller's array (no CEM with a policy)
+                if (X3_POLDIAG != 2 && valid && j >= 0 && j < A && a.actions)   // the caller's array (no CEM)
                     uu[r] = a.actions[((int64_t)h * a.K + cand) * A + j];
             }
         }
@@ -555,7 +572,7 @@ void rollout_x3(const RolloutArgs a) {
                 const int d = 16 * hv0 + 4 * q + r;
                 float v = 0.f;
                 if (d < S) {
-                    v = ((float)s[0][r] - pm[d]) / pm[32 + d];
+                    v = X3_POLDIAG == 4 ? ((float)s[0][r] - pm[d]) * pm[32 + d] : ((float)s[0][r] - pm[d]) / pm[32 + d];
                     v = fminf(fmaxf(v, -5.0f), 5.0f);
                 }
                 z[r] = v * 2048.0f;
@@ -590,23 +607,8 @@ void rollout_x3(const RolloutArgs a) {
                 xl[c] = (h4){l01[0], l01[1], l23[0], l23[1]};
             }
         };
-        h8 nh[PPn > 0 ? PPn : 1], nl[PPn > 0 ? PPn : 1];
-        auto load_layer = [&](int l) __attribute__((always_inline)) {
-            const __amdgpu_buffer_rsrc_t rs = layer_rsrc(a.pw[l], a.pwbytes[l]);
-            if (l < PL) {
-#pragma unroll
-                for (int p = 0; p < PPn; ++p) {
-                    nh[p] = fload(rs, voff, ((w * PPn + p) * 2 + 0) * 1024);
-                    nl[p] = fload(rs, voff, ((w * PPn + p) * 2 + 1) * 1024);
-                }
-            } else {                                    // output layer: k-step w/2 of its single tile
-                nh[0] = fload(rs, voff, ((w >> 1) * 2 + 0) * 1024);
-                nl[0] = fload(rs, voff, ((w >> 1) * 2 + 1) * 1024);
-            }
-        };
-        load_layer(1);
         epi(a.pwinv[0] * kTanhK, Pb);
-        for (int l = 1; l < PL; ++l) {
+        for (int l = 1; l < (X3_POLDIAG == 1 ? 1 : PL); ++l) {
             if (l > 1) X3_BARRIER();                    // every wave is done reading the slab
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -625,7 +627,7 @@ void rollout_x3(const RolloutArgs a) {
                     pacc[c] = mfma16(nh[p], bl, pacc[c]);
                     pacc[c] = mfma16(nl[p], bh, pacc[c]);
                 }
-            load_layer(l + 1);
+            if (l + 1 < PL) load_layer(l + 1);
             epi(a.pwinv[l] * kTanhK, Pb + l * PHP);
         }
         // output layer, K-split: this wave's 16 neurons are one half of a k-step B fragment
@@ -638,13 +640,13 @@ void rollout_x3(const RolloutArgs a) {
                 bh[(w & 1) * 4 + i] = xh[c][i];
                 bl[(w & 1) * 4 + i] = xl[c][i];
             }
-            f4 po = mfma16(nh[0], bh, (f4){0.f, 0.f, 0.f, 0.f});
-            po = mfma16(nh[0], bl, po);
-            po = mfma16(nl[0], bh, po);
+            f4 po = mfma16(oh, bh, (f4){0.f, 0.f, 0.f, 0.f});
+            po = mfma16(oh, bl, po);
+            po = mfma16(ol, bh, po);
             part[(w * NC + c) * 64 + lane] = po;
         }
         X3_BARRIER();                                   // partials complete
-        if (!actor) return;
+        if (!actor || X3_POLDIAG == 3) return;
         f4 o = part[(0 * NC + cw) * 64 + lane];
 #pragma unroll
         for (int g = 1; g < NW; ++g) o += part[(g * NC + cw) * 64 + lane];   // fixed summation order
@@ -1127,8 +1129,7 @@ int x3_max_nc(int hidden_padded) {
 // fused policy: one 128-wide policy tile per wave of an 8-wave group
 bool x3_policy_ok(int hidden_padded, int nc) {
 #ifdef X3_ONLY
-    (void)hidden_padded; (void)nc;
-    return false;
+    return hidden_padded == X3_ONLY && X3_NW512 == 8 && 2 * nc <= 8 && hidden_padded >= 512;
 #else
     return x3_waves(hidden_padded) == 8 && 2 * nc <= 8 && hidden_padded >= 512;
 #endif
@@ -1141,9 +1142,14 @@ size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int polic
 template <int NC>
 static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
 #ifdef X3_ONLY          // variant builds (tools/build_variants.sh): one width, NC = 4 only
-    if constexpr (NC == X3_ONLY_NC)
-        return hidden_padded == X3_ONLY && a.pL == 0 ? launch_x3_t<X3_ONLY, X3_ONLY_NC, X3_NW512>(a, st)
-                                                     : hipErrorInvalidValue;
+    if constexpr (NC == X3_ONLY_NC) {
+        if (hidden_padded != X3_ONLY || a.model == BCMPC_MODEL_REWARD) return hipErrorInvalidValue;
+        if (a.pL > 0) {                   // the delta net with a fused policy (8-wave groups only)
+            if constexpr (X3_NW512 == 8 && X3_ONLY >= 512) return launch_x3_t<X3_ONLY, X3_ONLY_NC, 8, 128>(a, st);
+            return hipErrorInvalidValue;
+        }
+        return launch_x3_t<X3_ONLY, X3_ONLY_NC, X3_NW512>(a, st);
+    }
     return hipErrorInvalidValue;
 #else
     if (a.model == BCMPC_MODEL_REWARD) {      // NNDynamicsRewardModel (hidden <= 512)
