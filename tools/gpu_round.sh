@@ -24,7 +24,7 @@ tail -2 gpurun_out/bench.log
 if [ "${PROFILE:-1}" = 1 ]; then
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- \
-        python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} \
+        python3 "$GRAFT_REPO_ROOT/bench.py" --steps "$STEPS" --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} \
         > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
     stop_on $? rocprof
     find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*" | head
