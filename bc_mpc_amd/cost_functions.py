@@ -45,6 +45,9 @@ def trajectory_cost_fn(cost_fn, states, actions, next_states):
     return trajectory_cost
 
 
+_PROBED: dict = {}     # (cost_fn, state_dim, action_dim) -> verdict of the probe below
+
+
 def is_cheetah_cost(cost_fn, state_dim: int = 20, action_dim: int = 6) -> bool:
     """True when ``cost_fn`` computes exactly cost_functions.cheetah_cost_fn.
 
@@ -56,6 +59,19 @@ def is_cheetah_cost(cost_fn, state_dim: int = 20, action_dim: int = 6) -> bool:
         return True
     if getattr(cost_fn, "__name__", "") != "cheetah_cost_fn" or state_dim < 18:
         return False
+    try:
+        return _PROBED[(cost_fn, state_dim, action_dim)]    # probed once per function (every env step asks)
+    except (KeyError, TypeError):
+        pass
+    verdict = _probe(cost_fn, state_dim, action_dim)
+    try:
+        _PROBED[(cost_fn, state_dim, action_dim)] = verdict
+    except TypeError:                                       # unhashable callable
+        pass
+    return verdict
+
+
+def _probe(cost_fn, state_dim: int, action_dim: int) -> bool:
     rs = np.random.RandomState(20240601)
     s = rs.standard_normal((64, state_dim)) * 0.3
     s[:8, 5] = 0.2

@@ -149,12 +149,16 @@ class RolloutEngine:
         self.device, self.cost, self.model = device, cost, model
         self.policy_hidden, self.policy_layers, self.policy_mode = policy_hidden, policy_layers, policy_mode
         self._keep = []
+        self._wver = None
+        self._pol = None
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, spec: MLPSpec, normalization: Sequence, version: int) -> None:
         """Re-sync hook; idempotent on ``version``."""
         if spec.model != self.model or spec.n_layers != self.n_layers or spec.hidden != self.hidden:
             raise ValueError("weight shapes do not match the engine configuration")
+        if version == self._wver:       # bcmpc_set_weights returns at once on a known version: skip the marshalling
+            return
         ks = [_f32(k) for k in spec.kernels]
         bs = [_f32(b) for b in spec.biases]
         S, A, h = self.state_dim, self.action_dim, self.hidden
@@ -200,11 +204,16 @@ class RolloutEngine:
             w.mean_reward, w.std_reward = _dp(rstats[0]), _dp(rstats[1])
             keep.append(rstats)
         _lib.check(self._lib.bcmpc_set_weights(self._h, ctypes.byref(w), ctypes.c_uint64(version)))
+        self._wver = version
 
     def set_policy(self, spec: PolicySpec, explore: float, version: int) -> None:
         """Policy weights of MPCcontrollerPolicyNet (controllers.py:160-178)."""
         if spec.n_layers != self.policy_layers or spec.hidden != self.policy_hidden:
             raise ValueError("policy shapes do not match the engine configuration")
+        if self._pol is not None and version == self._pol[0]:   # known version: only ``explore`` can change
+            self._pol[1].explore = float(explore)
+            _lib.check(self._lib.bcmpc_set_policy(self._h, ctypes.byref(self._pol[1]), ctypes.c_uint64(version)))
+            return
         S, A, ph = self.state_dim, self.action_dim, self.policy_hidden
         ks = [_f32(k) for k in spec.kernels]
         bs = [_f32(b) for b in spec.biases]
@@ -221,6 +230,7 @@ class RolloutEngine:
         p = _lib.Policy(karr, barr, vecs[0].ctypes.data_as(FP), vecs[1].ctypes.data_as(FP),
                         vecs[2].ctypes.data_as(FP), float(explore))
         _lib.check(self._lib.bcmpc_set_policy(self._h, ctypes.byref(p), ctypes.c_uint64(version)))
+        self._pol = (version, p, ks, bs, vecs, karr, barr)     # the struct's pointers stay valid while held here
 
     def first_actions(self) -> np.ndarray:
         """Step-0 actions of every candidate of the last rollout (policy engines), [K, A] f64."""

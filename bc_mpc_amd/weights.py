@@ -103,11 +103,26 @@ def _install_fit_hook(dyn_model) -> None:
     dyn_model._bcmpc_fit_hooked = True
 
 
+def _cached(dyn_model, version: int, make):
+    """The spec built for ``version`` (kept on the model object): get_action runs once per env
+    step, the weights change once per refit."""
+    hit = getattr(dyn_model, "_bcmpc_spec_cache", None)
+    if hit is not None and hit[0] == version:
+        return hit[1]
+    spec = make()
+    try:
+        dyn_model._bcmpc_spec_cache = (version, spec)
+    except AttributeError:                                  # (a slotted object: no cache)
+        pass
+    return spec
+
+
 def extract(dyn_model) -> Tuple[MLPSpec, List[np.ndarray], int]:
     """Return ``(spec, normalization10, version)`` for the engine."""
     norm = normalization_of(dyn_model)
     if hasattr(dyn_model, "mlp_spec"):                      # bc_mpc_amd.dynamics.NNDynamicsModel
-        return dyn_model.mlp_spec(), norm, int(dyn_model.version)
+        v = int(dyn_model.version)
+        return _cached(dyn_model, v, dyn_model.mlp_spec), norm, v
     w = getattr(dyn_model, "weights", None)
     if w is not None and hasattr(w, "kernels"):             # NumPy stand-ins
         kernels = [np.asarray(k) for k in w.kernels]
@@ -125,5 +140,6 @@ def extract(dyn_model) -> Tuple[MLPSpec, List[np.ndarray], int]:
         return spec, norm, int(version)
     if hasattr(dyn_model, "sess"):                          # reference TF1 NNDynamicsModel
         _install_fit_hook(dyn_model)
-        return _tf_weights(dyn_model), norm, int(dyn_model._bcmpc_version)
+        v = int(dyn_model._bcmpc_version)                   # (variables read once per refit)
+        return _cached(dyn_model, v, lambda: _tf_weights(dyn_model)), norm, v
     raise TypeError(f"cannot read dynamics weights from {type(dyn_model).__name__}")
