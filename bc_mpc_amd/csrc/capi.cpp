@@ -119,6 +119,7 @@ struct bcmpc_engine {
     int nwl = 0;                       // packed weight layers (RolloutArgs.w entries)
     float winv[BCMPC_MAX_LAYERS + 1]{};  // split kernel: 1 / operand scales per layer
     float pwinv[BCMPC_MAX_LAYERS + 1]{}; // ... and per fused-policy layer
+    float hsc[BCMPC_MAX_LAYERS]{};       // split LN nets: output scale of hidden layer l
     bool reward = false;               // BCMPC_MODEL_REWARD (NNDynamicsRewardModel)
     hipStream_t stream = nullptr;
     // device buffers
@@ -195,10 +196,12 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32 or SPLIT_F16");
     const bool split = c.precision == BCMPC_PREC_SPLIT_F16;
     if (split) {
-        // f16 operands need bounded hidden activations (tanh) and the plain delta net
-        if (c.activation != BCMPC_ACT_TANH || c.layer_norm)
-            return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports tanh nets without LayerNorm "
-                                               "in this build (use FP32)");
+        // relu / LayerNorm hidden layers (per-column scales or statistics exchanged across the
+        // workgroup): the plain delta net without a policy, hidden <= 512
+        if ((c.activation != BCMPC_ACT_TANH || c.layer_norm) &&
+            (reward || c.policy_hidden > 0 || padded_hidden(c.hidden) > 512))
+            return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports relu / LayerNorm nets only for the "
+                                               "delta net without a policy, hidden <= 512 (use FP32)");
         if (reward && c.state_dim < 16)
             return fail(BCMPC_ERR_UNSUPPORTED, "split reward engines need state_dim >= 16 (reward row in tile 1)");
         if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLIT4))
@@ -255,12 +258,14 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         const int nwx = x3_waves(e->HP);
         auto fits = [&](int n) {
             return n <= nwx && n <= x3_max_nc(e->HP) && (e->PL == 0 || x3_policy_ok(e->HP, n)) &&
-                   x3_lds(e->HP, reward ? 3 : c.n_layers, n, c.action_dim, e->PL, e->PHP) <= 160 * 1024;
+                   x3_lds(e->HP, reward ? 3 : c.n_layers, n, c.action_dim, e->PL, e->PHP,
+                          (c.activation == BCMPC_ACT_RELU ? 1 : 0) | (c.layer_norm ? 2 : 0)) <= 160 * 1024;
         };
         if (nc == 0) {
             nc = 1;
+            // (hidden <= 256: 32-candidate groups, two or three workgroups per CU, measured 6-18% ahead of 64)
             for (int n : {4, 2})
-                if (fits(n) && cols >= (int64_t)n * 256) { nc = n; break; }
+                if (fits(n) && cols >= (int64_t)n * 256 && !(n == 4 && e->HP <= 256)) { nc = n; break; }
         }
         if (!fits(nc)) {
             delete e;
@@ -449,11 +454,33 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
             if (l == 0) pack_x3_layer(w->kernels[0], in, out, 1, T, tb, sw, hh + 2 * e->w_off[0]);
             else if (l < L) pack_x3_layer(w->kernels[l], in, out, P, T, tb, sw, hh + 2 * e->w_off[l]);
             else pack_x3_layer(w->kernels[L], in, out, P, 2, 2, sw, hh + 2 * e->w_off[L]);
-            // layer 0's input scale is per candidate (kernel); hidden inputs are tanh * 2^12
-            e->winv[l] = (1.0f / sw) * (l == 0 ? 1.0f : 1.0f / 4096.0f);
+            // layer 0's input scale is per candidate (kernel); hidden inputs are tanh * 2^12, an LN
+            // output x hsc[l-1] (static), or relu x its column's power of two (undone in the kernel)
+            float in_scale = 4096.0f;
+            if (l > 0 && c.layer_norm) {
+                // |LN(x)_i| <= sqrt(h) |gamma_i| + |beta_i|: the power of two that keeps it below 2^12
+                float gm = 0.f, bm = 0.f;
+                for (int i = 0; i < h; ++i) {
+                    gm = std::max(gm, std::fabs(w->ln_gamma[l - 1][i]));
+                    bm = std::max(bm, std::fabs(w->ln_beta[l - 1][i]));
+                }
+                const float bound = std::sqrt((float)h) * gm + bm;
+                int ex = 0;
+                if (bound > 0.f && std::isfinite(bound)) (void)std::frexp(bound, &ex);
+                in_scale = std::ldexp(1.0f, std::max(-100, std::min(100, 12 - ex)));
+                e->hsc[l - 1] = in_scale;
+            } else if (l > 0 && c.activation == BCMPC_ACT_RELU) {
+                in_scale = 1.0f;
+            }
+            e->winv[l] = (1.0f / sw) * (l == 0 ? 1.0f : 1.0f / in_scale);
         }
         for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
         std::memcpy(hb.data() + e->b_off[L], w->biases[L], sizeof(float) * S);
+        if (c.layer_norm)
+            for (int l = 0; l < L; ++l) {
+                std::memcpy(hln.data() + (size_t)l * HP, w->ln_gamma[l], sizeof(float) * h);
+                std::memcpy(hln.data() + (size_t)(L + l) * HP, w->ln_beta[l], sizeof(float) * h);
+            }
     } else {
     pack_layer(w->kernels[0], S + A, h, 2, T, tb, hw.data() + e->w_off[0]);
     if (rw) {
@@ -673,6 +700,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     }
     for (int l = 0; l < e->nwl; ++l) a.winv[l] = e->winv[l];
     for (int l = 0; l <= e->PL; ++l) a.pwinv[l] = e->pwinv[l];
+    for (int l = 0; l < c.n_layers; ++l) a.hsc[l] = e->hsc[l];
     if (cem) {
         if (e->kernel == BCMPC_KERNEL_SOLO || e->PL > 0)
             return fail(BCMPC_ERR_UNSUPPORTED, "CEM runs on group-kernel engines without a policy");

@@ -72,6 +72,7 @@ struct RolloutArgs {
     // exact powers of two (layer 0: weight scale only; its input scale is per candidate)
     float winv[BCMPC_MAX_LAYERS + 1];
     float pwinv[BCMPC_MAX_LAYERS + 1];       // the same for the fused policy's layers
+    float hsc[BCMPC_MAX_LAYERS];             // split LN nets: power-of-two scale of hidden layer l's output
     uint64_t* stamps;                        // diagnostics (X3_STAMP builds): [blocks][NW][10] phase cycles
     // split kernel: np.argmin fused into the launch's tail (fused_argmin != 0): every workgroup
     // leaves its best (cost, index) in amin.scratch_c/i[blockIdx.x], the last to finish (ticket)
@@ -112,7 +113,8 @@ size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_
 hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st);
 int x3_waves(int hidden_padded);
 int x3_max_nc(int hidden_padded);
-size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int policy_layers, int policy_hidden_padded);
+size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int policy_layers, int policy_hidden_padded,
+              int ak = 0);
 bool x3_policy_ok(int hidden_padded, int nc);
 hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);

@@ -136,6 +136,12 @@ __device__ __forceinline__ float max_rows32(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+__device__ __forceinline__ float add_rows(float v) {       // sum over the 4 lane rows (same in every row)
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(t[0]) + __uint_as_float(t[1]);
+}
 __device__ __forceinline__ int partner_row16(int v) {    // the value of row (r ^ 1), same column
     const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
     return (int)r[0] == v ? (int)r[1] : (int)r[0];          // (equal values: either is right)
@@ -346,6 +352,116 @@ __device__ __forceinline__ void epi_pair(const f4& a0, const f4& a1, float f, co
     split8(v, hi, lo);
 }
 
+// relu / LayerNorm epilogue (AK != 0; bit 0 relu, bit 1 LayerNorm) of this wave's TW tiles x NC
+// columns, in place: BiasAdd + activation in f32, then ONE exchange of per-column statistics
+// across the NW waves (X3 barrier 6), then the split.
+//   LN (dynamics.py:68-69, tf.contrib.layers.layer_norm): each wave's (mean, M2) over its valid
+//     rows, merged in wave order (Chan et al.), var = M2 / hidden, the nn.batch_normalization form
+//     x * inv + (beta - mean * inv), inv = rsqrt(var + eps) * gamma; output x hsc (host power of
+//     two from |y| <= sqrt(hidden) max|gamma| + max|beta|).  A tanh net's activations are tanh x 2^12
+//     here, so its eps is 1e-12 x 2^24 (the normalised output is the same).
+//   relu without LN: the column max sets the column's power of two (max -> [2^11, 2^12)); the
+//     next layer undoes it through fcol (its epilogue factor, or the output factor).
+template <int AK, int TW, int NC, int NW>
+__device__ __forceinline__ void epi_colx(f4 (&acc)[TW][NC], const float (&f)[NC], const float* __restrict__ bias,
+                                         const float* __restrict__ lg, const float* __restrict__ lb, float hsc,
+                                         int hidden, float* xch, int w, int lane, h8 (&xh)[TW / 2][NC],
+                                         h8 (&xl)[TW / 2][NC], float (&fcol)[NC]) {
+    constexpr bool RELU = (AK & 1) != 0, LNK = (AK & 2) != 0;
+    const int q = lane >> 4, m = lane & 15;
+#pragma unroll
+    for (int j = 0; j < TW; ++j) {
+        const f4 b = *reinterpret_cast<const f4*>(bias + 16 * (w * TW + j) + 4 * q);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float z = fmaf(acc[j][c][r], f[c], b[r]);
+                acc[j][c][r] = RELU ? fmaxf(z, 0.f) : tanh_x4096(z);     // pad rows: exactly 0
+            }
+    }
+    const int nwr = min(max(hidden - 16 * TW * w, 0), 16 * TW);        // this wave's valid rows
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        float s0 = 0.f, s1 = 0.f;
+        if constexpr (LNK) {
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s0 += acc[j][c][r];
+            s0 = nwr > 0 ? add_rows(s0) / (float)nwr : 0.f;
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float d = acc[j][c][r] - s0;
+                    s1 += (16 * (w * TW + j) + 4 * q + r < hidden) ? d * d : 0.f;
+                }
+            s1 = add_rows(s1);
+        } else {
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s0 = fmaxf(s0, acc[j][c][r]);
+            s0 = max_rows32(max_rows16(s0));
+        }
+        if (q == 0) *reinterpret_cast<f2*>(xch + ((w * NC + c) * 16 + m) * 2) = (f2){s0, s1};
+    }
+    X3_BARRIER_ID(6);                                   // every wave's column statistics published
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if constexpr (LNK) {
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int g = 0; g < NW; ++g) {
+                const float nb = (float)min(max(hidden - 16 * TW * g, 0), 16 * TW);
+                if (nb > 0.f) {
+                    const f2 st = *reinterpret_cast<const f2*>(xch + ((g * NC + c) * 16 + m) * 2);
+                    const float nn = n + nb, d = st[0] - mean;
+                    mean = mean + d * (nb / nn);
+                    m2 = m2 + st[1] + d * d * (n * nb / nn);
+                    n = nn;
+                }
+            }
+            const float eps = RELU ? 1e-12f : 1e-12f * 16777216.0f;
+            const float rs = 1.0f / sqrtf(m2 / (float)hidden + eps);
+#pragma unroll
+            for (int j = 0; j < TW; ++j) {
+                const f4 gv = *reinterpret_cast<const f4*>(lg + 16 * (w * TW + j) + 4 * q);
+                const f4 bv = *reinterpret_cast<const f4*>(lb + 16 * (w * TW + j) + 4 * q);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float inv = rs * gv[r];
+                    acc[j][c][r] = (acc[j][c][r] * inv + (bv[r] - mean * inv)) * hsc;
+                }
+            }
+        } else {
+            float mx = 0.f;
+#pragma unroll
+            for (int g = 0; g < NW; ++g) mx = fmaxf(mx, xch[((g * NC + c) * 16 + m) * 2]);
+            int e = 0;
+            (void)frexpf(mx, &e);
+            int sh = 12 - e;
+            sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
+            const float sc = ldexpf(1.0f, sh);
+            fcol[c] = ldexpf(1.0f, -sh);
+#pragma unroll
+            for (int j = 0; j < TW; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[j][c][r] *= sc;
+        }
+    }
+#pragma unroll
+    for (int pp = 0; pp < TW / 2; ++pp)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const float v[8] = {acc[2 * pp][c][0], acc[2 * pp][c][1], acc[2 * pp][c][2], acc[2 * pp][c][3],
+                                acc[2 * pp + 1][c][0], acc[2 * pp + 1][c][1], acc[2 * pp + 1][c][2],
+                                acc[2 * pp + 1][c][3]};
+            split8(v, xh[pp][c], xl[pp][c]);
+        }
+}
+
 #ifndef X3_NW512                // waves per workgroup at hidden 512 (8: one 64-candidate group per CU;
 #define X3_NW512 8               // 4: two 32-candidate groups per CU, out of phase)
 #endif
@@ -378,14 +494,21 @@ __host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
 // column factors NC*16 | column max [2][NC*16] | penalty counts [2][NC*16] | action inputs
 // X3_NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab P*NC*2 KiB
 __host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
-__host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, int PL = 0, int PHP = 0) {
+// | AK != 0: column exchange [NW][NC*16][2] | LN gamma [L][HP], beta [L][HP]
+__host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, int PL = 0, int PHP = 0, int AK = 0,
+                                                  int NW = 8) {
     return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
-           NC * 2048 + (HP / 32) * NC * 2048;
+           NC * 2048 + (HP / 32) * NC * 2048 + (AK != 0 ? NW * NC * 16 * 8 : 0) + ((AK & 2) ? 2 * L * HP * 4 : 0);
 }
 
-template <int HP, int NC, int NW, int PHP, bool RW>
+template <int HP, int NC, int NW, int PHP, bool RW, int AK>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(x3_waves_per_eu(HP, NC, NW), 8)))
 void rollout_x3(const RolloutArgs a) {
+    // AK: hidden activation kind, 0 tanh (activations tanh x 2^12: static scales); bit 0 relu,
+    // bit 1 LayerNorm (epi_colx: one column exchange per hidden layer)
+    constexpr bool RELU = (AK & 1) != 0, LNK = (AK & 2) != 0, DYN = RELU && !LNK;
+    constexpr float kAct = RELU ? 1.0f : kTanhK;        // folded into the epilogue factors / biases
+    static_assert(AK == 0 || (PHP == 0 && !RW), "relu / LayerNorm: the plain delta net only");
     constexpr int T = HP / 16;          // hidden tiles
     constexpr int P = T / 2;            // hidden k-steps (32 wide)
     constexpr int TW = T / NW;          // output tiles per wave
@@ -426,7 +549,7 @@ void rollout_x3(const RolloutArgs a) {
     float* Bl = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kConstRows * kConstCols * 8);
     for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
     for (int l = 0; l < LB; ++l)
-        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kTanhK;
+        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kAct;
     float* const Bout = Bl + LB * HP;
     for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[LB][i];
     float* const Pb = Bout + 32;                        // policy: [PL][PHP] hidden biases (x 2 log2 e), params
@@ -443,6 +566,17 @@ void rollout_x3(const RolloutArgs a) {
     float* xa = reinterpret_cast<float*>(penbuf + 2 * NC * 16);   // [X3_NCH][CB][A] normalised action inputs
     f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)));
     f4* slab = slab0 + NC * 2 * 64;
+    float* const xch = reinterpret_cast<float*>(slab + P * NC * 2 * 64);   // AK: column exchange
+    float* const lnp = xch + NW * NC * 16 * 2;                            // LN: gamma [L][HP], beta [L][HP]
+    if constexpr (LNK)
+        for (int l = 0; l < L; ++l)
+            for (int i = threadIdx.x; i < HP; i += blockDim.x) {
+                lnp[l * HP + i] = a.lng[l][i];
+                lnp[(L + l) * HP + i] = a.lnb[l][i];
+            }
+    float fcol[NC];                                     // DYN: 2^-(column scale) of the last hidden layer
+#pragma unroll
+    for (int c = 0; c < NC; ++c) fcol[c] = 1.0f;
     __syncthreads();
 
     double s[NHV][4];                                   // dims 16*(hv0+k) + 4q + r
@@ -749,13 +883,13 @@ void rollout_x3(const RolloutArgs a) {
                 // this half's 4 slots are bytes [8*hv0, 8*hv0+8) of the lane's 16-byte B fragment
                 reinterpret_cast<h4*>(slab0 + (cw * 2 + 0) * 64 + lane)[hv0] = xh;
                 reinterpret_cast<h4*>(slab0 + (cw * 2 + 1) * 64 + lane)[hv0] = xl;
-                if (hv0 == 0 && q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kTanhK;
+                if (hv0 == 0 && q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kAct;
             } else {
                 h8 xh, xl;
                 split8(xin, xh, xl);
                 swrite(slab0 + (cw * 2 + 0) * 64 + lane, xh);
                 swrite(slab0 + (cw * 2 + 1) * 64 + lane, xl);
-                if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kTanhK;
+                if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kAct;
             }
         }
         X3_ST(1);
@@ -790,12 +924,19 @@ void rollout_x3(const RolloutArgs a) {
         else
             load_next(1);
         h8 xh[PW][NC], xl[PW][NC];                        // this wave's activations of the current layer
+        if constexpr (AK != 0) {
+            float f0[NC];
 #pragma unroll
-        for (int pp = 0; pp < PW; ++pp)
+            for (int c = 0; c < NC; ++c) f0[c] = colf[c * 16 + m];
+            epi_colx<AK, TW, NC, NW>(acc, f0, Bl, lnp, lnp + L * HP, a.hsc[0], a.hidden, xch, w, lane, xh, xl, fcol);
+        } else {
 #pragma unroll
-            for (int c = 0; c < NC; ++c)
-                epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[c * 16 + m], Bl, w * TW + 2 * pp, q,
-                         xh[pp][c], xl[pp][c]);
+            for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[c * 16 + m], Bl, w * TW + 2 * pp, q,
+                             xh[pp][c], xl[pp][c]);
+        }
         X3_ST(3);
 
         f4 po1[NC];                                       // RW: the reward row's output partial (tile 1)
@@ -864,7 +1005,7 @@ void rollout_x3(const RolloutArgs a) {
         // ---- hidden layers 1..L-1 [h -> h] through the slab ----
         for (int l = 1; l < (RW ? 1 : L); ++l) {
             // (l == 1: the slab's last readers were the owners' partial sums, before the barrier above)
-            if (l > 1) X3_BARRIER_ID(2);               // every wave is done reading the slab
+            if (l > 1 && AK == 0) X3_BARRIER_ID(2);    // every wave is done reading the slab (AK: barrier 6 was)
 #pragma unroll
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
@@ -878,19 +1019,27 @@ void rollout_x3(const RolloutArgs a) {
             for (int j = 0; j < TW; ++j)
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
-            const float f = a.winv[l] * kTanhK;
+            const float f = a.winv[l] * kAct;
             // own k-steps first: this wave's slab writes need no barrier
             mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane,
                                                  uh, ul, kown, ready);
             if constexpr (!X3_OWN) ready();
             X3_ST(5);
             load_next(l + 1);
+            if constexpr (AK != 0) {
+                float fl[NC];
 #pragma unroll
-            for (int pp = 0; pp < PW; ++pp)
+                for (int c = 0; c < NC; ++c) fl[c] = DYN ? f * fcol[c] : f;
+                epi_colx<AK, TW, NC, NW>(acc, fl, Bl + l * HP, lnp + l * HP, lnp + (L + l) * HP, a.hsc[l], a.hidden,
+                                         xch, w, lane, xh, xl, fcol);
+            } else {
 #pragma unroll
-                for (int c = 0; c < NC; ++c)
-                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
-                             xl[pp][c]);
+                for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c)
+                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q,
+                                 xh[pp][c], xl[pp][c]);
+            }
         }
         X3_ST(6);
 
@@ -947,6 +1096,12 @@ void rollout_x3(const RolloutArgs a) {
         if (hv0 == 0) npen = partner_row16((s[0][1] >= 0.2) + (s[0][2] >= 0.0) + (s[0][3] >= 0.0));
         const double s17 = s[NHV - 1][1];                 // dim 17: half 1, row q = 0, r = 1
         // ---- de-normalise + residual (dynamics.py:113,116), f64, no FMA ----
+        float foc = fo;                                   // DYN: undo the last hidden layer's column scale
+        if constexpr (DYN) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (c == cw) foc = fo * fcol[c];
+        }
 #pragma unroll
         for (int k = 0; k < NHV; ++k) {
             const f4 bv = *reinterpret_cast<const f4*>(Bout + 16 * (hv0 + k) + 4 * q);
@@ -954,7 +1109,7 @@ void rollout_x3(const RolloutArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int d = 16 * (hv0 + k) + 4 * q + r;
                 if (d < S) {
-                    const float dn = fmaf(o[k][r], fo, bv[r]);             // BiasAdd (f32)
+                    const float dn = fmaf(o[k][r], foc, bv[r]);            // BiasAdd (f32)
                     const double ud = __dadd_rn(__dmul_rn((double)dn, C[5 * 32 + d]), C[4 * 32 + d]);
                     s[k][r] = __dadd_rn(s[k][r], ud);
                 }
@@ -1082,25 +1237,26 @@ void rollout_x3(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
-template <int HP, int NC, int NW, int PHP = 0, bool RW = false>
+template <int HP, int NC, int NW, int PHP = 0, bool RW = false, int AK = 0>
 static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
-    if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1) > 160 * 1024) {
+    if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1, 0, 0, AK, NW) > 160 * 1024) {
         (void)a; (void)st;
         return hipErrorInvalidValue;
     } else {
         if (PHP > 0 && (a.pL < 1 || a.phidden_padded != PHP)) return hipErrorInvalidValue;
         static bool attr_set = false;
         if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW, PHP, RW>,
+            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW, PHP, RW, AK>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
             attr_set = true;
         }
         if (RW != (a.model == BCMPC_MODEL_REWARD) || (RW && (a.L != 2 || a.S < 16))) return hipErrorInvalidValue;
-        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, RW ? 3 : a.L, a.A, PHP > 0 ? a.pL : 0, PHP);
+        if (AK != ((a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0))) return hipErrorInvalidValue;
+        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, RW ? 3 : a.L, a.A, PHP > 0 ? a.pL : 0, PHP, AK, NW);
         if (lds > 160 * 1024) return hipErrorInvalidValue;
         const int64_t blocks = (a.K + 16 * NC - 1) / (16 * NC);
-        hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP, RW>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
+        hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP, RW, AK>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
         return hipGetLastError();
     }
 }
@@ -1135,8 +1291,22 @@ bool x3_policy_ok(int hidden_padded, int nc) {
 #endif
 }
 
-size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int policy_layers, int policy_hidden_padded) {
-    return (size_t)x3_lds_bytes_rt(hidden_padded, nc, n_layers, action_dim, policy_layers, policy_hidden_padded);
+size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int policy_layers, int policy_hidden_padded,
+              int ak) {
+    return (size_t)x3_lds_bytes_rt(hidden_padded, nc, n_layers, action_dim, policy_layers, policy_hidden_padded, ak,
+                                   x3_waves(hidden_padded));
+}
+
+// relu and / or LayerNorm nets (AK != 0): the plain delta net, hidden <= 512
+template <int NC, int AK>
+static hipError_t launch_x3_ak(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+    switch (hidden_padded) {
+        case 64: return launch_x3_t<64, NC, 2, 0, false, AK>(a, st);
+        case 128: return launch_x3_t<128, NC, 4, 0, false, AK>(a, st);
+        case 256: return launch_x3_t<256, NC, 4, 0, false, AK>(a, st);
+        case 512: return launch_x3_t<512, NC, X3_NW512, 0, false, AK>(a, st);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 template <int NC>
@@ -1152,6 +1322,12 @@ static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStrea
     }
     return hipErrorInvalidValue;
 #else
+    if (a.act == BCMPC_ACT_RELU || a.ln) {
+        if (a.model == BCMPC_MODEL_REWARD || a.pL > 0) return hipErrorInvalidValue;
+        if (a.act == BCMPC_ACT_RELU) return a.ln ? launch_x3_ak<NC, 3>(a, hidden_padded, st)
+                                                 : launch_x3_ak<NC, 1>(a, hidden_padded, st);
+        return launch_x3_ak<NC, 2>(a, hidden_padded, st);
+    }
     if (a.model == BCMPC_MODEL_REWARD) {      // NNDynamicsRewardModel (hidden <= 512)
         if (a.pL > 0) {
             if constexpr (X3_NW512 == 8)

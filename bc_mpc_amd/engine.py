@@ -99,8 +99,9 @@ class RolloutEngine:
                  policy_hidden: int = 0, policy_layers: int = 0, policy_mode: str = "explore",
                  model: str = "delta", precision: Optional[str] = None):
         """``precision``: "fp32" (v_mfma_f32_16x16x4_f32), "split" (f32-accurate hi/lo f16
-        operands on v_mfma_f32_16x16x32_f16, rollout_x3.hip; tanh nets without LayerNorm; a
-        fused policy needs dynamics hidden 449..1024, 449..512 with the reward net) or "auto" (split where it
+        operands on v_mfma_f32_16x16x32_f16, rollout_x3.hip; relu / LayerNorm only for the plain delta net
+        with hidden <= 512; a fused policy needs a tanh net of hidden 449..1024, 449..512 with the reward
+        net) or "auto" (split where it
         applies, else fp32).
         Default: "split" for the split* kernels, else $BCMPC_PRECISION or "auto"."""
         self._lib = _lib.load()
@@ -128,7 +129,9 @@ class RolloutEngine:
             # a fused policy runs in the split kernel's 8-wave groups (dynamics hidden 449..1024;
             # the reward net: hidden <= 512)
             top = 512 if model == "reward" else 1024
-            split_ok = (activation == "tanh" and not layer_norm and (model == "delta" or state_dim >= 16)
+            plain = activation == "tanh" and not layer_norm
+            split_ok = ((plain or (model == "delta" and not policy_hidden and hidden <= 512))
+                        and (model == "delta" or state_dim >= 16)
                         and (not policy_hidden or 448 < hidden <= top)
                         and kernel in ("auto", "split1", "split2", "split4"))
             precision = "split" if split_ok else "fp32"

@@ -33,11 +33,14 @@ WORKLOADS = {
     "cfg3": dict(K=65536, H=20, hidden=500, L=2, act="tanh"),
     "cfg4_shard": dict(K=32768, H=20, hidden=500, L=2, act="tanh"),   # 262144 / 8 per GPU
     "cfg3_relu": dict(K=65536, H=20, hidden=500, L=2, act="relu"),    # diagnostic: no tanh
+    "cfg3_h256": dict(K=65536, H=20, hidden=256, L=2, act="tanh"),    # diagnostic: a 256-wide tanh net
     "cfg5_pass": dict(K=65536, H=50, hidden=1024, L=3, act="tanh"),   # one random-shooting pass of cfg5
     # MPCcontrollerPolicyNet (controllers.py:160-237) at cfg3 dims: 20->128->128->6 tanh policy fused per step,
     # self_exp=False, explore=0.5 (train_mpc_ppo.py:36-37,178 defaults)
     "cfg3_policy": dict(K=65536, H=20, hidden=500, L=2, act="tanh", policy=(128, 2), explore=0.5),
-    "ppo_defaults": dict(K=400, H=7, hidden=256, L=2, act="relu"),
+    # train_mpc_ppo.py's own net (:52,74-75,539): 2x256 relu + LayerNorm, 400 paths, horizon 7
+    "ppo_defaults": dict(K=400, H=7, hidden=256, L=2, act="relu", ln=True),
+    "cfg3_ppo_net": dict(K=65536, H=20, hidden=256, L=2, act="relu", ln=True),   # that net at cfg3's K, H
     # MPCcontrollerReward (controllers.py:90-158) on NNDynamicsRewardModel (dynamics.py:121-238): tanh trunk 500,
     # two 500 heads, argmax of sum_h reward * gamma**h
     "cfg3_reward": dict(K=65536, H=20, hidden=500, L=2, act="tanh", reward=True, gamma=0.99),
@@ -157,7 +160,9 @@ def main():
     K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
     if args.precision == "auto":
         top = 512 if wl.get("reward") else 1024
-        args.precision = "split" if (act == "tanh" and (not wl.get("policy") or 448 < hidden <= top)) else "fp32"
+        plain = act == "tanh" and not wl.get("ln")     # relu / LN: the plain delta net, hidden <= 512
+        ok = plain or (not wl.get("reward") and not wl.get("policy") and hidden <= 512)
+        args.precision = "split" if (ok and (not wl.get("policy") or 448 < hidden <= top)) else "fp32"
     offset = rank * K
 
     # synthetic inputs: glorot kernels, 0.1 N biases, synthetic stats/state
@@ -173,6 +178,12 @@ def main():
         lim = np.sqrt(6.0 / (fi + fo))
         kernels.append(r.uniform(-lim, lim, (fi, fo)).astype(np.float32))
         biases.append((0.1 * r.standard_normal(fo)).astype(np.float32))
+    ln = bool(wl.get("ln"))
+    ln_g, ln_b = None, None
+    if ln:   # gamma ~ 1 + 0.1 N, beta ~ 0.1 N per hidden layer
+        rl = np.random.RandomState(99)
+        ln_g = [(1.0 + 0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
+        ln_b = [(0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
     r7 = np.random.RandomState(7)
     mean_obs = 0.1 * r7.standard_normal(S_DIM)
     std_obs = np.abs(r7.standard_normal(S_DIM)) * 0.5 + 0.2
@@ -204,9 +215,9 @@ def main():
                             precision=args.precision)
         eng.set_policy(PolicySpec(*pol_arrays), wl["explore"], 1)
     else:
-        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, cost=cost, model=model,
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, ln, H, K, device=local, cost=cost, model=model,
                             precision=args.precision)
-    eng.set_weights(MLPSpec(kernels, biases, act, model=model), norm, 1)
+    eng.set_weights(MLPSpec(kernels, biases, act, ln_g, ln_b, model=model), norm, 1)
     if reward:
         eng.set_discount(gamma)
     info = eng.info()
@@ -308,7 +319,7 @@ def main():
                 f"actions {'resident in HBM as [H,K,6] f64' if args.actions == 'hbm' else 'drawn in-kernel (Philox)'})",
         "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
                                + (f"reward net {hidden} trunk + 2x{hidden} heads tanh, argmax sum r*{gamma}^h"
-                                  if reward else f"{L}x{hidden} {act}")
+                                  if reward else f"{L}x{hidden} {act}" + (" + LayerNorm" if ln else ""))
                                + (f" + fused policy {policy[1]}x{policy[0]} tanh "
                                   f"({wl.get('policy_mode', 'explore')})" if policy else "")
                                + (f" + CEM {iters} iterations, {n_elite} elites, alpha {cem['alpha']}" if cem else "")
@@ -342,8 +353,9 @@ def main():
             pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import mpc_oracle as orc
-        w = orc.RewardMLPWeights(kernels, biases) if reward else orc.MLPWeights(kernels, biases, act)
-        net = (f"reward net {hidden}" if reward else f"{L}x{hidden} {act}") + (f" + policy {policy}" if policy else "")
+        w = orc.RewardMLPWeights(kernels, biases) if reward else orc.MLPWeights(kernels, biases, act, ln_g, ln_b)
+        net = (f"reward net {hidden}" if reward else f"{L}x{hidden} {act}" + (" + LN" if ln else "")) + \
+            (f" + policy {policy}" if policy else "")
         if policy and wl.get("policy_mode") == "stochastic":
             net += " (oracle policy in its deterministic explore branch: TF's sampler is not restatable)"
         out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, net,

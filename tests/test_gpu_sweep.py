@@ -75,3 +75,32 @@ def test_split_reward_shapes(K, H, hidden, kernel):
     print(f"[reward {kernel} K{K} H{H} {hidden}] max|dr|={d.max():.2e}")
     assert (d <= ATOL + RTOL * np.abs(want)).all()
     assert res.best_index == int(np.argmax(res.costs))
+
+
+ACTLN = [  # (K, H, hidden, L, activation, layer_norm, kernel): the relu / LayerNorm split variants
+    (65, 3, 64, 2, "relu", False, "split1"), (300, 2, 128, 1, "relu", False, "split4"),
+    (200, 4, 256, 2, "relu", True, "split4"), (97, 3, 200, 3, "relu", True, "split2"),
+    (130, 3, 500, 2, "relu", False, "split2"), (70, 5, 500, 2, "relu", True, "split1"),
+    (257, 2, 512, 2, "tanh", True, "split2"), (150, 2, 256, 2, "tanh", True, "split4"),
+    (90, 2, 100, 2, "tanh", True, "split1"),
+]
+
+
+@pytest.mark.parametrize("K,H,hidden,L,act,ln,kernel", ACTLN)
+def test_split_relu_layernorm_shapes(K, H, hidden, L, act, ln, kernel):
+    """relu hidden layers (per-column power-of-two scales exchanged across the workgroup) and
+    LayerNorm (column statistics exchanged, dynamics.py:68-69) in the split kernel vs the oracle."""
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    norm = orc.synthetic_normalization(seed=8)
+    w = orc.synthetic_weights(20, 6, hidden, L, act, ln, seed_base=57 + hidden)
+    state = orc.synthetic_state(norm, seed=9)
+    eng = RolloutEngine(20, 6, hidden, L, act, ln, H, K, kernel=kernel)
+    assert eng.precision == "split"
+    eng.set_weights(MLPSpec(w.kernels, w.biases, act, w.ln_gamma, w.ln_beta), norm, 1)
+    res = eng.get_action(state, None, seed=77, cand_offset=3, return_costs=True)
+    ap = orc.device_rng_actions(77, 3, K, H, -np.ones(6), np.ones(6))
+    want, paths = orc.rollout(orc.NumpyDynamics(w, norm), state, ap)
+    near = orc.near_threshold_mask(paths)
+    _check(res.costs, want, near, res.best_index - 3, res.first_action, ap[0],
+           f"{kernel} {act}{'+LN' if ln else ''} K{K} H{H} {L}x{hidden}")
+    eng.close()
