@@ -4,7 +4,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
-OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/cem.o build/fit.o build/capi.o build/mt19937.o
+OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o
 HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h $(SRC)/argmin_common.h
 
 all: $(LIB)
@@ -30,6 +30,10 @@ build/cem.o: $(SRC)/cem.hip $(HDR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 build/mt19937.o: $(SRC)/mt19937.cpp $(SRC)/mt19937.h
+	@mkdir -p build
+	g++ -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -c $< -o $@
+
+build/mt_jump.o: $(SRC)/mt_jump.cpp $(SRC)/mt19937.h
 	@mkdir -p build
 	g++ -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -c $< -o $@
 

@@ -150,6 +150,10 @@ SIGNATURES = [
     ("bcmpc_mt19937_uniform", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int32, ctypes.c_int64,
       _DP]),
+    ("bcmpc_mt19937_uniform_par", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int32, ctypes.c_int64,
+      ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _DP, ctypes.c_int32, ctypes.c_int64,
+      ctypes.POINTER(ctypes.c_int32)]),
     ("bcmpc_rollout_async", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

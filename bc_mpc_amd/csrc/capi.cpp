@@ -16,6 +16,10 @@
 
 using namespace bcmpc;
 
+// a host thread of the split NumPy-stream draw gets at least this many generator words (~1 ms of
+// drawing): below it the jump-ahead (~0.3 ms per thread) does not pay
+static constexpr int64_t kMtMinWordsPerThread = int64_t(1) << 20;
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -889,12 +893,23 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     Mt19937 g;
     std::memcpy(g.key, mt_key, sizeof(g.key));
     g.pos = *mt_pos;
-    // [H, k_global, A] in C order, one step at a time: step h's slice of this shard is copied
-    // while step h+1 is drawn (the earlier copies overlap the generator)
-    for (int h = 0; h < H; ++h) {
-        mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_stage + h * row);
-        HIP_TRY(hipMemcpyAsync(e->d_actions + h * row, e->h_stage + h * row, row * sizeof(double),
-                               hipMemcpyHostToDevice, e->stream));
+    // Large draws: the stream split over host threads by jump-ahead (mt_jump.cpp); each thread
+    // copies its own slice as soon as it is drawn.  Otherwise [H, k_global, A] in C order, one
+    // step at a time: step h's slice of this shard is copied while step h+1 is drawn.
+    int chunk_rc = 0;
+    auto copy_chunk = [&](int64_t o_lo, int64_t o_hi) -> int {
+        return hipMemcpyAsync(e->d_actions + o_lo, e->h_stage + o_lo, (size_t)(o_hi - o_lo) * sizeof(double),
+                              hipMemcpyHostToDevice, e->stream) == hipSuccess ? 0 : 1;
+    };
+    if (mt_uniform_rows_par(g, low, high, A, (int64_t)H * k_global, k_global, cand_offset, cand_offset + K,
+                            e->h_stage, mt_default_threads(), kMtMinWordsPerThread, copy_chunk, &chunk_rc) > 0) {
+        if (chunk_rc) return fail(BCMPC_ERR_HIP, "hipMemcpyAsync of a drawn action slice failed");
+    } else {
+        for (int h = 0; h < H; ++h) {
+            mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_stage + h * row);
+            HIP_TRY(hipMemcpyAsync(e->d_actions + h * row, e->h_stage + h * row, row * sizeof(double),
+                                   hipMemcpyHostToDevice, e->stream));
+        }
     }
     std::memcpy(mt_key, g.key, sizeof(g.key));
     *mt_pos = g.pos;
@@ -917,6 +932,32 @@ int bcmpc_mt19937_uniform(uint32_t* mt_key, int32_t* mt_pos, const double* low, 
     std::memcpy(g.key, mt_key, sizeof(g.key));
     g.pos = *mt_pos;
     mt_uniform_rows(g, low, high, action_dim, n_rows, 0, n_rows, out);
+    std::memcpy(mt_key, g.key, sizeof(g.key));
+    *mt_pos = g.pos;
+    return BCMPC_OK;
+}
+
+int bcmpc_mt19937_uniform_par(uint32_t* mt_key, int32_t* mt_pos, const double* low, const double* high,
+                              int32_t action_dim, int64_t n_rows, int64_t period, int64_t keep_lo, int64_t keep_hi,
+                              double* out, int32_t threads, int64_t min_words_per_thread, int32_t* used_threads) {
+    if (!mt_key || !mt_pos || !low || !high || !out || action_dim < 1 || action_dim > 64 || n_rows < 0 ||
+        period < 1 || keep_lo < 0 || keep_hi > period || keep_lo >= keep_hi || n_rows % period)
+        return fail(BCMPC_ERR_ARG, "bad argument");
+    if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
+    Mt19937 g;
+    std::memcpy(g.key, mt_key, sizeof(g.key));
+    g.pos = *mt_pos;
+    if (threads <= 0) threads = mt_default_threads();
+    if (min_words_per_thread < 0) min_words_per_thread = kMtMinWordsPerThread;
+    const int used = mt_uniform_rows_par(g, low, high, action_dim, n_rows, period, keep_lo, keep_hi, out, threads,
+                                         min_words_per_thread, nullptr, nullptr);
+    const bool par = used > 0;
+    if (!par) {
+        const int64_t kw = keep_hi - keep_lo;
+        for (int64_t p = 0; p < n_rows / period; ++p)
+            mt_uniform_rows(g, low, high, action_dim, period, keep_lo, keep_hi, out + p * kw * action_dim);
+    }
+    if (used_threads) *used_threads = par ? used : 1;
     std::memcpy(mt_key, g.key, sizeof(g.key));
     *mt_pos = g.pos;
     return BCMPC_OK;

@@ -15,10 +15,12 @@ inline uint32_t temper(uint32_t y) {
     return y;
 }
 
+}  // namespace
+
 // the next m random_sample doubles of the stream (mt19937_next_double, two words each);
 // AVX2 clone where the host has it (same integer ops and exactly rounded conversions)
 __attribute__((target_clones("avx2", "default")))
-void next_doubles(Mt19937& g, double* dbl, int64_t m) {
+void mt_next_doubles(Mt19937& g, double* dbl, int64_t m) {
     int64_t i = 0;
     while (i < m) {
         if (g.pos >= 624) g.twist();
@@ -43,8 +45,6 @@ void next_doubles(Mt19937& g, double* dbl, int64_t m) {
     }
 }
 
-}  // namespace
-
 void mt_uniform_rows(Mt19937& g, const double* low, const double* high, int A, int64_t n_rows, int64_t keep_lo,
                      int64_t keep_hi, double* out) {
     double range[64];
@@ -54,7 +54,7 @@ void mt_uniform_rows(Mt19937& g, const double* low, const double* high, int A, i
     const int64_t rows_per = std::max<int64_t>(1, (int64_t)(sizeof(buf) / sizeof(double)) / A);
     for (int64_t r0 = 0; r0 < n_rows; r0 += rows_per) {
         const int64_t nr = std::min(rows_per, n_rows - r0);
-        next_doubles(g, buf, nr * A);
+        mt_next_doubles(g, buf, nr * A);
         const int64_t a = std::max(r0, keep_lo), b = std::min(r0 + nr, keep_hi);
         for (int64_t r = a; r < b; ++r) {
             const double* d = buf + (r - r0) * A;

@@ -1,0 +1,277 @@
+// mt_jump.cpp -- NumPy's legacy MT19937 stream drawn by several host threads (see mt19937.h).
+//
+// The generator's words obey x[k+624] = x[k+397] ^ mix(x[k], x[k+1]), a linear map F on the
+// 624-word window W_k = (x[k] .. x[k+623]) over GF(2).  On every window the generator can reach
+// (the image of F) the characteristic polynomial phi (degree 19937) annihilates F, so
+// F^J W = (x^J mod phi)(F) W  (Haramoto, Matsumoto, L'Ecuyer 2008, "A fast jump ahead algorithm for
+// linear recurrences in a polynomial space").  phi is found once per process by Berlekamp-Massey on
+// one bit of the generated words; x^J mod phi by square-and-multiply; the polynomial is applied to a
+// window by Horner's rule (one generator step per coefficient, one window XOR per set coefficient).
+//
+// Thread t >= 1 starts at a block boundary b0 + 624 * t * M of the caller's stream (b0 = the caller's
+// key block), so its start window is F^(624 (tM - 1)) applied to twist(key) and the jump polynomials
+// depend only on (t, M): they are cached per process.  Thread t draws the doubles that start in its
+// blocks; the last thread ends in exactly the (key, pos) NumPy itself would hold.
+#include "mt19937.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <functional>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace bcmpc {
+
+namespace {
+
+constexpr int kDeg = 19937;                   // degree of MT19937's characteristic polynomial
+constexpr int kPW = kDeg / 64 + 1;            // words of a polynomial of degree <= kDeg
+constexpr int kN = 624, kM = 397;
+using Poly = std::vector<uint64_t>;
+
+inline uint32_t mix(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return (y >> 1) ^ (-(y & 1u) & 0x9908b0dfu);
+}
+inline int bit(const uint64_t* p, int64_t i) { return (int)((p[i >> 6] >> (i & 63)) & 1u); }
+
+// r ^= p << s (p: np words)
+void xor_shifted(uint64_t* r, const uint64_t* p, int np, int64_t s) {
+    const int64_t ws = s >> 6;
+    const int bs = (int)(s & 63);
+    if (bs == 0) {
+        for (int w = 0; w < np; ++w) r[w + ws] ^= p[w];
+    } else {
+        for (int w = 0; w < np; ++w) {
+            r[w + ws] ^= p[w] << bs;
+            r[w + ws + 1] ^= p[w] >> (64 - bs);
+        }
+    }
+}
+
+// Berlekamp-Massey over GF(2) on the LSBs of generated words; returns phi (bit i = coeff of x^i)
+Poly compute_phi() {
+    Mt19937 g;
+    g.key[0] = 5489u;                                      // init_genrand(5489)
+    for (int i = 1; i < kN; ++i) g.key[i] = 1812433253u * (g.key[i - 1] ^ (g.key[i - 1] >> 30)) + (uint32_t)i;
+    g.pos = kN;
+    const int64_t N = 2 * (int64_t)kDeg + 128;
+    std::vector<uint8_t> s((size_t)N);
+    for (int64_t n = 0; n < N; ++n) {
+        if (g.pos >= kN) g.twist();                        // raw (untempered) words, all generated
+        s[(size_t)n] = (uint8_t)(g.key[g.pos++] & 1u);
+    }
+    const int NW = (int)(N / 64) + 2;
+    Poly C(NW, 0), B(NW, 0), T(NW, 0), R(NW, 0);
+    C[0] = B[0] = 1;
+    int L = 0;
+    int64_t m = 1;
+    for (int64_t n = 0; n < N; ++n) {
+        // R bit i = s[n - i]
+        for (int w = NW - 1; w > 0; --w) R[w] = (R[w] << 1) | (R[w - 1] >> 63);
+        R[0] = (R[0] << 1) | s[(size_t)n];
+        const int lw = L / 64 + 1;
+        uint64_t acc = 0;
+        for (int w = 0; w < lw; ++w) acc ^= C[w] & R[w];
+        const int d = __builtin_popcountll(acc) & 1;
+        if (!d) {
+            ++m;
+        } else if (2 * L <= n) {
+            T = C;
+            xor_shifted(C.data(), B.data(), (int)(NW - 1 - (m >> 6)), m);
+            L = (int)(n + 1 - L);
+            B = T;
+            m = 1;
+        } else {
+            xor_shifted(C.data(), B.data(), (int)(NW - 1 - (m >> 6)), m);
+            ++m;
+        }
+    }
+    if (L != kDeg) std::abort();                           // MT19937's recurrence has degree 19937
+    Poly phi(kPW, 0);                                      // phi(x) = x^L C(1/x)
+    for (int i = 0; i <= L; ++i)
+        if (bit(C.data(), i)) phi[(size_t)(L - i) >> 6] |= 1ull << ((L - i) & 63);
+    return phi;
+}
+
+const Poly& phi_poly() {
+    static const Poly phi = compute_phi();
+    return phi;
+}
+
+// r (2*kPW words, degree < 2*kDeg) mod phi, in place
+void reduce(uint64_t* r, const Poly& phi) {
+    for (int64_t i = 2 * (int64_t)kDeg - 2; i >= kDeg; --i)
+        if (bit(r, i)) xor_shifted(r, phi.data(), kPW, i - kDeg);
+}
+
+// x^e mod phi
+Poly x_pow_mod(uint64_t e) {
+    const Poly& phi = phi_poly();
+    static const uint16_t* spread = [] {
+        static uint16_t t[256];
+        for (int b = 0; b < 256; ++b) {
+            uint16_t v = 0;
+            for (int k = 0; k < 8; ++k) v |= (uint16_t)(((b >> k) & 1) << (2 * k));
+            t[b] = v;
+        }
+        return t;
+    }();
+    Poly r(2 * kPW + 1, 0), sq(2 * kPW + 1, 0);
+    r[0] = 1;
+    for (int b = 63; b >= 0; --b) {
+        if ((e >> b) == 0) continue;                       // leading zeros
+        // r = r^2 mod phi
+        std::fill(sq.begin(), sq.end(), 0);
+        for (int w = 0; w < kPW; ++w) {
+            const uint64_t v = r[w];
+            uint64_t lo = 0, hi = 0;
+            for (int k = 0; k < 4; ++k) lo |= (uint64_t)spread[(v >> (8 * k)) & 255] << (16 * k);
+            for (int k = 0; k < 4; ++k) hi |= (uint64_t)spread[(v >> (32 + 8 * k)) & 255] << (16 * k);
+            sq[2 * w] = lo;
+            sq[2 * w + 1] = hi;
+        }
+        reduce(sq.data(), phi);
+        std::swap(r, sq);
+        if ((e >> b) & 1u) {                               // r = r * x mod phi
+            for (int w = kPW; w > 0; --w) r[w] = (r[w] << 1) | (r[w - 1] >> 63);
+            r[0] <<= 1;
+            if (bit(r.data(), kDeg)) xor_shifted(r.data(), phi.data(), kPW, 0);
+        }
+    }
+    r.resize(kPW);
+    return r;
+}
+
+// cached x^(624 * blocks) mod phi
+const Poly& block_jump(int64_t blocks) {
+    static std::mutex mu;
+    static std::map<int64_t, Poly> cache;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(blocks);
+        if (it != cache.end()) return it->second;
+    }
+    Poly p = x_pow_mod((uint64_t)blocks * kN);
+    std::lock_guard<std::mutex> lk(mu);
+    return cache.emplace(blocks, std::move(p)).first->second;   // (std::map nodes never move)
+}
+
+// out = g(F) w  (w a reachable window)
+__attribute__((target_clones("avx2", "default")))
+void apply_poly(const Poly& g, const uint32_t* w, uint32_t* out) {
+    int top = kDeg - 1;
+    while (top >= 0 && !bit(g.data(), top)) --top;
+    std::vector<uint32_t> buf(2 * kN, 0);
+    uint32_t* b = buf.data();
+    int s = 0;
+    for (int i = top; i >= 0; --i) {
+        b[s + kN] = b[s + kM] ^ mix(b[s], b[s + 1]);      // acc = F(acc)
+        if (++s == kN) {
+            std::memcpy(b, b + kN, kN * sizeof(uint32_t));
+            s = 0;
+        }
+        if (bit(g.data(), i)) {                            // acc ^= w
+            uint32_t* a = b + s;
+            for (int j = 0; j < kN; ++j) a[j] ^= w[j];
+        }
+    }
+    std::memcpy(out, b + s, kN * sizeof(uint32_t));
+}
+
+}  // namespace
+
+int mt_default_threads() {
+    const char* e = std::getenv("BCMPC_MT_THREADS");
+    if (e && *e) return std::max(1, std::atoi(e));
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::min<unsigned>(8u, hc ? hc : 1u);
+}
+
+void mt_jump_blocks(const Mt19937& g, int64_t blocks, Mt19937& out) {
+    // W1 = twist(key): the window one block past the caller's key block (generated, so reachable)
+    Mt19937 t = g;
+    t.twist();
+    if (blocks <= 1) {
+        out = t;
+    } else {
+        apply_poly(block_jump(blocks - 1), t.key, out.key);
+    }
+    out.pos = 0;
+}
+
+int mt_uniform_rows_par(Mt19937& g, const double* low, const double* high, int A, int64_t n_rows, int64_t period,
+                         int64_t keep_lo, int64_t keep_hi, double* out, int threads, int64_t min_words_per_thread,
+                         const std::function<int(int64_t, int64_t)>& on_chunk, int* chunk_rc) {
+    const int64_t ntot = n_rows * A;                      // doubles
+    const int64_t words = 2 * ntot;
+    int T = threads;
+    if (min_words_per_thread > 0) T = (int)std::min<int64_t>(T, words / min_words_per_thread);
+    const int64_t M = T > 0 ? words / ((int64_t)kN * T) : 0;   // blocks per thread
+    if (T < 2 || M < 1) return 0;
+    const int pos0 = g.pos;
+    std::vector<int64_t> D(T + 1);
+    D[0] = 0;
+    for (int t = 1; t < T; ++t) D[t] = ((int64_t)kN * t * M - pos0 + 1) / 2;   // first double starting in block tM
+    D[T] = ntot;
+    double range[64];
+    for (int j = 0; j < A; ++j) range[j] = high[j] - low[j];   // np.subtract(high, low)
+    const int64_t kw = keep_hi - keep_lo;
+    std::vector<Mt19937> gs(T);
+    std::vector<int> rcs(T, 0);
+    auto work = [&](int t) {
+        Mt19937& gt = gs[t];
+        if (t == 0) {
+            gt = g;
+        } else {
+            mt_jump_blocks(g, (int64_t)t * M, gt);
+            gt.pos = (int32_t)(pos0 + 2 * D[t] - (int64_t)kN * t * M);       // 0 or 1
+        }
+        constexpr int64_t kChunk = 4096, kFlush = int64_t(1) << 18;   // doubles
+        double buf[kChunk];
+        int64_t e = D[t];
+        int64_t r = e / A, j = e % A;
+        int64_t rp = r % period, rq = r / period;
+        int64_t o_lo = -1, o_hi = -1;
+        while (e < D[t + 1]) {
+            const int64_t n = std::min(kChunk, D[t + 1] - e);
+            mt_next_doubles(gt, buf, n);
+            for (int64_t i = 0; i < n; ++i) {
+                if (rp >= keep_lo && rp < keep_hi) {
+                    const int64_t o = (rq * kw + (rp - keep_lo)) * A + j;
+                    out[o] = low[j] + range[j] * buf[i];   // random_uniform: mul, then add
+                    if (o_lo < 0) o_lo = o;
+                    o_hi = o + 1;
+                }
+                if (++j == A) {
+                    j = 0;
+                    if (++rp == period) { rp = 0; ++rq; }
+                }
+            }
+            e += n;
+            // hand finished output on in ~2 MiB pieces, so its copy overlaps the rest of the draw
+            if (on_chunk && o_lo >= 0 && o_hi - o_lo >= kFlush && !rcs[t]) {
+                rcs[t] = on_chunk(o_lo, o_hi);
+                o_lo = -1;
+            }
+        }
+        if (on_chunk && o_lo >= 0 && !rcs[t]) rcs[t] = on_chunk(o_lo, o_hi);
+    };
+    std::vector<std::thread> pool;
+    pool.reserve(T - 1);
+    for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    g = gs[T - 1];
+    if (chunk_rc) {
+        *chunk_rc = 0;
+        for (int t = 0; t < T; ++t)
+            if (rcs[t]) { *chunk_rc = rcs[t]; break; }
+    }
+    return T;
+}
+
+}  // namespace bcmpc

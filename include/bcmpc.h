@@ -214,7 +214,8 @@ int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actio
  * from NumPy's legacy MT19937 state (mt_key[624] / mt_pos as np.random.get_state() holds
  * them; advanced in place, as the one NumPy call would advance them), step by step into
  * pinned memory, and this shard's [cand_offset, cand_offset + K) slice of each step is
- * copied while the next step is drawn.  Then as bcmpc_get_action (seed: the stochastic
+ * copied while the next step is drawn (large draws: split over host threads by jump-ahead,
+ * each thread's slice copied as soon as it is drawn; see bcmpc_mt19937_uniform_par).  Then as bcmpc_get_action (seed: the stochastic
  * policy's Philox normals); out->first_action is action_paths[0, best] of that same array
  * (policy engines: the mixed action, the array being the exploration draw of controllers.py:191).  Replaces the host-array form of
  * bcmpc_get_action on the drop-in path (no 8*H*K*A-byte pageable copy). */
@@ -226,6 +227,18 @@ int bcmpc_get_action_mt19937(bcmpc_engine* eng, const double* state, uint32_t* m
  * legacy MT19937 state (mt_key / mt_pos in/out) -- the generator bcmpc_get_action_mt19937 uses. */
 int bcmpc_mt19937_uniform(uint32_t* mt_key, int32_t* mt_pos, const double* low, const double* high,
                           int32_t action_dim, int64_t n_rows, double* out);
+
+/* Host only (no GPU): the same stream as bcmpc_mt19937_uniform, drawn by up to `threads` host
+ * threads (<= 0: BCMPC_MT_THREADS, else min(8, hardware threads)) that each jump ahead to their own
+ * block of the stream (MT19937 jump-ahead, csrc/mt_jump.cpp) and draw at least
+ * min_words_per_thread generator words (< 0: the library's default, 2^20).  n_rows rows in
+ * repeating groups of `period` rows; only rows r with r % period in [keep_lo, keep_hi) are stored
+ * (a shard's candidates of each step: period = k_global), densely in row order.  mt_key / mt_pos
+ * end exactly where the serial draw leaves them; *used_threads (optional) = threads used (1: serial).
+ * The path bcmpc_get_action_mt19937 takes for large draws. */
+int bcmpc_mt19937_uniform_par(uint32_t* mt_key, int32_t* mt_pos, const double* low, const double* high,
+                              int32_t action_dim, int64_t n_rows, int64_t period, int64_t keep_lo, int64_t keep_hi,
+                              double* out, int32_t threads, int64_t min_words_per_thread, int32_t* used_threads);
 
 /* Actions the last rollout actually used for step 0 (policy engines:
  * action_paths[0] of controllers.py:233), copied to host K x A doubles. */

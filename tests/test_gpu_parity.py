@@ -527,3 +527,37 @@ def test_dropin_numpy_stream_path_equals_host_array_path():
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
     assert out[0][2] == out[1][2] == float(g.z["next_draw"])
     assert_costs_close(out[0][1], g.costs, g.near, "numpy-stream path")
+
+
+@pytest.mark.parametrize("pre_draws", [0, 1, 313])
+def test_dropin_threaded_numpy_stream_equals_host_array_path(pre_draws):
+    """Large draws split over host threads by MT19937 jump-ahead (csrc/mt_jump.cpp), each thread
+    uploading its own slice: the same costs, action and global-stream position as the host-array
+    path (NumPy's own draw) at K = 65536, H = 6 (4.7M generator words: 4 threads)."""
+    from bc_mpc_amd import MPCcontroller, cheetah_cost_fn
+    g = Golden("cfg2_2x500_tanh")
+
+    class Box:
+        low, high = g.low, g.high
+        shape = (g.A,)
+
+    class Env:
+        action_space = Box()
+
+        class observation_space:
+            shape = (g.S,)
+
+    class Slow(MPCcontroller):
+        def sample_random_actions(self):
+            return super().sample_random_actions()
+
+    out = []
+    for cls in (MPCcontroller, Slow):
+        ctrl = cls(env=Env(), dyn_model=g.dyn(), horizon=6, cost_fn=cheetah_cost_fn, num_simulated_paths=65536)
+        ctrl.keep_costs = True
+        np.random.seed(99)
+        np.random.random(pre_draws)
+        a = ctrl.get_action(g.state)
+        out.append((a, ctrl.last_costs.copy(), np.random.get_state()))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][2][1], out[1][2][1]) and out[0][2][2] == out[1][2][2]

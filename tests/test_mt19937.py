@@ -36,3 +36,68 @@ def test_uniform_matches_numpy_stream(seed, pre_words):
     got = _draw(lib, low.astype(np.float64), high.astype(np.float64), H * K).reshape(H, K, 6)
     assert np.array_equal(got, want)
     assert np.array_equal(np.random.random(3), after)
+
+
+def _draw_par(lib, low, high, n_rows, period, keep_lo, keep_hi, threads, min_words):
+    st = np.random.get_state()
+    key = np.array(st[1], dtype=np.uint32)
+    pos = ctypes.c_int32(int(st[2]))
+    out = np.empty((n_rows // period * (keep_hi - keep_lo), len(low)))
+    used = ctypes.c_int32(0)
+    dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))   # noqa: E731
+    assert lib.bcmpc_mt19937_uniform_par(key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
+                                         dp(low), dp(high), len(low), n_rows, period, keep_lo, keep_hi, dp(out),
+                                         threads, min_words, ctypes.byref(used)) == 0
+    return out, key, pos.value, used.value
+
+
+@pytest.mark.parametrize("pre_words", [0, 1, 2, 311, 623, 624, 625, 1249, 5000])
+@pytest.mark.parametrize("threads", [2, 3, 8])
+@pytest.mark.parametrize("shard", [None, (17, 251), (0, 1), (299, 300)])
+def test_threaded_jump_ahead_matches_numpy(pre_words, threads, shard):
+    """Jump-ahead split of the draw (csrc/mt_jump.cpp): every thread's slice, the shard selection
+    and the final (key, pos) -- the representation np.random.get_state() holds, not only the
+    stream -- equal NumPy's one np.random.uniform call."""
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    low = np.array([-1, -0.5, 0, -2, -3, 0.1])
+    high = np.array([1, 0.5, 2, 2, 3, 0.2])
+    H, K = 9, 300
+    lo, hi = shard or (0, K)
+    np.random.seed(11)
+    np.random.randint(0, 2**31 - 1, size=pre_words, dtype=np.int64)
+    st = np.random.get_state()
+    want = np.random.uniform(low=low, high=high, size=[H, K, 6])
+    st_after = np.random.get_state()
+    np.random.set_state(st)
+    got, key, pos, used = _draw_par(lib, low, high, H * K, K, lo, hi, threads, 1)
+    assert used == threads                      # forced split (1 word per thread minimum)
+    assert np.array_equal(got.reshape(H, hi - lo, 6), want[:, lo:hi])
+    assert np.array_equal(key, st_after[1]) and pos == st_after[2]
+
+
+def test_threaded_default_threshold_large_draw():
+    """A draw of several million words splits under the library's default threshold and still equals
+    NumPy's; a small one stays serial."""
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    low, high = -np.ones(6), np.ones(6)
+    H, K = 6, 65536
+    np.random.seed(1234)
+    np.random.random(777)
+    st = np.random.get_state()
+    want = np.random.uniform(low=low, high=high, size=[H, K, 6])
+    st_after = np.random.get_state()
+    np.random.set_state(st)
+    got, key, pos, used = _draw_par(lib, low, high, H * K, K, 0, K, 4, -1)
+    assert used == 4
+    assert np.array_equal(got.reshape(H, K, 6), want)
+    assert np.array_equal(key, st_after[1]) and pos == st_after[2]
+    np.random.set_state(st)
+    small = np.random.uniform(low=low, high=high, size=[3, 100, 6])
+    st_small = np.random.get_state()
+    np.random.set_state(st)
+    got, key, pos, used = _draw_par(lib, low, high, 3 * 100, 100, 0, 100, 4, -1)
+    assert used == 1
+    assert np.array_equal(got.reshape(3, 100, 6), small)
+    assert np.array_equal(key, st_small[1]) and pos == st_small[2]

@@ -54,7 +54,35 @@ def main():
         for _ in range(3):
             np.random.uniform(-1, 1, size=[H, K, A])
         out["host_rng_ms"] = (time.perf_counter() - t0) / 3 * 1e3
-        for rng in ("numpy", "device"):
+        # the library's draw alone into a resident host array (serial, then split by jump-ahead)
+        import ctypes
+        from bc_mpc_amd import _lib
+        lib = _lib.load()
+        buf = np.zeros((H * K, A))
+        lo, hi = -np.ones(A), np.ones(A)
+        dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))   # noqa: E731
+        for name, thr in (("lib_draw_1thread_ms", 1), ("lib_draw_ms", 0)):
+            st = np.random.get_state()
+            key = np.array(st[1], dtype=np.uint32)
+            used = ctypes.c_int32(0)
+            ts = []
+            for _ in range(5):
+                pos = ctypes.c_int32(int(st[2]))
+                t0 = time.perf_counter()
+                lib.bcmpc_mt19937_uniform_par(key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos),
+                                              dp(lo), dp(hi), A, H * K, K, 0, K, dp(buf), thr, -1,
+                                              ctypes.byref(used))
+                ts.append(time.perf_counter() - t0)
+            out[name] = float(np.median(ts)) * 1e3
+            out[name.replace("_ms", "_threads")] = used.value
+        # numpy: the library's draw (split over host threads by jump-ahead when large);
+        # numpy_1thread: the same draw forced serial (BCMPC_MT_THREADS=1, read per call)
+        for mode in ("numpy", "numpy_1thread", "device"):
+            rng = "device" if mode == "device" else "numpy"
+            if mode == "numpy_1thread":
+                os.environ["BCMPC_MT_THREADS"] = "1"
+            else:
+                os.environ.pop("BCMPC_MT_THREADS", None)
             ctrl = MPCcontroller(_Env(), dyn, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K, rng=rng,
                                  seed=1 if rng == "device" else None)
             for _ in range(3):
@@ -65,8 +93,8 @@ def main():
                 ctrl.get_action(state)
                 ts.append(time.perf_counter() - t0)
             p50 = float(np.median(ts))
-            out[f"{rng}_p50_ms"] = p50 * 1e3
-            out[f"{rng}_cand_steps_per_s"] = K * H / p50
+            out[f"{mode}_p50_ms"] = p50 * 1e3
+            out[f"{mode}_cand_steps_per_s"] = K * H / p50
         print(json.dumps(out), flush=True)
 
 
