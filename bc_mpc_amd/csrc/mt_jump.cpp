@@ -15,6 +15,8 @@
 #include "mt19937.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <cstring>
@@ -22,6 +24,8 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include <emmintrin.h>
 
 namespace bcmpc {
 
@@ -160,26 +164,53 @@ const Poly& block_jump(int64_t blocks) {
     return cache.emplace(blocks, std::move(p)).first->second;   // (std::map nodes never move)
 }
 
-// out = g(F) w  (w a reachable window)
+// out = g(F) w  (w a reachable window).  Horner over 8-coefficient blocks (the sliding-window
+// form of Haramoto et al.): tab[v] = sum_j v_j F^j w for every byte v (F^j w = w's stream shifted by
+// j words), then acc = F^8 acc ^ tab[block] from the top block down: one window XOR per 8
+// coefficients instead of one per set coefficient.
 __attribute__((target_clones("avx2", "default")))
 void apply_poly(const Poly& g, const uint32_t* w, uint32_t* out) {
-    int top = kDeg - 1;
-    while (top >= 0 && !bit(g.data(), top)) --top;
+    constexpr int kQ = 8;
+    std::vector<uint32_t> ext(kN + kQ);                    // w's stream: x[0 .. 624 + kQ)
+    std::memcpy(ext.data(), w, kN * sizeof(uint32_t));
+    for (int k = kN; k < kN + kQ; ++k) ext[k] = ext[k - kN + kM] ^ mix(ext[k - kN], ext[k - kN + 1]);
+    std::vector<uint32_t> tab((size_t)(1 << kQ) * kN);
+    std::memset(tab.data(), 0, kN * sizeof(uint32_t));
+    for (int v = 1; v < (1 << kQ); ++v) {
+        const int top = 31 - __builtin_clz((unsigned)v);
+        const uint32_t* a = tab.data() + (size_t)(v ^ (1 << top)) * kN;
+        const uint32_t* b = ext.data() + top;
+        uint32_t* d = tab.data() + (size_t)v * kN;
+        for (int j = 0; j < kN; ++j) d[j] = a[j] ^ b[j];
+    }
     std::vector<uint32_t> buf(2 * kN, 0);
-    uint32_t* b = buf.data();
+    uint32_t* acc = buf.data();
     int s = 0;
-    for (int i = top; i >= 0; --i) {
-        b[s + kN] = b[s + kM] ^ mix(b[s], b[s + 1]);      // acc = F(acc)
-        if (++s == kN) {
-            std::memcpy(b, b + kN, kN * sizeof(uint32_t));
-            s = 0;
+    const int nblk = (kDeg + kQ - 1) / kQ;
+    bool started = false;
+    for (int blk = nblk - 1; blk >= 0; --blk) {
+        unsigned v = 0;
+        for (int j = 0; j < kQ; ++j) {
+            const int i = blk * kQ + j;
+            if (i < kDeg && bit(g.data(), i)) v |= 1u << j;
         }
-        if (bit(g.data(), i)) {                            // acc ^= w
-            uint32_t* a = b + s;
-            for (int j = 0; j < kN; ++j) a[j] ^= w[j];
+        if (started) {
+            for (int k = 0; k < kQ; ++k) {                  // acc = F^8 acc
+                acc[s + kN] = acc[s + kM] ^ mix(acc[s], acc[s + 1]);
+                if (++s == kN) {
+                    std::memcpy(acc, acc + kN, kN * sizeof(uint32_t));
+                    s = 0;
+                }
+            }
+        }
+        if (v) {
+            const uint32_t* t = tab.data() + (size_t)v * kN;
+            uint32_t* a = acc + s;
+            for (int j = 0; j < kN; ++j) a[j] ^= t[j];
+            started = true;
         }
     }
-    std::memcpy(out, b + s, kN * sizeof(uint32_t));
+    std::memcpy(out, acc + s, kN * sizeof(uint32_t));
 }
 
 }  // namespace
@@ -222,7 +253,9 @@ int mt_uniform_rows_par(Mt19937& g, const double* low, const double* high, int A
     const int64_t kw = keep_hi - keep_lo;
     std::vector<Mt19937> gs(T);
     std::vector<int> rcs(T, 0);
+    static const bool dbg = std::getenv("BCMPC_MT_DEBUG") != nullptr;
     auto work = [&](int t) {
+        const auto t0 = std::chrono::steady_clock::now();
         Mt19937& gt = gs[t];
         if (t == 0) {
             gt = g;
@@ -230,35 +263,88 @@ int mt_uniform_rows_par(Mt19937& g, const double* low, const double* high, int A
             mt_jump_blocks(g, (int64_t)t * M, gt);
             gt.pos = (int32_t)(pos0 + 2 * D[t] - (int64_t)kN * t * M);       // 0 or 1
         }
-        constexpr int64_t kChunk = 4096, kFlush = int64_t(1) << 18;   // doubles
-        double buf[kChunk];
+        const auto t1 = std::chrono::steady_clock::now();
+        constexpr int64_t kRows = 1024, kFlush = int64_t(1) << 18;   // rows per generator call; doubles
+        std::vector<double> bufv((size_t)(kRows * A));
+        double* buf = bufv.data();
         int64_t e = D[t];
-        int64_t r = e / A, j = e % A;
+        const int64_t e_end = D[t + 1];
+        int64_t r = e / A;                                 // current row, its place in the keep pattern
         int64_t rp = r % period, rq = r / period;
         int64_t o_lo = -1, o_hi = -1;
-        while (e < D[t + 1]) {
-            const int64_t n = std::min(kChunk, D[t + 1] - e);
+        // elements [j0, j0 + n) of row r (rp, rq) from d
+        auto emit = [&](int j0, const double* d, int n) {
+            if (rp < keep_lo || rp >= keep_hi) return;
+            const int64_t o = (rq * kw + (rp - keep_lo)) * A;
+            for (int i = 0; i < n; ++i) out[o + j0 + i] = low[j0 + i] + range[j0 + i] * d[i];   // mul, then add
+            if (o_lo < 0) o_lo = o + j0;
+            o_hi = o + j0 + n;
+        };
+        auto next_row = [&]() {
+            ++r;
+            if (++rp == period) { rp = 0; ++rq; }
+        };
+        if (e % A) {                                       // the head of a row the previous thread began
+            const int j0 = (int)(e % A);
+            const int n = (int)std::min<int64_t>(A - j0, e_end - e);
             mt_next_doubles(gt, buf, n);
-            for (int64_t i = 0; i < n; ++i) {
-                if (rp >= keep_lo && rp < keep_hi) {
-                    const int64_t o = (rq * kw + (rp - keep_lo)) * A + j;
-                    out[o] = low[j] + range[j] * buf[i];   // random_uniform: mul, then add
-                    if (o_lo < 0) o_lo = o;
-                    o_hi = o + 1;
-                }
-                if (++j == A) {
-                    j = 0;
-                    if (++rp == period) { rp = 0; ++rq; }
+            emit(j0, buf, n);
+            e += n;
+            if (j0 + n == A) next_row();
+        }
+        const bool all = keep_lo == 0 && keep_hi == period;   // every row kept: output index = e
+        std::vector<double> lowx, rangex;
+        if (all) {
+            lowx.resize((size_t)(kRows * A));
+            rangex.resize((size_t)(kRows * A));
+            for (int64_t i = 0; i < kRows * A; ++i) { lowx[i] = low[i % A]; rangex[i] = range[i % A]; }
+        }
+        while (e + A <= e_end) {                           // whole rows
+            const int64_t nr = std::min(kRows, (e_end - e) / A);
+            mt_next_doubles(gt, buf, nr * A);
+            if (all) {
+                double* o = out + e;
+                const double* lx = lowx.data();
+                const double* rx = rangex.data();
+                const int64_t n = nr * A;
+                int64_t i = 0;
+                if (((uintptr_t)o & 15) && n > 0) { o[0] = lx[0] + rx[0] * buf[0]; i = 1; }
+                // streaming stores: the output is read next by the DMA engine, not by this core
+                for (; i + 2 <= n; i += 2)
+                    _mm_stream_pd(o + i, _mm_add_pd(_mm_loadu_pd(lx + i), _mm_mul_pd(_mm_loadu_pd(rx + i),
+                                                                                     _mm_loadu_pd(buf + i))));
+                for (; i < n; ++i) o[i] = lx[i] + rx[i] * buf[i];
+                if (o_lo < 0) o_lo = e;
+                o_hi = e + nr * A;
+                r += nr;
+            } else {
+                for (int64_t i = 0; i < nr; ++i) {
+                    emit(0, buf + i * A, A);
+                    next_row();
                 }
             }
-            e += n;
+            e += nr * A;
             // hand finished output on in ~2 MiB pieces, so its copy overlaps the rest of the draw
             if (on_chunk && o_lo >= 0 && o_hi - o_lo >= kFlush && !rcs[t]) {
+                _mm_sfence();
                 rcs[t] = on_chunk(o_lo, o_hi);
                 o_lo = -1;
             }
         }
+        if (e < e_end) {                                   // the start of a row the next thread ends
+            const int n = (int)(e_end - e);
+            mt_next_doubles(gt, buf, n);
+            if (all) { rp = r % period; rq = r / period; }
+            emit(0, buf, n);
+        }
+        _mm_sfence();                                      // streaming stores visible before any copy
         if (on_chunk && o_lo >= 0 && !rcs[t]) rcs[t] = on_chunk(o_lo, o_hi);
+        if (dbg) {
+            const auto t2 = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "mt thread %d: jump %.3f ms, draw %.3f ms (%lld doubles)\n", t,
+                         std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                         std::chrono::duration<double, std::milli>(t2 - t1).count(), (long long)(D[t + 1] - D[t]));
+        }
     };
     std::vector<std::thread> pool;
     pool.reserve(T - 1);
