@@ -16,9 +16,12 @@
 
 using namespace bcmpc;
 
-// a host thread of the split NumPy-stream draw gets at least this many generator words (~1 ms of
-// drawing): below it the jump-ahead (~0.3 ms per thread) does not pay
-static constexpr int64_t kMtMinWordsPerThread = int64_t(1) << 20;
+// a host thread of the split NumPy-stream draw gets at least this many generator words
+// (BCMPC_MT_MIN_WORDS overrides): below it the jump-ahead (~0.1 ms per thread) does not pay
+static int64_t mt_min_words() {
+    const char* v = std::getenv("BCMPC_MT_MIN_WORDS");
+    return (v && *v) ? std::max<int64_t>(1, std::atoll(v)) : int64_t(1) << 20;
+}
 
 namespace {
 
@@ -895,20 +898,28 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     g.pos = *mt_pos;
     // Large draws: the stream split over host threads by jump-ahead (mt_jump.cpp); each thread
     // copies its own slice as soon as it is drawn.  Otherwise [H, k_global, A] in C order, one
-    // step at a time: step h's slice of this shard is copied while step h+1 is drawn.
+    // step at a time, the drawn steps copied while the next ones are drawn.
     int chunk_rc = 0;
     auto copy_chunk = [&](int64_t o_lo, int64_t o_hi) -> int {
         return hipMemcpyAsync(e->d_actions + o_lo, e->h_stage + o_lo, (size_t)(o_hi - o_lo) * sizeof(double),
                               hipMemcpyHostToDevice, e->stream) == hipSuccess ? 0 : 1;
     };
     if (mt_uniform_rows_par(g, low, high, A, (int64_t)H * k_global, k_global, cand_offset, cand_offset + K,
-                            e->h_stage, mt_default_threads(), kMtMinWordsPerThread, copy_chunk, &chunk_rc) > 0) {
+                            e->h_stage, mt_default_threads(), mt_min_words(), copy_chunk, &chunk_rc) > 0) {
         if (chunk_rc) return fail(BCMPC_ERR_HIP, "hipMemcpyAsync of a drawn action slice failed");
     } else {
+        // copies go out in pieces of >= 2 MiB (one per call for small draws: each copy costs ~5-10 us
+        // of runtime overhead)
+        constexpr size_t kPiece = size_t(1) << 18;   // doubles
+        int h_sent = 0;
         for (int h = 0; h < H; ++h) {
             mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_stage + h * row);
-            HIP_TRY(hipMemcpyAsync(e->d_actions + h * row, e->h_stage + h * row, row * sizeof(double),
-                                   hipMemcpyHostToDevice, e->stream));
+            if ((size_t)(h + 1 - h_sent) * row >= kPiece || h + 1 == H) {
+                HIP_TRY(hipMemcpyAsync(e->d_actions + h_sent * row, e->h_stage + h_sent * row,
+                                       (size_t)(h + 1 - h_sent) * row * sizeof(double), hipMemcpyHostToDevice,
+                                       e->stream));
+                h_sent = h + 1;
+            }
         }
     }
     std::memcpy(mt_key, g.key, sizeof(g.key));
@@ -948,7 +959,7 @@ int bcmpc_mt19937_uniform_par(uint32_t* mt_key, int32_t* mt_pos, const double* l
     std::memcpy(g.key, mt_key, sizeof(g.key));
     g.pos = *mt_pos;
     if (threads <= 0) threads = mt_default_threads();
-    if (min_words_per_thread < 0) min_words_per_thread = kMtMinWordsPerThread;
+    if (min_words_per_thread < 0) min_words_per_thread = mt_min_words();
     const int used = mt_uniform_rows_par(g, low, high, action_dim, n_rows, period, keep_lo, keep_hi, out, threads,
                                          min_words_per_thread, nullptr, nullptr);
     const bool par = used > 0;
