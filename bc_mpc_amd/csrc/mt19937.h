@@ -64,14 +64,17 @@ int mt_default_threads();
 // out = the state at the start of block `blocks` (>= 1) after g's key block: key = that block's
 // 624 raw words, pos = 0 (the words twist(g.key) would hold after `blocks` twists)
 void mt_jump_blocks(const Mt19937& g, int64_t blocks, Mt19937& out);
-// The same draw as mt_uniform_rows over n_rows rows, split over up to `threads` host threads
-// (each >= min_words_per_thread generator words), for a keep set that repeats with `period` rows:
+// out = g advanced by `words` generator words (a jump to the block that holds the word, then its position)
+void mt_state_at(const Mt19937& g, int64_t words, Mt19937& out);
+// The same draw as mt_uniform_rows over n_rows rows, for a keep set that repeats with `period` rows:
 // row r is kept iff r % period is in [keep_lo, keep_hi) and lands at output row
-// (r / period) * (keep_hi - keep_lo) + r % period - keep_lo.  Every thread hands its kept output
-// output in ranges [o_lo, o_hi) (doubles, ~2 MiB each) to on_chunk as they are written (from that
-// thread, in order); the first
-// nonzero on_chunk result lands in *chunk_rc.  Returns the number of threads used, or 0 (nothing
-// drawn) when the draw is too small to split; g is advanced exactly as the serial draw advances it.
+// (r / period) * (keep_hi - keep_lo) + r % period - keep_lo.  The kept rows are split over up to
+// `threads` host threads (each >= min_words_per_thread generator words); a thread jumps to the start
+// of every run of kept rows it draws, so a shard's draw costs its own rows plus one jump per run, not
+// the whole stream.  Each thread hands its output on in ranges [o_lo, o_hi) (doubles, ~2 MiB each)
+// to on_chunk as they are written (from that thread, in order); the first nonzero on_chunk result
+// lands in *chunk_rc.  Returns the number of threads used, or 0 (nothing drawn) when the kept draw
+// is too small to split; g ends exactly where NumPy's one draw of all n_rows rows leaves it.
 int mt_uniform_rows_par(Mt19937& g, const double* low, const double* high, int A, int64_t n_rows, int64_t period,
                          int64_t keep_lo, int64_t keep_hi, double* out, int threads, int64_t min_words_per_thread,
                          const std::function<int(int64_t, int64_t)>& on_chunk, int* chunk_rc);

@@ -234,116 +234,103 @@ void mt_jump_blocks(const Mt19937& g, int64_t blocks, Mt19937& out) {
     out.pos = 0;
 }
 
+void mt_state_at(const Mt19937& g, int64_t words, Mt19937& out) {
+    const int64_t p = g.pos + words;                     // word index relative to g's key block
+    const int64_t f = p / kN;
+    if (f == 0) {
+        out = g;
+    } else {
+        mt_jump_blocks(g, f, out);
+    }
+    out.pos = (int32_t)(p - f * kN);
+}
+
 int mt_uniform_rows_par(Mt19937& g, const double* low, const double* high, int A, int64_t n_rows, int64_t period,
-                         int64_t keep_lo, int64_t keep_hi, double* out, int threads, int64_t min_words_per_thread,
-                         const std::function<int(int64_t, int64_t)>& on_chunk, int* chunk_rc) {
-    const int64_t ntot = n_rows * A;                      // doubles
-    const int64_t words = 2 * ntot;
+                        int64_t keep_lo, int64_t keep_hi, double* out, int threads, int64_t min_words_per_thread,
+                        const std::function<int(int64_t, int64_t)>& on_chunk, int* chunk_rc) {
+    if (period < 1 || n_rows % period || keep_lo < 0 || keep_hi > period || keep_lo >= keep_hi) return 0;
+    const int64_t nper = n_rows / period, kw = keep_hi - keep_lo;
+    const int64_t rows_k = nper * kw;                    // kept rows (= output rows)
+    const int64_t words_k = 2 * rows_k * A;              // generator words behind them
     int T = threads;
-    if (min_words_per_thread > 0) T = (int)std::min<int64_t>(T, words / min_words_per_thread);
-    const int64_t M = T > 0 ? words / ((int64_t)kN * T) : 0;   // blocks per thread
-    if (T < 2 || M < 1) return 0;
-    const int pos0 = g.pos;
-    std::vector<int64_t> D(T + 1);
-    D[0] = 0;
-    for (int t = 1; t < T; ++t) D[t] = ((int64_t)kN * t * M - pos0 + 1) / 2;   // first double starting in block tM
-    D[T] = ntot;
+    if (min_words_per_thread > 0) T = (int)std::min<int64_t>(T, words_k / min_words_per_thread);
+    T = (int)std::min<int64_t>(T, rows_k);
+    if (T < 2) return 0;
+    // kept runs of global rows [r0, r1) -> output rows from o0 (one run per period, merged when
+    // they touch: a whole-draw keep is one run); every thread jumps to the start of each run it
+    // touches, so a shard draws only its own rows (plus one jump per run)
+    struct Run { int64_t r0, r1, o0; };
+    std::vector<Run> runs;
+    for (int64_t p = 0; p < nper; ++p) {
+        const int64_t r0 = p * period + keep_lo, r1 = p * period + keep_hi;
+        if (!runs.empty() && runs.back().r1 == r0) runs.back().r1 = r1;
+        else runs.push_back({r0, r1, p * kw});
+    }
     double range[64];
     for (int j = 0; j < A; ++j) range[j] = high[j] - low[j];   // np.subtract(high, low)
-    const int64_t kw = keep_hi - keep_lo;
+    constexpr int64_t kRows = 1024, kFlush = int64_t(1) << 18;   // rows per generator call; doubles
+    std::vector<double> lowx((size_t)(kRows * A)), rangex((size_t)(kRows * A));
+    for (int64_t i = 0; i < kRows * A; ++i) { lowx[i] = low[i % A]; rangex[i] = range[i % A]; }
     std::vector<Mt19937> gs(T);
+    std::vector<int64_t> last_end(T, -1);                 // global row each thread's generator stopped at
     std::vector<int> rcs(T, 0);
     static const bool dbg = std::getenv("BCMPC_MT_DEBUG") != nullptr;
     auto work = [&](int t) {
         const auto t0 = std::chrono::steady_clock::now();
-        Mt19937& gt = gs[t];
-        if (t == 0) {
-            gt = g;
-        } else {
-            mt_jump_blocks(g, (int64_t)t * M, gt);
-            gt.pos = (int32_t)(pos0 + 2 * D[t] - (int64_t)kN * t * M);       // 0 or 1
-        }
-        const auto t1 = std::chrono::steady_clock::now();
-        constexpr int64_t kRows = 1024, kFlush = int64_t(1) << 18;   // rows per generator call; doubles
+        double jump_ms = 0.0;
+        const int64_t oa = rows_k * t / T, ob = rows_k * (t + 1) / T;   // this thread's output rows
         std::vector<double> bufv((size_t)(kRows * A));
         double* buf = bufv.data();
-        int64_t e = D[t];
-        const int64_t e_end = D[t + 1];
-        int64_t r = e / A;                                 // current row, its place in the keep pattern
-        int64_t rp = r % period, rq = r / period;
-        int64_t o_lo = -1, o_hi = -1;
-        // elements [j0, j0 + n) of row r (rp, rq) from d
-        auto emit = [&](int j0, const double* d, int n) {
-            if (rp < keep_lo || rp >= keep_hi) return;
-            const int64_t o = (rq * kw + (rp - keep_lo)) * A;
-            for (int i = 0; i < n; ++i) out[o + j0 + i] = low[j0 + i] + range[j0 + i] * d[i];   // mul, then add
-            if (o_lo < 0) o_lo = o + j0;
-            o_hi = o + j0 + n;
-        };
-        auto next_row = [&]() {
-            ++r;
-            if (++rp == period) { rp = 0; ++rq; }
-        };
-        if (e % A) {                                       // the head of a row the previous thread began
-            const int j0 = (int)(e % A);
-            const int n = (int)std::min<int64_t>(A - j0, e_end - e);
-            mt_next_doubles(gt, buf, n);
-            emit(j0, buf, n);
-            e += n;
-            if (j0 + n == A) next_row();
-        }
-        const bool all = keep_lo == 0 && keep_hi == period;   // every row kept: output index = e
-        std::vector<double> lowx, rangex;
-        if (all) {
-            lowx.resize((size_t)(kRows * A));
-            rangex.resize((size_t)(kRows * A));
-            for (int64_t i = 0; i < kRows * A; ++i) { lowx[i] = low[i % A]; rangex[i] = range[i % A]; }
-        }
-        while (e + A <= e_end) {                           // whole rows
-            const int64_t nr = std::min(kRows, (e_end - e) / A);
-            mt_next_doubles(gt, buf, nr * A);
-            if (all) {
-                double* o = out + e;
+        Mt19937& gt = gs[t];
+        int64_t at = -1;                                   // global row gt is positioned at
+        int64_t o_lo = -1, o_hi = -1;                      // output doubles written, not yet handed on
+        // first run holding output row oa
+        size_t ri = (size_t)(std::upper_bound(runs.begin(), runs.end(), oa,
+                                              [](int64_t o, const Run& r) { return o < r.o0; }) - runs.begin()) - 1;
+        for (int64_t o = oa; o < ob; ++ri) {
+            const Run& r = runs[ri];
+            const int64_t g0 = r.r0 + (o - r.o0);
+            const int64_t n_rows_here = std::min(ob - o, (r.r1 - r.r0) - (o - r.o0));
+            if (at != g0) {
+                const auto j0 = std::chrono::steady_clock::now();
+                mt_state_at(g, 2 * g0 * A, gt);
+                jump_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - j0).count();
+            }
+            for (int64_t done = 0; done < n_rows_here;) {
+                const int64_t nr = std::min(kRows, n_rows_here - done);
+                const int64_t n = nr * A;
+                mt_next_doubles(gt, buf, n);
+                double* dst = out + (o + done) * A;
                 const double* lx = lowx.data();
                 const double* rx = rangex.data();
-                const int64_t n = nr * A;
                 int64_t i = 0;
-                if (((uintptr_t)o & 15) && n > 0) { o[0] = lx[0] + rx[0] * buf[0]; i = 1; }
+                if (((uintptr_t)dst & 15) && n > 0) { dst[0] = lx[0] + rx[0] * buf[0]; i = 1; }
                 // streaming stores: the output is read next by the DMA engine, not by this core
                 for (; i + 2 <= n; i += 2)
-                    _mm_stream_pd(o + i, _mm_add_pd(_mm_loadu_pd(lx + i), _mm_mul_pd(_mm_loadu_pd(rx + i),
-                                                                                     _mm_loadu_pd(buf + i))));
-                for (; i < n; ++i) o[i] = lx[i] + rx[i] * buf[i];
-                if (o_lo < 0) o_lo = e;
-                o_hi = e + nr * A;
-                r += nr;
-            } else {
-                for (int64_t i = 0; i < nr; ++i) {
-                    emit(0, buf + i * A, A);
-                    next_row();
+                    _mm_stream_pd(dst + i, _mm_add_pd(_mm_loadu_pd(lx + i), _mm_mul_pd(_mm_loadu_pd(rx + i),
+                                                                                       _mm_loadu_pd(buf + i))));
+                for (; i < n; ++i) dst[i] = lx[i] + rx[i] * buf[i];   // random_uniform: mul, then add
+                if (o_lo < 0) o_lo = (o + done) * A;
+                o_hi = (o + done + nr) * A;
+                done += nr;
+                // hand finished output on in ~2 MiB pieces, so its copy overlaps the rest of the draw
+                if (on_chunk && o_hi - o_lo >= kFlush && !rcs[t]) {
+                    _mm_sfence();
+                    rcs[t] = on_chunk(o_lo, o_hi);
+                    o_lo = -1;
                 }
             }
-            e += nr * A;
-            // hand finished output on in ~2 MiB pieces, so its copy overlaps the rest of the draw
-            if (on_chunk && o_lo >= 0 && o_hi - o_lo >= kFlush && !rcs[t]) {
-                _mm_sfence();
-                rcs[t] = on_chunk(o_lo, o_hi);
-                o_lo = -1;
-            }
-        }
-        if (e < e_end) {                                   // the start of a row the next thread ends
-            const int n = (int)(e_end - e);
-            mt_next_doubles(gt, buf, n);
-            if (all) { rp = r % period; rq = r / period; }
-            emit(0, buf, n);
+            o += n_rows_here;
+            at = g0 + n_rows_here;
         }
         _mm_sfence();                                      // streaming stores visible before any copy
         if (on_chunk && o_lo >= 0 && !rcs[t]) rcs[t] = on_chunk(o_lo, o_hi);
+        last_end[t] = at;
         if (dbg) {
-            const auto t2 = std::chrono::steady_clock::now();
-            std::fprintf(stderr, "mt thread %d: jump %.3f ms, draw %.3f ms (%lld doubles)\n", t,
-                         std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                         std::chrono::duration<double, std::milli>(t2 - t1).count(), (long long)(D[t + 1] - D[t]));
+            const double all_ms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            std::fprintf(stderr, "mt thread %d: jumps %.3f ms, total %.3f ms (%lld rows)\n", t, jump_ms, all_ms,
+                         (long long)(ob - oa));
         }
     };
     std::vector<std::thread> pool;
@@ -351,7 +338,17 @@ int mt_uniform_rows_par(Mt19937& g, const double* low, const double* high, int A
     for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
     work(0);
     for (auto& th : pool) th.join();
-    g = gs[T - 1];
+    if (last_end[T - 1] == n_rows) {
+        g = gs[T - 1];                                     // it drew the stream's last word
+    } else {                                               // NumPy's representation: the block of the last word
+        const int64_t p = g.pos + 2 * n_rows * A;
+        const int64_t q = (p + kN - 1) / kN - 1;
+        Mt19937 fin;
+        if (q == 0) fin = g;
+        else mt_jump_blocks(g, q, fin);
+        fin.pos = (int32_t)(p - q * kN);
+        g = fin;
+    }
     if (chunk_rc) {
         *chunk_rc = 0;
         for (int t = 0; t < T; ++t)

@@ -101,3 +101,24 @@ def test_threaded_default_threshold_large_draw():
     assert used == 1
     assert np.array_equal(got.reshape(3, 100, 6), small)
     assert np.array_equal(key, st_small[1]) and pos == st_small[2]
+
+
+def test_shard_draw_jumps_over_other_ranks_rows():
+    """A rank's slice of every step at multi-GPU sizes (rank 1 of 4, K_global = 32768, H = 20): the
+    threads jump over the other ranks' rows (one jump per run of kept rows) and still land on NumPy's
+    values and NumPy's final state."""
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    low, high = -np.ones(6), np.ones(6)
+    H, Kg, N, r = 20, 32768, 4, 1
+    lo, hi = r * Kg // N, (r + 1) * Kg // N
+    np.random.seed(4242)
+    np.random.random(5)
+    st = np.random.get_state()
+    want = np.random.uniform(low=low, high=high, size=[H, Kg, 6])[:, lo:hi]
+    st_after = np.random.get_state()
+    np.random.set_state(st)
+    got, key, pos, used = _draw_par(lib, low, high, H * Kg, Kg, lo, hi, 8, 1 << 16)
+    assert used == 8
+    assert np.array_equal(got.reshape(H, hi - lo, 6), want)
+    assert np.array_equal(key, st_after[1]) and pos == st_after[2]
