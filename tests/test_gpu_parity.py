@@ -561,3 +561,34 @@ def test_dropin_threaded_numpy_stream_equals_host_array_path(pre_draws):
         out.append((a, ctrl.last_costs.copy(), np.random.get_state()))
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
     assert np.array_equal(out[0][2][1], out[1][2][1]) and out[0][2][2] == out[1][2][2]
+
+
+def test_numpy_stream_shards_equal_whole_draw():
+    """Multi-GPU parity mode on one card: two engines own the halves of K_global = 65536 (H = 6) and each
+    draws only its own rows of every step (jump-ahead over the other half, csrc/mt_jump.cpp).  Their cost
+    vectors concatenate to the single engine's, and every engine leaves the global stream where NumPy's
+    one draw leaves it."""
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    S, A, H, KG = 20, 6, 6, 65536
+    w = orc.synthetic_weights(S, A, 128, 2, "tanh", False)
+    norm = orc.synthetic_normalization(S, A)
+    state = orc.synthetic_state(norm)
+    low, high = -np.ones(A), np.ones(A)
+    np.random.seed(2024)
+    np.random.random(3)
+    st0 = np.random.get_state()
+    np.random.uniform(low, high, [H, KG, A])
+    st_want = np.random.get_state()
+    costs, states = [], []
+    for off, k in ((0, KG), (0, KG // 2), (KG // 2, KG // 2)):
+        eng = RolloutEngine(S, A, 128, 2, "tanh", False, H, k, device=0)
+        eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+        np.random.set_state(st0)
+        res = eng.get_action_numpy_stream(state, low, high, KG, cand_offset=off, return_costs=True)
+        costs.append(res.costs.copy())
+        states.append(np.random.get_state())
+        eng.close()
+    assert np.array_equal(np.concatenate(costs[1:]), costs[0])
+    for st in states:
+        assert np.array_equal(st[1], st_want[1]) and st[2] == st_want[2]
