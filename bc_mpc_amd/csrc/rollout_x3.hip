@@ -67,6 +67,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef X3_DIAG_NOMFMA
 #define X3_DIAG_NOMFMA 0
 #endif
+#ifndef X3_DIAG_ONEPASS          // hidden layers: only the hi x hi MFMA pass (results inexact; timing only)
+#define X3_DIAG_ONEPASS 0
+#endif
 #ifndef X3_DIAG_LOADS            // 1: only hi fragments are loaded (lo = hi); 2: no weight loads in mm
 #define X3_DIAG_LOADS 0
 #endif
@@ -175,6 +178,7 @@ __device__ __forceinline__ void unit_x3(const h8 (&ah)[G], const h8 (&al)[G], co
     for (int c = 0; c < NC; ++c) {
 #pragma unroll
         for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bh[c], acc[g * G + j][c]);
+        if constexpr (X3_DIAG_ONEPASS) continue;       // timing only: the hi x hi pass alone
 #pragma unroll
         for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bl[c], acc[g * G + j][c]);
 #pragma unroll
