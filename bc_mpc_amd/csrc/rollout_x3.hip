@@ -67,9 +67,6 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef X3_DIAG_NOMFMA
 #define X3_DIAG_NOMFMA 0
 #endif
-#ifndef X3_COLHALF               // hidden layers swept in two column halves (weights streamed twice), the
-#define X3_COLHALF 0             // first half's epilogue interleaved with the second half's MFMAs
-#endif
 #ifndef X3_DIAG_ONEPASS          // hidden layers: only the hi x hi MFMA pass (results inexact; timing only)
 #define X3_DIAG_ONEPASS 0
 #endif
@@ -323,51 +320,6 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
     if constexpr (NG == 1) bread_x3<NC>(slab, kstep(NU - 1), lane, bh, bl);
     unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
-}
-
-// Column-half sweep (X3_COLHALF): acc[TW][NCH] += W * X[columns c0 .. c0+NCH) over the P k-steps in
-// the order k0, k0+1, ... (mod P), in units of TW/2 tiles (two per k-step) ping-ponged through two
-// register sets; s0h/s0l (TW tiles) arrive holding the first k-step's two units.  OWN: bar() after
-// this wave's own k-steps.  epi(u) runs after unit u's MFMAs are issued (independent VALU work to
-// interleave with them).  NEXT: the k-step at next_off (TW tiles) is loaded into s0h/s0l while the
-// last units run (the caller's next sweep starts with it).
-template <int TW, int NC, int NCH, int P, bool OWN, int PW, bool NEXT, typename Bar, typename Epi>
-__device__ __forceinline__ void mm_x3c(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NCH],
-                                       int lane, h8 (&s0h)[TW], h8 (&s0l)[TW], int c0, int k0, int next_off,
-                                       Bar bar, Epi epi) {
-    constexpr int G2 = TW / 2;
-    constexpr int NU = P * 2;
-    constexpr int STEPB = TW * 2048;
-    constexpr int NOWN = OWN ? PW * 2 : -1;
-    const int voff = lane * 16;
-    auto kstep = [&](int u) {
-        const int p = u / 2 + k0;
-        return p >= P ? p - P : p;
-    };
-    auto uoff = [&](int u) { return wbase + kstep(u) * STEPB + (u % 2) * G2 * 2048; };
-    h8 rh[2][G2], rl[2][G2], bh[NCH], bl[NCH], th[G2], tl[G2];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        if (u >= 1 && u + 1 < NU) aload_x3<G2>(rs, voff, uoff(u + 1), rh[(u + 1) & 1], rl[(u + 1) & 1], true);
-        __builtin_amdgcn_sched_barrier(0);              // keep the loads ahead of the MFMAs they overlap
-        if (u == NOWN) bar();                           // the other waves' k-steps from here on
-        if (u % 2 == 0) {
-#pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-                bh[c] = sread(slab + sidx<NC>(kstep(u), c0 + c, 0, lane));
-                bl[c] = sread(slab + sidx<NC>(kstep(u), c0 + c, 1, lane));
-            }
-        }
-        if (u < 2) {
-#pragma unroll
-            for (int j = 0; j < G2; ++j) { th[j] = s0h[u * G2 + j]; tl[j] = s0l[u * G2 + j]; }
-            unit_x3<TW, NCH, G2>(th, tl, bh, bl, u % 2, acc);
-        } else {
-            unit_x3<TW, NCH, G2>(rh[u & 1], rl[u & 1], bh, bl, u % 2, acc);
-        }
-        if (NEXT && u == NU - 2) aload_x3<TW>(rs, voff, next_off, s0h, s0l, true);
-        epi(u);
-    }
 }
 
 // Epilogue of one tile pair (k-step) for one column: BiasAdd (f32, after undoing
@@ -1072,39 +1024,6 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
             const float f = a.winv[l] * kAct;
-            constexpr bool CH = X3_COLHALF && X3_OWN && NC == 4 && AK == 0 && !RW && PHP == 0 && TW == G && TW % 2 == 0;
-            if constexpr (CH) {
-                // columns 0-1, then 2-3 with the weights streamed again; columns 0-1's epilogue
-                // runs between columns 2-3's MFMAs (one tile pair x column per operand unit)
-                f4 ca[TW][2], cb[TW][2];
-#pragma unroll
-                for (int j = 0; j < TW; ++j)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) { ca[j][c] = (f4){0.f, 0.f, 0.f, 0.f}; cb[j][c] = ca[j][c]; }
-                const __amdgpu_buffer_rsrc_t rsl = layer_rsrc(a.w[l], a.wbytes[l]);
-                const int wb = w * P * TW * 2048;
-                auto noepi = [](int) __attribute__((always_inline)) {};
-                auto nobar = []() __attribute__((always_inline)) {};
-                mm_x3c<TW, NC, 2, P, true, PW, true>(rsl, wb, slab, ca, lane, uh, ul, 0, kown, wb + kown * TW * 2048,
-                                                     ready, noepi);
-                auto epi_a = [&](int u) __attribute__((always_inline)) {
-                    if (u >= 2 && u < 2 + 2 * PW) {            // (units 0-1 still read the slab's k-step)
-                        const int pp = (u - 2) >> 1, c = (u - 2) & 1;
-                        epi_pair(ca[2 * pp][c], ca[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][c],
-                                 xl[pp][c]);
-                    }
-                };
-                mm_x3c<TW, NC, 2, P, false, PW, false>(rsl, wb, slab, cb, lane, uh, ul, 2, kown, 0, nobar, epi_a);
-                X3_ST(5);
-                load_next(l + 1);
-#pragma unroll
-                for (int pp = 0; pp < PW; ++pp)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        epi_pair(cb[2 * pp][c], cb[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q, xh[pp][2 + c],
-                                 xl[pp][2 + c]);
-                continue;
-            }
             // own k-steps first: this wave's slab writes need no barrier
             mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane,
                                                  uh, ul, kown, ready);
