@@ -4,7 +4,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
-OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o
+OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/rollout_x3_plain.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o
 HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h $(SRC)/argmin_common.h
 
 all: $(LIB)
@@ -17,9 +17,18 @@ build/rollout_grp.o: $(SRC)/rollout_grp.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# the split kernel in two units (X3_PART in rollout_x3.hip): the plain tanh delta net with the
+# iterative-ILP scheduler (-2% kernel time at cfg3, no spills), the policy / reward / relu-LN kernels
+# with the default one (iterative-ILP spills them)
+X3ILP    ?= -mllvm -amdgpu-sched-strategy=iterative-ilp
+
 build/rollout_x3.o: $(SRC)/rollout_x3.hip $(HDR)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DX3_PART=2 -c $< -o $@
+
+build/rollout_x3_plain.o: $(SRC)/rollout_x3.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) $(X3ILP) -DX3_PART=1 -c $< -o $@
 
 build/fit.o: $(SRC)/fit.hip $(HDR)
 	@mkdir -p build

@@ -1241,6 +1241,16 @@ void rollout_x3(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
+// X3_PART splits the instantiations over two translation units so each can be built with its own
+// scheduler (Makefile): 1 = the plain tanh delta net without a policy (cfg2..cfg5; built with
+// -amdgpu-sched-strategy=iterative-ilp, measured -2% kernel time at cfg3), 2 = everything else plus
+// the host helpers (the default scheduler: iterative-ilp spills the policy / reward / relu-LN
+// kernels), 0 = both in one unit (variant builds).
+#ifndef X3_PART
+#define X3_PART 0
+#endif
+hipError_t launch_rollout_x3_plain(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
+
 template <int HP, int NC, int NW, int PHP = 0, bool RW = false, int AK = 0>
 static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
     if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1, 0, 0, AK, NW) > 160 * 1024) {
@@ -1265,6 +1275,7 @@ static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
     }
 }
 
+#if X3_PART != 1
 int x3_waves(int hidden_padded) {
     switch (hidden_padded) {
         case 64: return 2;
@@ -1301,6 +1312,38 @@ size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int polic
                                    x3_waves(hidden_padded));
 }
 
+#endif  // X3_PART != 1
+
+// the plain tanh delta net without a policy (X3_PART 1)
+template <int NC>
+static hipError_t launch_x3_plain_nc(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+    switch (hidden_padded) {
+        case 64: return launch_x3_t<64, NC, 2>(a, st);
+        case 128: return launch_x3_t<128, NC, 4>(a, st);
+        case 256: return launch_x3_t<256, NC, 4>(a, st);
+        case 512: return launch_x3_t<512, NC, X3_NW512>(a, st);
+        case 768:
+            if constexpr (NC <= 2) return launch_x3_t<768, NC, 8>(a, st);
+            return hipErrorInvalidValue;
+        case 1024:
+            if constexpr (NC <= 2) return launch_x3_t<1024, NC, 8>(a, st);
+            return hipErrorInvalidValue;
+        default: return hipErrorInvalidValue;
+    }
+}
+
+#if X3_PART == 1 && !defined(X3_ONLY)
+hipError_t launch_rollout_x3_plain(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st) {
+    switch (nc) {
+        case 1: return launch_x3_plain_nc<1>(a, hidden_padded, st);
+        case 2: return launch_x3_plain_nc<2>(a, hidden_padded, st);
+        case 4: return launch_x3_plain_nc<4>(a, hidden_padded, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+#endif
+
+#if X3_PART != 1
 // relu and / or LayerNorm nets (AK != 0): the plain delta net, hidden <= 512
 template <int NC, int AK>
 static hipError_t launch_x3_ak(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
@@ -1361,19 +1404,11 @@ static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStrea
             default: return hipErrorInvalidValue;
         }
     }
-    switch (hidden_padded) {
-        case 64: return launch_x3_t<64, NC, 2>(a, st);
-        case 128: return launch_x3_t<128, NC, 4>(a, st);
-        case 256: return launch_x3_t<256, NC, 4>(a, st);
-        case 512: return launch_x3_t<512, NC, X3_NW512>(a, st);
-        case 768:
-            if constexpr (NC <= 2) return launch_x3_t<768, NC, 8>(a, st);
-            return hipErrorInvalidValue;
-        case 1024:
-            if constexpr (NC <= 2) return launch_x3_t<1024, NC, 8>(a, st);
-            return hipErrorInvalidValue;
-        default: return hipErrorInvalidValue;
-    }
+#if X3_PART == 0
+    return launch_x3_plain_nc<NC>(a, hidden_padded, st);
+#else
+    return launch_rollout_x3_plain(a, hidden_padded, NC, st);
+#endif
 #endif
 }
 
@@ -1385,5 +1420,6 @@ hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hi
         default: return hipErrorInvalidValue;
     }
 }
+#endif  // X3_PART != 1
 
 }  // namespace bcmpc

@@ -27,7 +27,7 @@ for spec in "$@"; do
     ( $H $flags -c bc_mpc_amd/csrc/rollout.hip -o build/variants/rollout_$name.o &&
       $H $flags -c bc_mpc_amd/csrc/rollout_grp.hip -o build/variants/rollout_grp_$name.o &&
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
-          build/variants/rollout_$name.o build/variants/rollout_grp_$name.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/rollout_x3.o \
+          build/variants/rollout_$name.o build/variants/rollout_grp_$name.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/rollout_x3.o build/rollout_x3_plain.o \
           build/variants/capi.o ) &
   fi
 done
