@@ -17,14 +17,16 @@ build/rollout_grp.o: $(SRC)/rollout_grp.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-# the split kernel in two units (X3_PART in rollout_x3.hip): the plain tanh delta net with the
-# iterative-ILP scheduler (-2% kernel time at cfg3, no spills), the policy / reward / relu-LN kernels
-# with the default one (iterative-ILP spills them)
+# the split kernel in two units (X3_PART in rollout_x3.hip), each with the scheduler that measured best
+# (profiles/r01_sched_ilp_ab.txt, profiles/r01_sched_part2_ab.txt): the plain tanh delta net with
+# iterative-ILP (-1..2% kernel time at cfg3/cfg4), the policy / reward / relu-LN kernels with max-ILP
+# (-0.6..1.7%; iterative-ILP spills the policy+reward kernel, +10%)
 X3ILP    ?= -mllvm -amdgpu-sched-strategy=iterative-ilp
+X3P2     ?= -mllvm -amdgpu-sched-strategy=max-ilp
 
 build/rollout_x3.o: $(SRC)/rollout_x3.hip $(HDR)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -DX3_PART=2 -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(X3P2) -DX3_PART=2 -c $< -o $@
 
 build/rollout_x3_plain.o: $(SRC)/rollout_x3.hip $(HDR)
 	@mkdir -p build

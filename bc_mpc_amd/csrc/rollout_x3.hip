@@ -1244,8 +1244,8 @@ void rollout_x3(const RolloutArgs a) {
 // X3_PART splits the instantiations over two translation units so each can be built with its own
 // scheduler (Makefile): 1 = the plain tanh delta net without a policy (cfg2..cfg5; built with
 // -amdgpu-sched-strategy=iterative-ilp, measured -2% kernel time at cfg3), 2 = everything else plus
-// the host helpers (the default scheduler: iterative-ilp spills the policy / reward / relu-LN
-// kernels), 0 = both in one unit (variant builds).
+// the host helpers (built with max-ilp: -0.6..1.7%; iterative-ilp spills the policy + reward
+// kernel), 0 = both in one unit (variant builds).
 #ifndef X3_PART
 #define X3_PART 0
 #endif
