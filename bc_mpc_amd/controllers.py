@@ -66,6 +66,18 @@ class RandomController(Controller):
         return self.env.action_space.sample()
 
 
+def _stock(fn):
+    """Mark a sample_random_actions body that is the reference's np.random.uniform draw verbatim:
+    get_action may then make that same draw in the library (same values, same stream advance)."""
+    fn._bcmpc_stock_sampler = True
+    return fn
+
+
+def _stock_sampler(obj) -> bool:
+    return ("sample_random_actions" not in obj.__dict__
+            and getattr(type(obj).sample_random_actions, "_bcmpc_stock_sampler", False))
+
+
 def _default_device() -> int:
     if "LOCAL_RANK" in os.environ:
         return int(os.environ["LOCAL_RANK"])
@@ -76,6 +88,13 @@ def _default_device() -> int:
     except Exception:  # pragma: no cover
         pass
     return 0
+
+
+def _comm_device(ctrl) -> int:
+    """The GPU of a controller's engine: the min-loc record goes through it under RCCL."""
+    if ctrl._engine is not None:
+        return ctrl._engine.device
+    return _default_device() if ctrl._device is None else ctrl._device
 
 
 class MPCcontroller(Controller):
@@ -115,6 +134,7 @@ class MPCcontroller(Controller):
         self.keep_costs = False
 
     # controllers.py:43-55
+    @_stock
     def sample_random_actions(self):
         np_action_paths = np.random.uniform(low=self.env.action_space.low, high=self.env.action_space.high,
                                             size=[self.horizon, self.num_simulated_paths,
@@ -172,8 +192,7 @@ class MPCcontroller(Controller):
             raise ValueError("attempt to get argmin of an empty sequence")
         # the reference's draw, made by the library straight into pinned memory and uploaded step
         # by step (same values, same stream advance) unless sample_random_actions is overridden
-        if (self.rng == "numpy" and fused and hi > lo and "sample_random_actions" not in self.__dict__
-                and type(self).sample_random_actions is MPCcontroller.sample_random_actions):
+        if self.rng == "numpy" and fused and hi > lo and _stock_sampler(self):
             eng = self._engine_for(spec, S, A, hi - lo, fused)
             eng.set_weights(spec, norm, version)
             res = eng.get_action_numpy_stream(state, self.env.action_space.low, self.env.action_space.high, K, lo,
@@ -181,7 +200,7 @@ class MPCcontroller(Controller):
             if res is not None:
                 self.last_costs = res.costs
                 cost, index, first_g = _dist.allgather_minloc(True, res.best_cost, res.best_index, res.first_action,
-                                                              A, self._group)
+                                                              A, self._group, device=_comm_device(self))
                 self.last_cost, self.last_index = cost, index
                 return first_g                               # = action_paths[0, index] (controllers.py:84-85)
 
@@ -207,7 +226,8 @@ class MPCcontroller(Controller):
                 valid, cost, index, first = True, float(costs[i]), lo + i, local[0, i, :].copy()
                 self.last_costs = costs
 
-        cost, index, first_g = _dist.allgather_minloc(valid, cost, index, first, A, self._group)
+        cost, index, first_g = _dist.allgather_minloc(valid, cost, index, first, A, self._group,
+                                                      device=_comm_device(self))
         self.last_cost, self.last_index = cost, index
         if action_paths is not None:
             opt_action_path = action_paths[:, index, :]     # controllers.py:84-85
@@ -282,6 +302,7 @@ class MPCcontrollerPolicyNet(Controller):
         self.keep_costs = False
 
     # controllers.py:181-186
+    @_stock
     def sample_random_actions(self):
         np_action_paths = np.random.uniform(low=self.env.action_space.low, high=self.env.action_space.high,
                                             size=[self.horizon, self.num_simulated_paths,
@@ -326,8 +347,7 @@ class MPCcontrollerPolicyNet(Controller):
         _check_model(spec, self._MODEL, type(self).__name__)
         pspec, pversion = _policy.extract(self.policy_net)
         sign = -1.0 if reward else 1.0                         # argmax(r) == argmin(-r), ties and NaN alike
-        if (K > 0 and hi > lo and "sample_random_actions" not in self.__dict__
-                and type(self).sample_random_actions is MPCcontrollerPolicyNet.sample_random_actions):
+        if K > 0 and hi > lo and _stock_sampler(self):
             # the exploration draw (controllers.py:191) made by the library into pinned memory,
             # same values and stream advance as sample_random_actions
             eng = self._engine_for(spec, pspec, S, A, hi - lo)
@@ -339,7 +359,7 @@ class MPCcontrollerPolicyNet(Controller):
                                                   lo, return_costs=self.keep_costs, seed=seed)
                 self.last_costs = res.costs
                 cost, index, first_g = _dist.allgather_minloc(True, sign * res.best_cost, res.best_index,
-                                                              res.first_action, A, self._group)
+                                                              res.first_action, A, self._group, device=_comm_device(self))
                 self.last_cost, self.last_index = sign * cost, index
                 return first_g
         exploration = self.sample_random_actions()           # every rank draws the full [H, K, A]
@@ -355,7 +375,8 @@ class MPCcontrollerPolicyNet(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, cost, index, first = True, res.best_cost, res.best_index, res.first_action
             self.last_costs = res.costs
-        cost, index, first_g = _dist.allgather_minloc(valid, sign * cost, index, first, A, self._group)
+        cost, index, first_g = _dist.allgather_minloc(valid, sign * cost, index, first, A, self._group,
+                                                      device=_comm_device(self))
         self.last_cost, self.last_index = sign * cost, index
         return first_g                                         # copy of action_paths[0, argmin] (:233-235)
 
@@ -473,7 +494,8 @@ class MPCcontrollerReward(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, neg, index, first = True, -res.best_cost, res.best_index, res.first_action
             self.last_rewards = res.costs
-        neg, index, first_g = _dist.allgather_minloc(valid, neg, index, first, A, self._group)
+        neg, index, first_g = _dist.allgather_minloc(valid, neg, index, first, A, self._group,
+                                                     device=_comm_device(self))
         self.last_reward, self.last_index = -neg, index
         if action_paths is not None:
             return copy.copy(action_paths[:, index, :][0])    # controllers.py:154-156
@@ -509,6 +531,7 @@ class MPCcontrollerPolicyNetReward(MPCcontrollerPolicyNet):
         self.gamma = gamma
 
     # controllers.py:310-316
+    @_stock
     def sample_random_actions(self):
         np_action_paths = np.random.uniform(low=self.env.action_space.low, high=self.env.action_space.high,
                                             size=[self.horizon, self.num_simulated_paths,

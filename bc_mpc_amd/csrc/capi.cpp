@@ -951,7 +951,7 @@ int bcmpc_mt19937_uniform(uint32_t* mt_key, int32_t* mt_pos, const double* low, 
 int bcmpc_mt19937_uniform_par(uint32_t* mt_key, int32_t* mt_pos, const double* low, const double* high,
                               int32_t action_dim, int64_t n_rows, int64_t period, int64_t keep_lo, int64_t keep_hi,
                               double* out, int32_t threads, int64_t min_words_per_thread, int32_t* used_threads) {
-    if (!mt_key || !mt_pos || !low || !high || !out || action_dim < 1 || action_dim > 64 || n_rows < 0 ||
+    if (!mt_key || !mt_pos || !low || !high || !out || action_dim < 1 || n_rows < 0 ||
         period < 1 || keep_lo < 0 || keep_hi > period || keep_lo >= keep_hi || n_rows % period)
         return fail(BCMPC_ERR_ARG, "bad argument");
     if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");

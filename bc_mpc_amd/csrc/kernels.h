@@ -102,6 +102,37 @@ struct RefitArgs {                           // per-(h, j) elite mean / std, smo
     int32_t iter, H, A;
     double alpha;
 };
+// ---- NumPy's legacy MT19937 stream drawn on the device (mt_device.hip) ----
+// One chunk = a contiguous range of the draw's generator words [s, s + n) (both even: whole
+// random_sample doubles), drawn by one workgroup starting from the 624-word window of stream block
+// f = floor(s / 624) (block 0 = the caller's key; block 1 = twist(key); block f >= 2 = jump
+// polynomial jidx applied to block 1), then written as uniforms to out[out0 ..).  final != 0: the
+// chunk ends the draw and leaves NumPy's (key, pos) in MtDrawArgs::final_state.
+struct MtChunk {
+    int64_t s;        // first draw word (relative to the caller's pos)
+    int64_t n;        // words (even)
+    int64_t out0;     // output double index of the first double, < 0: not stored
+    int32_t f;        // start block
+    int32_t jidx;     // jump polynomial (f >= 2), else -1
+    int32_t final_;   // 1: write final_state after the last word
+    int32_t j0;       // (s / 2) % A: action column of the first double
+};
+constexpr int kMtN = 624;
+constexpr int kMtPolyWords = 624;                // 19937 coefficient bits, padded to 624 u32
+constexpr int kMtStream = 32 * kMtPolyWords + 768; // words of the block-1 stream the jumps correlate with
+struct MtDrawArgs {
+    const uint32_t* in;        // [624] key, [624] = pos (NumPy's get_state()[1], [2])
+    const double* bounds;      // [2][A]: low, high (np.random.uniform's low / high as f64)
+    uint32_t* xs;              // [kMtStream] scratch: x[0..) = block 1 onwards
+    const uint32_t* polys;     // [Cj][kMtPolyWords] x^(624 (f - 1)) mod phi, bit i = coefficient of x^i
+    const MtChunk* chunks;     // [nchunks]
+    uint32_t* part;            // [Cj][S][624] scratch: partial jumped windows (XOR-combined)
+    uint32_t* final_state;     // [625] NumPy's key + pos after the whole draw
+    double* out;               // the shard's [H][K][A] action array
+    int32_t nchunks, Cj, S, A;
+};
+hipError_t launch_mt_draw(const MtDrawArgs& a, hipStream_t st);
+
 constexpr int kPolParams = 96;
 
 constexpr int kArgminParts = 256;

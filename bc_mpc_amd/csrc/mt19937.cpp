@@ -2,6 +2,7 @@
 #include "mt19937.h"
 
 #include <algorithm>
+#include <vector>
 
 namespace bcmpc {
 
@@ -47,7 +48,7 @@ void mt_next_doubles(Mt19937& g, double* dbl, int64_t m) {
 
 void mt_uniform_rows(Mt19937& g, const double* low, const double* high, int A, int64_t n_rows, int64_t keep_lo,
                      int64_t keep_hi, double* out) {
-    double range[64];
+    std::vector<double> range((size_t)A);                      // (any A: no fixed-size buffer)
     for (int j = 0; j < A; ++j) range[j] = high[j] - low[j];    // np.subtract(high, low)
     constexpr int64_t kRows = 2048;
     double buf[kRows * 16];

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include <functional>
+#include <vector>
 
 namespace bcmpc {
 
@@ -64,6 +65,9 @@ int mt_default_threads();
 // out = the state at the start of block `blocks` (>= 1) after g's key block: key = that block's
 // 624 raw words, pos = 0 (the words twist(g.key) would hold after `blocks` twists)
 void mt_jump_blocks(const Mt19937& g, int64_t blocks, Mt19937& out);
+// x^(624 (f - 1)) mod phi for each f (>= 1; the jump from a stream's block 1 to its block f), packed
+// as 624 u32 words per polynomial (bit i % 32 of word i / 32 = coefficient of x^i); cached per process
+void mt_block_polys(const std::vector<int64_t>& fs, uint32_t* out);
 // out = g advanced by `words` generator words (a jump to the block that holds the word, then its position)
 void mt_state_at(const Mt19937& g, int64_t words, Mt19937& out);
 // The same draw as mt_uniform_rows over n_rows rows, for a keep set that repeats with `period` rows:

@@ -26,6 +26,8 @@
 #include <vector>
 
 #include <emmintrin.h>
+#include <smmintrin.h>
+#include <wmmintrin.h>
 
 namespace bcmpc {
 
@@ -106,10 +108,80 @@ const Poly& phi_poly() {
     return phi;
 }
 
-// r (2*kPW words, degree < 2*kDeg) mod phi, in place
-void reduce(uint64_t* r, const Poly& phi) {
-    for (int64_t i = 2 * (int64_t)kDeg - 2; i >= kDeg; --i)
-        if (bit(r, i)) xor_shifted(r, phi.data(), kPW, i - kDeg);
+// r = a * b (carry-less), r: 2 * kPW + 1 words, zeroed by the caller
+__attribute__((target("pclmul,sse4.1")))
+void clmul_poly_hw(const uint64_t* a, const uint64_t* b, uint64_t* r) {
+    for (int i = 0; i < kPW; ++i) {
+        if (!a[i]) continue;
+        const __m128i ai = _mm_set_epi64x(0, (long long)a[i]);
+        for (int j = 0; j < kPW; ++j) {
+            const __m128i p = _mm_clmulepi64_si128(ai, _mm_set_epi64x(0, (long long)b[j]), 0x00);
+            r[i + j] ^= (uint64_t)_mm_cvtsi128_si64(p);
+            r[i + j + 1] ^= (uint64_t)_mm_extract_epi64(p, 1);
+        }
+    }
+}
+
+void clmul_poly_sw(const uint64_t* a, const uint64_t* b, uint64_t* r) {
+    for (int64_t i = 0; i < kDeg; ++i)
+        if (bit(a, i)) xor_shifted(r, b, kPW, i);
+}
+
+void clmul_poly(const uint64_t* a, const uint64_t* b, uint64_t* r) {
+    static const bool hw = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+    if (hw) clmul_poly_hw(a, b, r);
+    else clmul_poly_sw(a, b, r);
+}
+
+// the kPW low words of r >> s (r: nw words)
+Poly shr(const uint64_t* r, int nw, int64_t s) {
+    Poly o(kPW, 0);
+    const int64_t ws = s >> 6;
+    const int bs = (int)(s & 63);
+    for (int w = 0; w < kPW; ++w) {
+        const int64_t i = w + ws;
+        const uint64_t lo = i < nw ? r[i] : 0, hi = i + 1 < nw ? r[i + 1] : 0;
+        o[w] = bs ? (lo >> bs) | (hi << (64 - bs)) : lo;
+    }
+    return o;
+}
+
+// Barrett constant mu = floor(x^(2 kDeg) / phi) (degree kDeg), by long division once per process
+const Poly& barrett_mu() {
+    static const Poly mu = [] {
+        const Poly& phi = phi_poly();
+        Poly rem(2 * kPW + 1, 0), q(kPW, 0);
+        rem[(2 * kDeg) >> 6] |= 1ull << ((2 * kDeg) & 63);
+        for (int64_t i = 2 * (int64_t)kDeg; i >= kDeg; --i)
+            if (bit(rem.data(), i)) {
+                q[(size_t)(i - kDeg) >> 6] |= 1ull << ((i - kDeg) & 63);
+                xor_shifted(rem.data(), phi.data(), kPW, i - kDeg);
+            }
+        return q;
+    }();
+    return mu;
+}
+
+// r (2 kPW + 1 words, deg < 2 kDeg) mod phi into out (kPW words) by Barrett reduction:
+// q = ((r >> n) mu) >> n, out = r - q phi (exact over GF(2)); ~10x faster than the bitwise reduce
+void barrett_reduce(const uint64_t* r, uint64_t* out) {
+    const Poly& phi = phi_poly();
+    const Poly& mu = barrett_mu();
+    Poly t(2 * kPW + 1, 0), u(2 * kPW + 1, 0);
+    const Poly rh = shr(r, 2 * kPW + 1, kDeg);
+    clmul_poly(rh.data(), mu.data(), t.data());
+    const Poly q = shr(t.data(), 2 * kPW + 1, kDeg);
+    clmul_poly(q.data(), phi.data(), u.data());
+    for (int w = 0; w < kPW; ++w) out[w] = r[w] ^ u[w];
+    out[kPW - 1] &= (1ull << (kDeg & 63)) - 1;        // bits >= kDeg cancel exactly
+}
+
+// a * b mod phi
+Poly mulmod(const Poly& a, const Poly& b) {
+    Poly r(2 * kPW + 1, 0), out(kPW, 0);
+    clmul_poly(a.data(), b.data(), r.data());
+    barrett_reduce(r.data(), out.data());
+    return out;
 }
 
 // x^e mod phi
@@ -138,8 +210,8 @@ Poly x_pow_mod(uint64_t e) {
             sq[2 * w] = lo;
             sq[2 * w + 1] = hi;
         }
-        reduce(sq.data(), phi);
-        std::swap(r, sq);
+        barrett_reduce(sq.data(), r.data());
+        std::fill(r.begin() + kPW, r.end(), 0);
         if ((e >> b) & 1u) {                               // r = r * x mod phi
             for (int w = kPW; w > 0; --w) r[w] = (r[w] << 1) | (r[w - 1] >> 63);
             r[0] <<= 1;
@@ -213,7 +285,54 @@ void apply_poly(const Poly& g, const uint32_t* w, uint32_t* out) {
     std::memcpy(out, acc + s, kN * sizeof(uint32_t));
 }
 
+// cached x^(624 (f - 1)) mod phi: the jump from block 1 to block f of a stream (f >= 1)
+std::mutex g_fpoly_mu;
+std::map<int64_t, Poly> g_fpoly;
+
 }  // namespace
+
+void mt_block_polys(const std::vector<int64_t>& fs, uint32_t* out) {
+    std::vector<int64_t> want;
+    {
+        std::lock_guard<std::mutex> lk(g_fpoly_mu);
+        for (int64_t f : fs)
+            if (f >= 1 && !g_fpoly.count(f)) want.push_back(f);
+    }
+    std::sort(want.begin(), want.end());
+    want.erase(std::unique(want.begin(), want.end()), want.end());
+    if (!want.empty()) {
+        // sorted runs per thread: the run's first polynomial by square-and-multiply, the rest by one
+        // multiplication each with the (cached) step polynomial x^(624 (f_i - f_{i-1}))
+        const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)mt_default_threads(), (want.size() + 7) / 8));
+        for (int t = 0; t < T; ++t) {                    // the steps every run uses, once
+            const size_t a = want.size() * t / T, b = want.size() * (t + 1) / T;
+            for (size_t i = a + 1; i < b; ++i) (void)block_jump(want[i] - want[i - 1]);
+        }
+        std::vector<Poly> res(want.size());
+        auto work = [&](int t) {
+            const size_t a = want.size() * t / T, b = want.size() * (t + 1) / T;
+            for (size_t i = a; i < b; ++i) {
+                if (i == a) res[i] = x_pow_mod((uint64_t)kN * (uint64_t)(want[i] - 1));
+                else res[i] = mulmod(res[i - 1], block_jump(want[i] - want[i - 1]));
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+        work(0);
+        for (auto& th : pool) th.join();
+        std::lock_guard<std::mutex> lk(g_fpoly_mu);
+        for (size_t i = 0; i < want.size(); ++i) g_fpoly.emplace(want[i], std::move(res[i]));
+    }
+    std::lock_guard<std::mutex> lk(g_fpoly_mu);
+    for (size_t k = 0; k < fs.size(); ++k) {
+        const Poly& p = g_fpoly.at(std::max<int64_t>(1, fs[k]));
+        uint32_t* o = out + k * 624;
+        for (int w = 0; w < 312; ++w) {
+            o[2 * w] = (uint32_t)p[w];
+            o[2 * w + 1] = (uint32_t)(p[w] >> 32);
+        }
+    }
+}
 
 int mt_default_threads() {
     const char* e = std::getenv("BCMPC_MT_THREADS");
@@ -266,7 +385,7 @@ int mt_uniform_rows_par(Mt19937& g, const double* low, const double* high, int A
         if (!runs.empty() && runs.back().r1 == r0) runs.back().r1 = r1;
         else runs.push_back({r0, r1, p * kw});
     }
-    double range[64];
+    std::vector<double> range((size_t)A);
     for (int j = 0; j < A; ++j) range[j] = high[j] - low[j];   // np.subtract(high, low)
     constexpr int64_t kRows = 1024, kFlush = int64_t(1) << 18;   // rows per generator call; doubles
     std::vector<double> lowx((size_t)(kRows * A)), rangex((size_t)(kRows * A));

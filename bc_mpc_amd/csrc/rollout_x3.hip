@@ -79,6 +79,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef X3_STAMP                 // per-phase s_memtime totals, printed by two blocks at exit
 #define X3_STAMP 0
 #endif
+// The knobs above exist only for A/B timing builds: they are refused unless the build is a
+// tools/build_variants.sh variant (which defines BCMPC_DIAG_VARIANT and writes build/variants/,
+// loaded only through BCMPC_LIB); `make` / __graft_entry__.build() can never produce them.
+#if (X3_DIAG_NOTANH || X3_DIAG_SMALLW || X3_DIAG_NOOWNER || X3_DIAG_NOMFMA || X3_DIAG_ONEPASS || \
+     X3_DIAG_LOADS || X3_DIAG_NOBAR || X3_STAMP) && !defined(BCMPC_DIAG_VARIANT)
+#error "X3_DIAG_* / X3_STAMP are timing-only diagnostics (wrong results): build them with tools/build_variants.sh"
+#endif
 #define X3_ST(k)                                                        \
     do {                                                                \
         if constexpr (X3_STAMP) {                                       \

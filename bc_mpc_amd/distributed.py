@@ -64,8 +64,11 @@ def select(records: np.ndarray) -> np.ndarray:
 
 
 def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optional[np.ndarray],
-                     action_dim: int, group=None) -> Tuple[float, int, np.ndarray]:
-    """One collective per control step; returns the global (cost, index, first_action)."""
+                     action_dim: int, group=None, device: Optional[int] = None) -> Tuple[float, int, np.ndarray]:
+    """One collective per control step; returns the global (cost, index, first_action).
+    ``device``: the GPU this rank's engine runs on -- under nccl (RCCL) the record goes through
+    that device, so each rank's collective uses its own GPU even when the caller never called
+    torch.cuda.set_device (default: torch's current device)."""
     import torch
     import torch.distributed as dist
     rank, ws = world(group)
@@ -78,7 +81,10 @@ def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optiona
     if ws == 1:
         return float(rec[1]), int(rec[2]), rec[3:].copy()
     backend = dist.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    if backend == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
+    else:
+        dev = torch.device("cpu")
     t = torch.from_numpy(rec).to(dev)
     out = torch.empty(ws * rec.size, dtype=torch.float64, device=dev)
     dist.all_gather_into_tensor(out, t, group=group)

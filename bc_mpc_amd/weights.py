@@ -65,23 +65,29 @@ def is_reward_net(kernels) -> bool:
     return sh[1] == (h, h) and sh[3] == (h, h) and sh[2][0] == h and sh[4] == (h, 1)
 
 
-def _tf_weights(dyn_model) -> MLPSpec:  # pragma: no cover - TF1 is absent in this image
-    import tensorflow as tf
+def _tf_weights(dyn_model, tf=None) -> MLPSpec:
+    """Read NNDynamicsModel's variables (dynamics.py:54-71 under scope "NNDynamicsModel", :31)
+    through its session: ``dense{,_1,..}/{kernel,bias}:0`` and ``LayerNorm{,_1,..}/{gamma,beta}:0``
+    exactly (the Adam slots ``.../kernel/Adam:0`` are not fetched); the activation from the op
+    types under ``scope/dense``.  ``tf``: the tensorflow module (default: the imported one; TF1 is
+    absent in this image, tests install a stand-in)."""
+    if tf is None:
+        import tensorflow as tf
     scope = getattr(dyn_model, "scope", "NNDynamicsModel")
-    var_list = [v for v in tf.global_variables() if v.name.startswith(scope + "/")]
-    vals = dyn_model.sess.run(var_list)
-    by_name = {v.name: x for v, x in zip(var_list, vals)}
-
-    def idx(name, base):
-        m = re.match(rf"{scope}/{base}(?:_(\d+))?/", name)
-        return None if m is None else (0 if m.group(1) is None else int(m.group(1)))
-
-    dense = sorted({idx(n, "dense") for n in by_name if idx(n, "dense") is not None})
-    kernels = [by_name[f"{scope}/dense{'' if i == 0 else f'_{i}'}/kernel:0"] for i in dense]
-    biases = [by_name[f"{scope}/dense{'' if i == 0 else f'_{i}'}/bias:0"] for i in dense]
-    lns = sorted({idx(n, "LayerNorm") for n in by_name if idx(n, "LayerNorm") is not None})
-    g = [by_name[f"{scope}/LayerNorm{'' if i == 0 else f'_{i}'}/gamma:0"] for i in lns] or None
-    b = [by_name[f"{scope}/LayerNorm{'' if i == 0 else f'_{i}'}/beta:0"] for i in lns] or None
+    pat = re.compile(rf"{re.escape(scope)}/(dense|LayerNorm)(?:_(\d+))?/(kernel|bias|gamma|beta):0$")
+    found = {}
+    for v in tf.global_variables():
+        m = pat.match(v.name)
+        if m:
+            found[(m.group(1), 0 if m.group(2) is None else int(m.group(2)), m.group(3))] = v
+    keys = sorted(found)
+    vals = dict(zip(keys, dyn_model.sess.run([found[k] for k in keys])))
+    dense = sorted({i for (kind, i, _) in keys if kind == "dense"})
+    kernels = [vals[("dense", i, "kernel")] for i in dense]
+    biases = [vals[("dense", i, "bias")] for i in dense]
+    lns = sorted({i for (kind, i, _) in keys if kind == "LayerNorm"})
+    g = [vals[("LayerNorm", i, "gamma")] for i in lns] or None
+    b = [vals[("LayerNorm", i, "beta")] for i in lns] or None
     ops = {op.type for op in dyn_model.sess.graph.get_operations() if op.name.startswith(scope + "/dense")}
     act = "tanh" if "Tanh" in ops else "relu"
     model = "reward" if hasattr(dyn_model, "reward_predict") and is_reward_net(kernels) else "delta"

@@ -1,17 +1,26 @@
 #!/usr/bin/env python3
 """Benchmark: random-shooting MPC get_action on MI355X (libbcmpc).
 
-One "step" = one control step of MPCcontroller.get_action (controllers.py:57-88):
-fan out the state, roll K candidate action sequences H steps through the
-dynamics MLP, score them with the cheetah cost, argmin, return the first
-action to the host.  Inputs (state, [H, K, A] f64 actions) are resident in HBM
-before the timed region (synthetic HalfCheetah-dim data, random-init weights
-of the configured architecture).
+One "step" = one complete control step of MPCcontroller.get_action
+(controllers.py:57-88) through the library's synchronous entry point
+(bcmpc_get_action): the host state goes in, K candidate action sequences of
+horizon H are drawn on the device (Philox, ``--actions device``, default),
+rolled through the dynamics MLP, scored with the cheetah cost, argmin'd, and
+the result (index, cost, first action) comes back to the host.  ``p50_ms`` is
+the latency of that call; ``value`` = K*H*N / wall time.  ``--actions hbm``
+times the older resident-input rollout (a [H, K, A] f64 array uploaded once
+before timing) for A/B only.
+
+``dropin_parity_p50_ms``: ``bc_mpc_amd.MPCcontroller.get_action`` with the
+reference's RNG contract (rng="numpy": exactly the np.random.uniform(size=
+[H, K_global, A]) draw of controllers.py:53 from the global legacy stream,
+the first action taken from that array) at the same K and H -- the
+drop-in's latency including the draw.
 
 Multi-GPU (driver: torch.distributed.run, one rank per GPU): weak scaling --
 each rank owns K candidates of its own (global K = N*K); per step every rank
 runs its shard and the ranks agree on the global argmin through one
-all-gather (bc_mpc_amd.distributed).  Rank 0 prints ONE JSON line.
+all-gather of the 144-byte result records.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -77,45 +86,114 @@ def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None, reward=False):
     return f
 
 
-def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5, gamma=1.0, cem=None):
-    """The oracle (NumPy restatement of the reference path, kind "port") timed on
-    the host cores over a bounded sample of the same workload."""
-    from oracle import mpc_oracle as orc
-    reward = isinstance(spec_w, orc.RewardMLPWeights)
+def _cpu_model() -> str:
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5, gamma=1.0, cem=None):
+    """The oracle (NumPy restatement of the reference path, kind "port") timed on the host
+    cores: at the workload's FULL K with the BLAS pool's threads (calls until ``budget_s``), and
+    at 1 thread (one full-K call when that fits the budget, else a K sample).  CEM workloads
+    (cfg5: ~3 min per full-size oracle call) are sampled at K=1024."""
+    from oracle import mpc_oracle as orc
+    from threadpoolctl import threadpool_info, threadpool_limits
+    reward = isinstance(spec_w, orc.RewardMLPWeights)
+    threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     dyn = orc.NumpyRewardDynamics(spec_w, norm) if reward else orc.NumpyDynamics(spec_w, norm)
-    Ks = min(1024 if cem else 8192, K_full)
-    rs = np.random.RandomState(0)
     low, high = -np.ones(A_DIM), np.ones(A_DIM)
-    done, calls, t0 = 0, 0, time.perf_counter()
-    while True:
-        if cem:                           # the oracle's CEM loop: cem iterations x Ks x H candidate-steps
+
+    def one_call(Ks, calls, rs):
+        if cem:                           # the oracle's CEM loop: iterations x Ks x H candidate-steps
             E = max(1, int(round(cem["elite_frac"] * Ks)))
             orc.cem_get_action(lambda s, a: orc.rollout(dyn, s, a)[0], state, H, Ks, low, high, cem["iterations"],
                                E, cem["alpha"], calls, np.zeros((H, A_DIM)), np.full((H, A_DIM), 0.5))
-            done += Ks * H * (cem["iterations"] - 1)
-        elif reward and pol is None:        # MPCcontrollerReward body (env.sample stand-in: one uniform draw)
+            return Ks * H * cem["iterations"]
+        if reward and pol is None:        # MPCcontrollerReward body (env.sample stand-in: one uniform draw)
             orc.reward_rollout(dyn, state, rs.uniform(low, high, (H, Ks, A_DIM)), gamma)
         elif reward:
             orc.policy_reward_get_action(dyn, orc.NumpyPolicy(orc.PolicyWeights(*pol)), state, H, Ks, low, high,
                                          explore, rng=rs)
         elif pol is None:
-            orc.get_action(dyn, state, H, Ks, -np.ones(A_DIM), np.ones(A_DIM), rng=rs)
+            orc.get_action(dyn, state, H, Ks, low, high, rng=rs)
         else:
-            orc.policy_get_action(dyn, orc.NumpyPolicy(orc.PolicyWeights(*pol)), state, H, Ks, -np.ones(A_DIM),
-                                  np.ones(A_DIM), explore, rng=rs)
-        done += Ks * H
-        calls += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    el = time.perf_counter() - t0
-    return dict(value=done / el, unit="candidate-steps/s", cores=int(threads), kind="port",
-                sample=f"{calls} oracle get_action calls at K={Ks} (of the workload's K={K_full}), H={H}, "
-                       f"{net}, OpenBLAS {threads} threads, {el:.1f} s")
+            orc.policy_get_action(dyn, orc.NumpyPolicy(orc.PolicyWeights(*pol)), state, H, Ks, low, high,
+                                  explore, rng=rs)
+        return Ks * H
+
+    def timed(Ks, budget, max_calls=1 << 30):
+        rs = np.random.RandomState(0)
+        done, calls, t0 = 0, 0, time.perf_counter()
+        while calls < max_calls:
+            done += one_call(Ks, calls, rs)
+            calls += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        el = time.perf_counter() - t0
+        return done / el, calls, el
+
+    Ks = min(1024, K_full) if cem else K_full
+    v, calls, el = timed(Ks, budget_s)
+    per_call = el / calls
+    # 1 thread: one full-K call unless it would take over ~6x the budget (assumed linear in the pool size)
+    K1 = Ks if per_call * threads <= 6 * budget_s else max(256, int(Ks * 6 * budget_s / (per_call * threads)))
+    with threadpool_limits(limits=1, user_api="blas"):
+        v1, calls1, el1 = timed(K1, 0.0, max_calls=1)
+    return dict(value=v, unit="candidate-steps/s", cores=int(threads), kind="port", K_sampled=Ks,
+                value_1thread=v1, K_sampled_1thread=K1, cpu_model=_cpu_model(),
+                sample=f"{calls} oracle get_action calls at K={Ks} (workload K={K_full}), H={H}, {net}, "
+                       f"OpenBLAS {threads} threads, {el:.1f} s; 1 thread: {calls1} call at K={K1}, {el1:.1f} s")
+
+
+class _Space:
+    def __init__(self, n, lo=None, hi=None):
+        self.shape = (n,)
+        if lo is not None:
+            self.low, self.high = lo, hi
+
+
+class _Env:                        # HalfCheetah's spaces (cheetah_env.py:21-27; ctrlrange [-1, 1])
+    observation_space = _Space(S_DIM)
+    action_space = _Space(A_DIM, -np.ones(A_DIM, np.float32), np.ones(A_DIM, np.float32))
+
+
+def dropin_parity_p50(K_global, H, hidden, L, act, ln, kernels, biases, ln_g, ln_b, norm, state, device, calls,
+                      world):
+    """p50 of the drop-in ``bc_mpc_amd.MPCcontroller.get_action`` in parity mode (rng="numpy": the
+    reference's np.random.uniform draw of controllers.py:53 from the seeded global stream, the
+    first action taken from that array), host state in, host action out; every rank calls it
+    (K_global sharded over the ranks by the controller)."""
+    import torch
+    import torch.distributed as dist
+    from bc_mpc_amd import MPCcontroller, cheetah_cost_fn
+    from bc_mpc_amd.dynamics import NNDynamicsModel
+    dyn = NNDynamicsModel(_Env(), L, hidden, act, None, norm, 512, 1, 1e-3, layer_norm=ln, device=device)
+    dyn.load_weights(kernels, biases, ln_g, ln_b)
+    ctrl = MPCcontroller(_Env(), dyn, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K_global,
+                         device=device)
+    np.random.seed(0)                                  # train_mpc_ppo.py:499
+    for _ in range(3):
+        ctrl.get_action(state)
+    ts = []
+    for _ in range(calls):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        ctrl.get_action(state)
+        ts.append(time.perf_counter() - t0)
+    torch.cuda.synchronize(device)
+    p50 = float(np.median(ts))
+    out = {"p50_ms": p50 * 1e3, "p90_ms": float(np.percentile(ts, 90)) * 1e3, "calls": calls,
+           "cand_steps_per_s": K_global * H / p50, "K_global": K_global, "horizon": H,
+           "rng": "numpy legacy MT19937 stream (np.random.seed(0)), drawn by the library",
+           "mt_path": os.environ.get("BCMPC_MT_PATH", "default")}
+    ctrl._engine.close()
+    return out
 
 
 def main():
@@ -124,8 +202,12 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
-    ap.add_argument("--actions", default="hbm", choices=["hbm", "device"],
-                    help="hbm: [H,K,A] f64 actions resident in HBM (parity mode input); device: in-kernel Philox")
+    ap.add_argument("--actions", default="device", choices=["hbm", "device"],
+                    help="device: a complete get_action with in-kernel Philox actions (host state in, host result "
+                         "out); hbm: the rollout alone on a [H,K,A] f64 action array resident in HBM (A/B)")
+    ap.add_argument("--dropin-calls", type=int, default=20,
+                    help="MPCcontroller.get_action calls (rng='numpy', the reference's draw) timed for "
+                         "dropin_parity_p50_ms (0: skip)")
     ap.add_argument("--precision", default=os.environ.get("BCMPC_PRECISION", "auto"), choices=["auto", "fp32", "split"],
                     help="fp32: f32 MFMA (rollout_grp); split: f32-accurate hi/lo f16 MFMA (rollout_x3, tanh "
                          "NNDynamicsModel without LayerNorm; with a fused policy: hidden 449..1024); auto: split "
@@ -267,8 +349,16 @@ def main():
     def step(i):
         if cem:
             return cem_step(i)
-        eng.rollout_async(d_state.data_ptr(), 0, d_actions.data_ptr() if d_actions is not None else None,
-                          0xB0B + i, offset, d_costs.data_ptr(), None, d_res.data_ptr(), stream.cuda_stream)
+        if d_actions is None:
+            # the complete control step: state H2D, device-drawn actions, rollout, argmin, result D2H
+            res = eng.get_action(state, None, seed=0xB0B + i, cand_offset=offset)
+            if world == 1:
+                return res.best_cost, res.best_index, res.first_action
+            sign = -1.0 if reward else 1.0              # learned reward: argmax == argmin of -r
+            return bdist.allgather_minloc(True, sign * res.best_cost, res.best_index, res.first_action, A_DIM,
+                                          device=local)
+        eng.rollout_async(d_state.data_ptr(), 0, d_actions.data_ptr(), 0xB0B + i, offset, d_costs.data_ptr(), None,
+                          d_res.data_ptr(), stream.cuda_stream)
         # the min-loc exchange straight from the device result (stream-ordered after the argmin
         # launch), then one D2H of the gathered records (argmax for the learned reward)
         return bdist.allgather_result(d_res, A_DIM, maximize=reward)
@@ -294,6 +384,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    dropin = None
+    if args.dropin_calls > 0 and not (cem or policy or reward):
+        dropin = dropin_parity_p50(K * world, H, hidden, L, act, ln, kernels, biases, ln_g, ln_b, norm, state,
+                                   local, args.dropin_calls, world)
+
     total_cand_steps = K * world * H * iters * args.steps
     value = total_cand_steps / elapsed
     fpcs = flop_per_cand_step(hidden, L, policy=policy, reward=reward)
@@ -316,7 +411,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32" if eng.precision == "fp32" else "f32 (hi/lo f16 split operands, 3 MFMA passes, f32 accumulate)",
         "data": f"synthetic (HalfCheetah dims s=20,a=6; random-init {'two-head reward net' if reward else 'dynamics MLP'}; "
-                f"actions {'resident in HBM as [H,K,6] f64' if args.actions == 'hbm' else 'drawn in-kernel (Philox)'})",
+                f"actions {'resident in HBM as [H,K,6] f64, rollout only' if args.actions == 'hbm' else 'drawn in-kernel (Philox); step = complete get_action, host state in, host result out'})",
         "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
                                + (f"reward net {hidden} trunk + 2x{hidden} heads tanh, argmax sum r*{gamma}^h"
                                   if reward else f"{L}x{hidden} {act}" + (" + LayerNorm" if ln else ""))
@@ -324,13 +419,17 @@ def main():
                                   f"({wl.get('policy_mode', 'explore')})" if policy else "")
                                + (f" + CEM {iters} iterations, {n_elite} elites, alpha {cem['alpha']}" if cem else "")
                                + (", fp32 MFMA" if eng.precision == "fp32" else ", split-f16 MFMA (f32-accurate)")
-                               + ", 1 RCCL all-gather min-loc per step"
-                               + (" (+1 all-gather of the local top-E per CEM iteration)" if cem else ""),
+                               + (f", {world} ranks: 1 all-gather min-loc per step"
+                                  + (" (+1 all-gather of the local top-E per CEM iteration)" if cem else "")
+                                  if world > 1 else ", 1 GPU (no collective)"),
                    "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
                    "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
                    "collective": f"{backend} all_gather min-loc, {3 + A_DIM} f64 per rank per step" if world > 1
                    else "none (1 rank)"},
         "p50_ms": float(np.percentile(step_s, 50) * 1e3),
+        "dropin_parity_p50_ms": dropin["p50_ms"] if dropin else None,
+        "dropin_parity": dropin if dropin else "n/a (MPCcontroller drop-in is timed for the plain delta-net "
+                                                "workloads; policy / reward / CEM controllers: tools/bench_dropin.py)",
         "p90_ms": float(np.percentile(step_s, 90) * 1e3),
         "kernel_ms_avg": kern_avg_s * 1e3,
         "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": peak,

@@ -89,3 +89,81 @@ def test_tf_fit_hook_bumps_version():
     f.fit(None)
     f.fit(None)
     assert f._bcmpc_version == v0 + 2
+
+
+class _RecordingEngine:
+    """RolloutEngine stand-in recording which action source get_action took."""
+    calls = []
+
+    def __init__(self, *a, **k):
+        self.device = k.get("device", 0)
+
+    def set_action_bounds(self, low, high):
+        pass
+
+    def set_weights(self, spec, norm, version):
+        pass
+
+    def set_policy(self, spec, explore, version):
+        pass
+
+    def set_discount(self, gamma):
+        pass
+
+    def numpy_stream_available(self, low, high):
+        return True
+
+    def get_action_numpy_stream(self, state, low, high, k_global, cand_offset=0, return_costs=False, seed=0):
+        from bc_mpc_amd.engine import StepResult
+        _RecordingEngine.calls.append("numpy_stream")
+        return StepResult(0, 1.0, np.zeros(6))
+
+    def get_action(self, state, actions, seed=0, cand_offset=0, return_costs=False):
+        from bc_mpc_amd.engine import StepResult
+        _RecordingEngine.calls.append("host_array")
+        return StepResult(0, 1.0, np.zeros(6))
+
+    def close(self):
+        pass
+
+
+class _Box:
+    def __init__(self, n, lo, hi):
+        self.low, self.high, self.shape = np.full(n, lo, np.float32), np.full(n, hi, np.float32), (n,)
+
+
+class _Env:
+    action_space = _Box(6, -1, 1)
+    observation_space = _Box(20, -np.inf, np.inf)
+
+
+@pytest.mark.parametrize("cls", ["MPCcontroller", "MPCcontrollerPolicyNet", "MPCcontrollerPolicyNetReward"])
+def test_stock_samplers_take_the_library_draw(monkeypatch, cls):
+    """Every controller whose sample_random_actions is the reference's np.random.uniform body
+    (controllers.py:43-55, 181-186, 310-316) -- including the reward subclass, which restates its
+    own copy -- draws through the library (get_action_numpy_stream); an instance or subclass
+    override of the sampler falls back to the host array."""
+    from bc_mpc_amd import controllers as C
+    from bc_mpc_amd.cost_functions import cheetah_cost_fn
+    from oracle import mpc_oracle as orc
+    monkeypatch.setattr(C, "RolloutEngine", _RecordingEngine)
+    norm = orc.synthetic_normalization(reward=cls.endswith("Reward"))
+    if cls.endswith("Reward"):
+        dyn = orc.NumpyRewardDynamics(orc.synthetic_reward_weights(20, 6, 64), norm)
+    else:
+        dyn = orc.NumpyDynamics(orc.synthetic_weights(20, 6, 64, 2, "tanh", False), norm)
+    pol = orc.NumpyPolicy(orc.synthetic_policy())
+    make = {"MPCcontroller": lambda: C.MPCcontroller(_Env(), dyn, 3, cheetah_cost_fn, 8),
+            "MPCcontrollerPolicyNet": lambda: C.MPCcontrollerPolicyNet(_Env(), dyn, pol, 0.5, False, 3,
+                                                                       cheetah_cost_fn, 8),
+            "MPCcontrollerPolicyNetReward": lambda: C.MPCcontrollerPolicyNetReward(_Env(), dyn, pol, 0.5, False, 3,
+                                                                                   cheetah_cost_fn, 8)}[cls]
+    _RecordingEngine.calls = []
+    make().get_action(orc.synthetic_state(norm))
+    assert _RecordingEngine.calls == ["numpy_stream"]
+    # an override is the caller's own sampler: its array is used as is
+    ctrl = make()
+    ctrl.sample_random_actions = lambda: np.zeros((3, 8, 6))
+    _RecordingEngine.calls = []
+    ctrl.get_action(orc.synthetic_state(norm))
+    assert _RecordingEngine.calls == ["host_array"]

@@ -6,7 +6,7 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/variants
-H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize"
+H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -DBCMPC_DIAG_VARIANT"
 X3=0
 if [ "${1:-}" = "-x" ]; then X3=1; shift; fi
 make -s -j8 ARCH=gfx950 >/dev/null
