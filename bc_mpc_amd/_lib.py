@@ -147,6 +147,9 @@ SIGNATURES = [
     ("bcmpc_get_action_mt19937", ctypes.c_int,
      [ctypes.c_void_p, _DP, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP,
       ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.POINTER(Result), _DP]),
+    ("bcmpc_mt19937_uniform_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int64,
+      ctypes.c_int64, _DP]),
     ("bcmpc_mt19937_uniform", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int32, ctypes.c_int64,
       _DP]),

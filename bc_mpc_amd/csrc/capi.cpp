@@ -166,6 +166,17 @@ struct bcmpc_engine {
     double explore = 0.0;
     uint64_t pol_version = 0;
     bool has_policy = false;
+    // NumPy-stream draw on the device (bcmpc_get_action_mt19937, mt_device.hip): chunk plan and jump
+    // polynomials per (k_global, cand_offset), built on the first call of that shape
+    int64_t mt_kg = -1, mt_off = -1;
+    int32_t mt_nchunks = 0, mt_cj = 0, mt_s = 0;
+    uint32_t* d_mt_io = nullptr;        // [0, 625) key + pos in, [640, 1265) final key + pos out
+    double* d_mt_bounds = nullptr;      // [2][A] low, high
+    uint32_t* d_mt_xs = nullptr;        // [kMtStream]
+    uint32_t* d_mt_polys = nullptr;     // [Cj][kMtPolyWords]
+    MtChunk* d_mt_chunks = nullptr;
+    uint32_t* d_mt_part = nullptr;      // [Cj][S][624]
+    uint32_t* h_mt_io = nullptr;        // pinned mirror of d_mt_io (+ bounds at word 1280)
 };
 
 extern "C" {
@@ -392,10 +403,12 @@ int bcmpc_destroy(bcmpc_engine* e) {
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
                     (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
                     (void*)e->d_count, (void*)e->d_amin_c, (void*)e->d_amin_i,
-                    (void*)e->d_amin_ticket})
+                    (void*)e->d_amin_ticket, (void*)e->d_mt_io, (void*)e->d_mt_bounds, (void*)e->d_mt_xs,
+                    (void*)e->d_mt_polys, (void*)e->d_mt_chunks, (void*)e->d_mt_part})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -865,6 +878,138 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
     return BCMPC_OK;
 }
 
+// ---- NumPy-stream draw on the device -------------------------------------------------------
+// Generator words per chunk (one workgroup each; BCMPC_MT_CHUNK_WORDS overrides) and coefficient
+// slices per jump polynomial (BCMPC_MT_SPLITS): chunks trade jump work (one 624 x 19937 GF(2)
+// correlation each, ~0.24 us of the whole chip, VALU-bound) against serial generation (~0.5 words
+// per ns per workgroup).  cfg3 (15.7M words): 2^15 words -> 480 chunks x 17 slices, draw ~0.2 ms
+// (tools/mt_device_sweep.py, profiles/r02_mt_device_sweep.txt).
+static int64_t mt_chunk_words() {
+    const char* v = std::getenv("BCMPC_MT_CHUNK_WORDS");
+    return (v && *v) ? std::max<int64_t>(2, std::atoll(v)) & ~int64_t(1) : int64_t(1) << 15;
+}
+static int mt_splits(int cj) {
+    const char* v = std::getenv("BCMPC_MT_SPLITS");
+    if (v && *v) return std::max(1, std::min(64, std::atoi(v)));
+    return std::max(2, std::min(32, (8192 + cj - 1) / std::max(1, cj)));
+}
+static bool mt_device_path() {
+    const char* v = std::getenv("BCMPC_MT_PATH");
+    return !(v && std::strcmp(v, "host") == 0);
+}
+
+// The draw's chunks for this engine's shard of [H, k_global, A]: the shard's rows of step h are the
+// draw words [2A (h kg + off), 2A (h kg + off + K)) (one run; all steps merge into one when the shard
+// is the whole draw), each run cut into pieces of <= mt_chunk_words() words; the chunk that draws
+// the draw's last word also leaves NumPy's final state, else one extra chunk draws that word alone.
+static int mt_plan(bcmpc_engine* e, int64_t kg, int64_t off) {
+    if (e->mt_kg == kg && e->mt_off == off) return BCMPC_OK;
+    const int64_t K = e->cfg.num_paths, A = e->cfg.action_dim, H = e->cfg.horizon;
+    const int64_t N = 2 * A * H * kg;
+    struct Run { int64_t s, len, out0; };
+    std::vector<Run> runs;
+    if (off == 0 && K == kg) runs.push_back({0, N, 0});
+    else
+        for (int64_t h = 0; h < H; ++h) runs.push_back({2 * A * (h * kg + off), 2 * A * K, h * K * A});
+    const int64_t target = mt_chunk_words();
+    std::vector<MtChunk> ch;
+    bool has_final = false;
+    for (const Run& r : runs) {
+        const int64_t R = r.len / 2, P = std::max<int64_t>(1, (r.len + target - 1) / target);
+        for (int64_t p = 0; p < P; ++p) {
+            const int64_t d0 = R * p / P, d1 = R * (p + 1) / P;
+            if (d1 <= d0) continue;
+            MtChunk c{};
+            c.s = r.s + 2 * d0;
+            c.n = 2 * (d1 - d0);
+            c.out0 = r.out0 + d0;
+            c.f = (int32_t)(c.s / kMtN);
+            c.j0 = (int32_t)((c.s / 2) % A);
+            c.final_ = c.s + c.n == N;
+            has_final |= c.final_ != 0;
+            ch.push_back(c);
+        }
+    }
+    if (!has_final) {
+        MtChunk c{};
+        c.s = N - 2; c.n = 2; c.out0 = -1; c.f = (int32_t)((N - 2) / kMtN); c.final_ = 1;
+        ch.push_back(c);
+    }
+    std::vector<int64_t> fs;
+    for (MtChunk& c : ch) {
+        c.jidx = -1;
+        if (c.f >= 2) { c.jidx = (int32_t)fs.size(); fs.push_back(c.f); }
+    }
+    const int cj = (int)fs.size(), S = mt_splits(cj);
+    std::vector<uint32_t> polys((size_t)std::max(1, cj) * kMtPolyWords, 0);
+    if (cj) mt_block_polys(fs, polys.data());
+    for (void* p : {(void*)e->d_mt_polys, (void*)e->d_mt_chunks, (void*)e->d_mt_part})
+        if (p) (void)hipFree(p);
+    e->d_mt_polys = nullptr; e->d_mt_chunks = nullptr; e->d_mt_part = nullptr;
+    e->mt_kg = e->mt_off = -1;
+    if (!e->d_mt_io) {
+        HIP_TRY(hipMalloc(&e->d_mt_io, 1280 * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&e->d_mt_bounds, 2 * BCMPC_MAX_ACTION * sizeof(double)));
+        HIP_TRY(hipMalloc(&e->d_mt_xs, (size_t)kMtStream * sizeof(uint32_t)));
+        HIP_TRY(hipHostMalloc(&e->h_mt_io, 1280 * sizeof(uint32_t) + 2 * BCMPC_MAX_ACTION * sizeof(double),
+                              hipHostMallocDefault));
+    }
+    HIP_TRY(hipMalloc(&e->d_mt_polys, polys.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&e->d_mt_chunks, ch.size() * sizeof(MtChunk)));
+    HIP_TRY(hipMalloc(&e->d_mt_part, (size_t)std::max(1, cj) * S * kMtN * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(e->d_mt_polys, polys.data(), polys.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_mt_chunks, ch.data(), ch.size() * sizeof(MtChunk), hipMemcpyHostToDevice));
+    e->mt_nchunks = (int32_t)ch.size();
+    e->mt_cj = cj;
+    e->mt_s = S;
+    e->mt_kg = kg;
+    e->mt_off = off;
+    return BCMPC_OK;
+}
+
+static int ensure_actions(bcmpc_engine* e) {
+    const size_t n = (size_t)e->cfg.horizon * (size_t)e->cfg.num_paths * (size_t)e->cfg.action_dim;
+    if (n > e->actions_cap) {
+        if (e->d_actions) (void)hipFree(e->d_actions);
+        e->d_actions = nullptr;
+        e->actions_cap = 0;
+        HIP_TRY(hipMalloc(&e->d_actions, n * sizeof(double)));
+        e->actions_cap = n;
+    }
+    return BCMPC_OK;
+}
+
+// enqueue the draw of this shard's [H, K, A] from NumPy's state (key, pos) into e->d_actions and the
+// final state into d_mt_io[640..1265) (copied back by the caller after its sync)
+static int mt_draw_enqueue(bcmpc_engine* e, const uint32_t* mt_key, int32_t pos, const double* low,
+                           const double* high, int64_t kg, int64_t off) {
+    int rc = mt_plan(e, kg, off);
+    if (rc != BCMPC_OK) return rc;
+    rc = ensure_actions(e);
+    if (rc != BCMPC_OK) return rc;
+    const int A = e->cfg.action_dim;
+    std::memcpy(e->h_mt_io, mt_key, kMtN * sizeof(uint32_t));
+    e->h_mt_io[kMtN] = (uint32_t)pos;
+    double* hb = reinterpret_cast<double*>(e->h_mt_io + 1280);
+    for (int j = 0; j < A; ++j) { hb[j] = low[j]; hb[A + j] = high[j]; }
+    HIP_TRY(hipMemcpyAsync(e->d_mt_io, e->h_mt_io, (kMtN + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_mt_bounds, hb, 2 * A * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    MtDrawArgs a{};
+    a.in = e->d_mt_io;
+    a.bounds = e->d_mt_bounds;
+    a.xs = e->d_mt_xs;
+    a.polys = e->d_mt_polys;
+    a.chunks = e->d_mt_chunks;
+    a.part = e->d_mt_part;
+    a.final_state = e->d_mt_io + 640;
+    a.out = e->d_actions;
+    a.nchunks = e->mt_nchunks; a.Cj = e->mt_cj; a.S = e->mt_s; a.A = A;
+    HIP_TRY(launch_mt_draw(a, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->h_mt_io + 640, e->d_mt_io + 640, (kMtN + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           e->stream));
+    return BCMPC_OK;
+}
+
 int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_key, int32_t* mt_pos,
                              const double* low, const double* high, int64_t k_global, int64_t cand_offset,
                              uint64_t seed, bcmpc_result* out, double* costs_out) {
@@ -875,6 +1020,28 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         return fail(BCMPC_ERR_ARG, "this engine's candidates must lie inside [0, k_global)");
     if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
     HIP_TRY(hipSetDevice(c.device));
+    if (mt_device_path()) {
+        // the draw on the device: state + (key, pos) up, draw, rollout, argmin, result + final state down,
+        // one synchronisation.  NumPy's state is handed back only when the whole call succeeded.
+        HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
+        int rc = mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
+        if (rc == BCMPC_OK)
+            rc = rollout_impl(e, e->d_state, 0, e->d_actions, seed, cand_offset, e->d_costs, nullptr, e->d_result,
+                              e->stream);
+        if (rc == BCMPC_OK &&
+            hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            rc = fail(BCMPC_ERR_HIP, "result copy failed");
+        if (rc == BCMPC_OK && costs_out &&
+            hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            rc = fail(BCMPC_ERR_HIP, "costs copy failed");
+        const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: nothing left in flight)
+        if (rc != BCMPC_OK) return rc;
+        if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+        std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
+        *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];
+        *out = *e->h_result;
+        return BCMPC_OK;
+    }
     const int64_t K = c.num_paths;
     const int A = c.action_dim, H = c.horizon;
     const size_t row = (size_t)K * A, n = (size_t)H * row;
@@ -887,6 +1054,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     }
     if (n > e->stage_cap) {                       // pinned staging: the generator writes, the DMA reads
         if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
         e->h_stage = nullptr;
         e->stage_cap = 0;
         HIP_TRY(hipHostMalloc(&e->h_stage, n * sizeof(double), hipHostMallocDefault));
@@ -922,15 +1090,41 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             }
         }
     }
-    std::memcpy(mt_key, g.key, sizeof(g.key));
-    *mt_pos = g.pos;
     int rc = rollout_impl(e, e->d_state, 0, e->d_actions, seed, cand_offset, e->d_costs, nullptr, e->d_result, e->stream);
+    if (rc == BCMPC_OK &&
+        hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+        rc = fail(BCMPC_ERR_HIP, "result copy failed");
+    if (rc == BCMPC_OK && costs_out &&
+        hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * K, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+        rc = fail(BCMPC_ERR_HIP, "costs copy failed");
+    // (also on error: the staging buffer's copies are done before it can be reused)
+    const hipError_t se = hipStreamSynchronize(e->stream);
     if (rc != BCMPC_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream));
-    if (costs_out)
-        HIP_TRY(hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * K, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));   // (also: the staging buffer is free again)
+    if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+    std::memcpy(mt_key, g.key, sizeof(g.key));      // NumPy's state advances only when the call succeeded
+    *mt_pos = g.pos;
     *out = *e->h_result;
+    return BCMPC_OK;
+}
+
+int bcmpc_mt19937_uniform_device(bcmpc_engine* e, uint32_t* mt_key, int32_t* mt_pos, const double* low,
+                                 const double* high, int64_t k_global, int64_t cand_offset, double* out) {
+    if (!e || !mt_key || !mt_pos || !low || !high || !out) return fail(BCMPC_ERR_ARG, "null argument");
+    const bcmpc_config& c = e->cfg;
+    if (c.num_paths < 1 || k_global < c.num_paths || cand_offset < 0 || cand_offset + c.num_paths > k_global)
+        return fail(BCMPC_ERR_ARG, "this engine's candidates must lie inside [0, k_global)");
+    if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
+    HIP_TRY(hipSetDevice(c.device));
+    int rc = mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
+    const size_t n = (size_t)c.horizon * c.num_paths * c.action_dim;
+    if (rc == BCMPC_OK &&
+        hipMemcpyAsync(out, e->d_actions, n * sizeof(double), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+        rc = fail(BCMPC_ERR_HIP, "action copy failed");
+    const hipError_t se = hipStreamSynchronize(e->stream);
+    if (rc != BCMPC_OK) return rc;
+    if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+    std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
+    *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];
     return BCMPC_OK;
 }
 

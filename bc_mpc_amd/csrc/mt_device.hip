@@ -31,9 +31,11 @@ namespace bcmpc {
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kWave = 64;                 // mt_jump_kernel: one wave per (chunk, coefficient slice)
+constexpr int kGen = 256;                 // generators: 4 waves (a phase is 227 independent words)
 constexpr int kLag = 227;                 // 624 - 397: words producible in parallel
 constexpr int kRing = 2048;               // generator ring (words), power of two
+constexpr int kQ = 10;                    // jump: window words m per lane (64 x 10 >= 624)
 
 __device__ __forceinline__ uint32_t mix(uint32_t a, uint32_t b) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -48,10 +50,9 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
     return y;
 }
 
-// one phase: ring words [n0, n0 + 227) from the 624 before them (all threads; one barrier after)
+// one phase: ring words [n0, n0 + 227) from the 624 before them (227 independent words)
 __device__ __forceinline__ void gen_phase(uint32_t* ring, int64_t n0) {
-    const int t = threadIdx.x;
-    if (t < kLag) {
+    for (int t = threadIdx.x; t < kLag; t += kGen) {
         const int64_t n = n0 + t;
         ring[n & (kRing - 1)] = ring[(n - kLag) & (kRing - 1)] ^
                                 mix(ring[(n - kMtN) & (kRing - 1)], ring[(n - kMtN + 1) & (kRing - 1)]);
@@ -60,14 +61,13 @@ __device__ __forceinline__ void gen_phase(uint32_t* ring, int64_t n0) {
 }
 
 // x[0 .. kMtStream) = y[624 ..): block 1 onwards, the stream every jump correlates with
-__global__ __launch_bounds__(kThreads) void mt_stream_kernel(const uint32_t* __restrict__ in,
-                                                             uint32_t* __restrict__ xs) {
+__global__ __launch_bounds__(kGen) void mt_stream_kernel(const uint32_t* __restrict__ in,
+                                                         uint32_t* __restrict__ xs) {
     __shared__ uint32_t ring[kRing];
-    for (int i = threadIdx.x; i < kMtN; i += kThreads) ring[i] = in[i];
+    for (int i = threadIdx.x; i < kMtN; i += kGen) ring[i] = in[i];
     __syncthreads();
     for (int64_t n0 = kMtN; n0 < kMtN + kMtStream; n0 += kLag) {
-        const int t = threadIdx.x;
-        if (t < kLag) {
+        for (int t = threadIdx.x; t < kLag; t += kGen) {
             const int64_t n = n0 + t;
             const uint32_t v = ring[(n - kLag) & (kRing - 1)] ^
                                mix(ring[(n - kMtN) & (kRing - 1)], ring[(n - kMtN + 1) & (kRing - 1)]);
@@ -79,51 +79,61 @@ __global__ __launch_bounds__(kThreads) void mt_stream_kernel(const uint32_t* __r
 }
 
 // partial window of jump polynomial blockIdx.x / S over its coefficient words [w0, w1):
-// part[m] = XOR_{i in [32 w0, 32 w1), g_i = 1} x[i + m], m in [0, 624)
-__global__ __launch_bounds__(kThreads) void mt_jump_kernel(MtDrawArgs a) {
-    extern __shared__ uint32_t seg[];     // x[32 w0 .. 32 w1 + 768)
+// part[m] = XOR_{i in [32 w0, 32 w1), g_i = 1} x[i + m], m in [0, 624).  Lane l owns m = 10 l + q,
+// q < 10: per coefficient word it reads the 41 stream words x[32 w + 10 l .. + 41) once into
+// registers and XORs v[k + q] into acc[q] for every set bit k (a uniform branch per bit), i.e.
+// ~4 LDS words per 32 x 10 (term, m) pairs instead of one per pair.
+__global__ __launch_bounds__(kWave) void mt_jump_kernel(MtDrawArgs a) {
+    extern __shared__ uint32_t seg[];     // x[32 w0 .. 32 w1 + 32 + kWave kQ)
     const int j = blockIdx.x / a.S, sp = blockIdx.x % a.S;
     const int w0 = sp * kMtPolyWords / a.S, w1 = (sp + 1) * kMtPolyWords / a.S;
-    const int base = 32 * w0, len = 32 * (w1 - w0) + 768;
-    for (int i = threadIdx.x; i < len; i += kThreads) seg[i] = a.xs[base + i];
+    const int base = 32 * w0, len = 32 * (w1 - w0) + 32 + kWave * kQ;
+    for (int i = threadIdx.x; i < len; i += kWave) seg[i] = a.xs[base + i];
     __syncthreads();
-    const int t = threadIdx.x;
-    const bool third = t < kMtN - 2 * kThreads;          // m = t + 512 exists for t < 112
-    uint32_t acc0 = 0, acc1 = 0, acc2 = 0;
+    const int l = threadIdx.x;
+    uint32_t acc[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) acc[q] = 0;
     const uint32_t* g = a.polys + (size_t)j * kMtPolyWords;
     for (int w = w0; w < w1; ++w) {
-        uint32_t cw = __builtin_amdgcn_readfirstlane(g[w]);
-        const int ib = 32 * (w - w0);
-        while (cw) {                                      // uniform loop over the set coefficients
-            const int i = ib + __builtin_ctz(cw);
-            cw &= cw - 1;
-            acc0 ^= seg[i + t];
-            acc1 ^= seg[i + t + kThreads];
-            if (third) acc2 ^= seg[i + t + 2 * kThreads];
+        const uint32_t cw = __builtin_amdgcn_readfirstlane(g[w]);
+        if (!cw) continue;
+        const uint2* xp = reinterpret_cast<const uint2*>(seg + 32 * (w - w0) + kQ * l);   // 8-byte aligned
+        uint32_t v[32 + kQ];
+#pragma unroll
+        for (int t = 0; t < (32 + kQ) / 2; ++t) {
+            const uint2 p = xp[t];
+            v[2 * t] = p.x;
+            v[2 * t + 1] = p.y;
         }
+#pragma unroll
+        for (int k = 0; k < 32; ++k)
+            if (cw & (1u << k)) {
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) acc[q] ^= v[k + q];
+            }
     }
     uint32_t* p = a.part + (size_t)blockIdx.x * kMtN;
-    p[t] = acc0;
-    p[t + kThreads] = acc1;
-    if (third) p[t + 2 * kThreads] = acc2;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
+        if (kQ * l + q < kMtN) p[kQ * l + q] = acc[q];
 }
 
 // one workgroup per chunk: window -> words [o, o + n) of the local stream -> uniforms
-__global__ __launch_bounds__(kThreads) void mt_gen_kernel(MtDrawArgs a) {
+__global__ __launch_bounds__(kGen) void mt_gen_kernel(MtDrawArgs a) {
     __shared__ uint32_t ring[kRing];
     const MtChunk ch = a.chunks[blockIdx.x];
     const int t = threadIdx.x;
     const int32_t pos = (int32_t)a.in[kMtN];
     // local stream index l: l = 0 is word 0 of the start window
-    int f = ch.f;
+    const int f = ch.f;
     int64_t o = (int64_t)pos + ch.s - (int64_t)kMtN * f;   // local index of the chunk's first word
     if (f <= 1) {                                         // block 1 = the key block run forward
         o += (int64_t)kMtN * f;
-        f = 0;
-        for (int i = t; i < kMtN; i += kThreads) ring[i] = a.in[i];
+        for (int i = t; i < kMtN; i += kGen) ring[i] = a.in[i];
     } else {
         const uint32_t* p = a.part + (size_t)ch.jidx * a.S * kMtN;
-        for (int i = t; i < kMtN; i += kThreads) {
+        for (int i = t; i < kMtN; i += kGen) {
             uint32_t v = 0;
             for (int s = 0; s < a.S; ++s) v ^= p[(size_t)s * kMtN + i];
             ring[i] = v;
@@ -136,27 +146,37 @@ __global__ __launch_bounds__(kThreads) void mt_gen_kernel(MtDrawArgs a) {
     const double* high = a.bounds + A;
     int64_t avail = kMtN;                                 // local words [0, avail) generated
     int64_t e_done = 0;                                   // doubles emitted
+    const int64_t need = o + 2 * nd;                      // words the chunk reads
     while (e_done < nd) {
-        // generate up to 4 phases (908 words): the ring keeps 624 words of history + the batch
-        // + at most one unemitted word
-        const int64_t need = o + 2 * nd;
-        for (int k = 0; k < 4 && avail < need; ++k, avail += kLag) gen_phase(ring, avail);
-        // every double whose two words exist
+        // one interval: the next phase's 227 words (threads < 227) and, alongside, every double
+        // whose two words were generated before this interval (~114 in steady state) -- the
+        // emission fills the LDS-latency bubbles of the phase; one barrier per 227 words.  Ring
+        // slots written here alias words < avail - 1821, all emitted and older than the phase's
+        // reads (>= avail - 624).
         const int64_t e_avail = avail > o ? (avail - o) / 2 : 0;
         const int64_t e_end = e_avail < nd ? e_avail : nd;
+        if (avail < need && t < kLag) {
+            const int64_t n = avail + t;
+            ring[n & (kRing - 1)] = ring[(n - kLag) & (kRing - 1)] ^
+                                    mix(ring[(n - kMtN) & (kRing - 1)], ring[(n - kMtN + 1) & (kRing - 1)]);
+        }
         if (ch.out0 >= 0) {
-            for (int64_t e = e_done + t; e < e_end; e += kThreads) {
+            int jj = (ch.j0 + (int)(e_done + t)) % A;      // action column, advanced by kGen per pass
+            const int step = kGen % A;
+            for (int64_t e = e_done + t; e < e_end; e += kGen) {
                 const int64_t l = o + 2 * e;
                 const uint32_t wa = temper(ring[l & (kRing - 1)]) >> 5;
                 const uint32_t wb = temper(ring[(l + 1) & (kRing - 1)]) >> 6;
                 // (a * 2^26 + b) / 2^53: exact in f64 (< 2^53), as rk_double
                 const double d = (double)(((uint64_t)wa << 26) | wb) * 0x1p-53;
-                const int jj = (ch.j0 + (int)e) % A;
                 const double lo = low[jj];
                 a.out[ch.out0 + e] = __dadd_rn(lo, __dmul_rn(__dsub_rn(high[jj], lo), d));
+                jj += step;
+                if (jj >= A) jj -= A;
             }
         }
         e_done = e_end;
+        if (avail < need) avail += kLag;
         __syncthreads();
     }
     if (ch.final_) {
@@ -168,7 +188,7 @@ __global__ __launch_bounds__(kThreads) void mt_gen_kernel(MtDrawArgs a) {
             gen_phase(ring, avail);
             avail += kLag;
         }
-        for (int i = t; i < kMtN; i += kThreads) a.final_state[i] = ring[(b0 + i) & (kRing - 1)];
+        for (int i = t; i < kMtN; i += kGen) a.final_state[i] = ring[(b0 + i) & (kRing - 1)];
         if (t == 0) a.final_state[kMtN] = (uint32_t)(last - b0 + 1);
     }
 }
@@ -177,10 +197,10 @@ __global__ __launch_bounds__(kThreads) void mt_gen_kernel(MtDrawArgs a) {
 
 hipError_t launch_mt_draw(const MtDrawArgs& a, hipStream_t st) {
     if (a.Cj > 0) {
-        hipLaunchKernelGGL(mt_stream_kernel, dim3(1), dim3(kThreads), 0, st, a.in, a.xs);
+        hipLaunchKernelGGL(mt_stream_kernel, dim3(1), dim3(kGen), 0, st, a.in, a.xs);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
         const int w_max = (kMtPolyWords + a.S - 1) / a.S + 1;
-        const size_t lds = (size_t)(32 * w_max + 768) * sizeof(uint32_t);
+        const size_t lds = (size_t)(32 * w_max + 32 + kWave * kQ) * sizeof(uint32_t);
         static size_t attr = 48 * 1024;                   // (set once per size above the default)
         if (lds > attr) {
             const hipError_t e = hipFuncSetAttribute((const void*)mt_jump_kernel,
@@ -188,10 +208,10 @@ hipError_t launch_mt_draw(const MtDrawArgs& a, hipStream_t st) {
             if (e != hipSuccess) return e;
             attr = lds;
         }
-        hipLaunchKernelGGL(mt_jump_kernel, dim3(a.Cj * a.S), dim3(kThreads), lds, st, a);
+        hipLaunchKernelGGL(mt_jump_kernel, dim3(a.Cj * a.S), dim3(kWave), lds, st, a);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(mt_gen_kernel, dim3(a.nchunks), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(mt_gen_kernel, dim3(a.nchunks), dim3(kGen), 0, st, a);
     return hipGetLastError();
 }
 

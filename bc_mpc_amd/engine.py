@@ -287,11 +287,12 @@ class RolloutEngine:
     def get_action_numpy_stream(self, state, low, high, k_global: int, cand_offset: int = 0,
                                 return_costs: bool = False, seed: int = 0) -> Optional[StepResult]:
         """get_action on the actions ``np.random.uniform(low, high, [H, k_global, A])`` would
-        return from the global legacy stream (controllers.py:53), drawn by the library's
-        MT19937 restatement from ``np.random.get_state()`` straight into pinned memory and
-        uploaded step by step (bcmpc_get_action_mt19937); the global stream is then advanced
-        exactly as that one NumPy call advances it.  Returns None (nothing drawn) when the
-        global generator is not the legacy MT19937 or the bounds are not per-action vectors."""
+        return from the global legacy stream (controllers.py:53), drawn by the library's MT19937
+        restatement from ``np.random.get_state()`` on the GPU (default) or on the host
+        (BCMPC_MT_PATH=host) by bcmpc_get_action_mt19937; the global stream is then advanced
+        exactly as that one NumPy call advances it -- only when the call succeeds (a failing call
+        raises and leaves the stream untouched).  Returns None (nothing drawn) when the global
+        generator is not the legacy MT19937 or the bounds are not per-action vectors."""
         if not self.numpy_stream_available(low, high):
             return None
         st = np.random.get_state()
@@ -312,6 +313,26 @@ class RolloutEngine:
         np.random.set_state((st[0], key, pos.value, st[3], st[4]))
         return StepResult(int(res.best_index), float(res.best_cost),
                           np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
+
+    def numpy_stream_draw(self, low, high, k_global: int, cand_offset: int = 0) -> np.ndarray:
+        """This engine's shard ``[:, cand_offset:cand_offset + K]`` of the array
+        ``np.random.uniform(low, high, [H, k_global, A])`` would return from the global legacy stream,
+        drawn on the GPU (bcmpc_mt19937_uniform_device); the global stream is advanced exactly as that
+        one NumPy call advances it."""
+        st = np.random.get_state()
+        if not (isinstance(st, tuple) and st[0] == "MT19937"):
+            raise ValueError("the global generator is not NumPy's legacy MT19937")
+        lo, hi = _f64(low).reshape(-1), _f64(high).reshape(-1)
+        if lo.shape != (self.action_dim,) or hi.shape != (self.action_dim,):
+            raise ValueError("low / high must be per-action vectors")
+        key = np.array(st[1], dtype=np.uint32)
+        pos = ctypes.c_int32(int(st[2]))
+        out = np.empty((self.horizon, self.num_paths, self.action_dim), dtype=np.float64)
+        _lib.check(self._lib.bcmpc_mt19937_uniform_device(
+            self._h, key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(pos), _dp(lo), _dp(hi),
+            ctypes.c_int64(k_global), ctypes.c_int64(cand_offset), _dp(out)))
+        np.random.set_state((st[0], key, pos.value, st[3], st[4]))
+        return out
 
     def rollout_async(self, d_state: int, state_stride: int, d_actions: Optional[int], seed: int,
                       cand_offset: int, d_costs: Optional[int], d_traj: Optional[int],

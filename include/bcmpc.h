@@ -210,18 +210,29 @@ int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actio
                      uint64_t seed, int64_t cand_offset, bcmpc_result* out, double* costs_out);
 
 /* MPCcontroller.get_action with the reference's RNG contract (controllers.py:53): the
- * [H, k_global, A] array np.random.uniform(low, high, size) would return is drawn on the host
- * from NumPy's legacy MT19937 state (mt_key[624] / mt_pos as np.random.get_state() holds
- * them; advanced in place, as the one NumPy call would advance them), step by step into
- * pinned memory, and this shard's [cand_offset, cand_offset + K) slice of each step is
- * copied while the next step is drawn (large draws: split over host threads by jump-ahead,
- * each thread's slice copied as soon as it is drawn; see bcmpc_mt19937_uniform_par).  Then as bcmpc_get_action (seed: the stochastic
- * policy's Philox normals); out->first_action is action_paths[0, best] of that same array
- * (policy engines: the mixed action, the array being the exploration draw of controllers.py:191).  Replaces the host-array form of
- * bcmpc_get_action on the drop-in path (no 8*H*K*A-byte pageable copy). */
+ * [H, k_global, A] array np.random.uniform(low, high, size) would return is drawn from NumPy's
+ * legacy MT19937 state (mt_key[624] / mt_pos as np.random.get_state() holds them; advanced in
+ * place, as the one NumPy call would advance them, and only when the call succeeds) -- only this
+ * shard's [cand_offset, cand_offset + K) slice of each step is produced:
+ *   default: ON THE GPU (mt_device.hip): the draw is cut into chunks, each chunk's start window
+ *     reached by an MT19937 jump-ahead polynomial (GF(2) correlation on the device) and its words
+ *     generated, tempered and scaled by one workgroup straight into HBM; no host draw, no PCIe
+ *     upload of the array (the key, 2.5 KB, goes up; the final state comes back with the result);
+ *   BCMPC_MT_PATH=host: on the host into pinned memory, step by step or split over host threads
+ *     by jump-ahead (bcmpc_mt19937_uniform_par), each slice copied as soon as it is drawn.
+ * Then as bcmpc_get_action (seed: the stochastic policy's Philox normals); out->first_action is
+ * action_paths[0, best] of that same array (policy engines: the mixed action, the array being the
+ * exploration draw of controllers.py:191). */
 int bcmpc_get_action_mt19937(bcmpc_engine* eng, const double* state, uint32_t* mt_key, int32_t* mt_pos,
                              const double* low, const double* high, int64_t k_global, int64_t cand_offset,
                              uint64_t seed, bcmpc_result* out, double* costs_out);
+
+/* The same draw as bcmpc_get_action_mt19937 on the device, alone: this engine's shard
+ * [H, K, A] of np.random.uniform(low, high, [H, k_global, A]) (controllers.py:53) drawn on the GPU
+ * from (mt_key, mt_pos), copied to `out` (host, H*K*A doubles); mt_key / mt_pos advance as the one
+ * NumPy call would advance them.  For tests and for callers that want the array itself. */
+int bcmpc_mt19937_uniform_device(bcmpc_engine* eng, uint32_t* mt_key, int32_t* mt_pos, const double* low,
+                                 const double* high, int64_t k_global, int64_t cand_offset, double* out);
 
 /* Host only (no GPU): n_rows x action_dim doubles of np.random.uniform(low, high) from the
  * legacy MT19937 state (mt_key / mt_pos in/out) -- the generator bcmpc_get_action_mt19937 uses. */
