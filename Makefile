@@ -4,7 +4,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
-OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/rollout_x3_plain.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o build/mt_device.o
+OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/rollout_x3_plain.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o
 HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h $(SRC)/argmin_common.h
 
 all: $(LIB)
@@ -40,6 +40,10 @@ build/mt_device.o: $(SRC)/mt_device.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+build/comm.o: $(SRC)/comm.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 build/cem.o: $(SRC)/cem.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -57,7 +61,7 @@ build/capi.o: $(SRC)/capi.cpp $(HDR) $(SRC)/mt19937.h
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB): $(OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ) -ldl
 
 # resource usage report (VGPR/SGPR/LDS/occupancy) for the rollout kernels
 resources: $(SRC)/rollout.hip $(SRC)/rollout_grp.hip $(HDR)

@@ -24,6 +24,7 @@ LIB_PATH = os.environ.get("BCMPC_LIB") or os.path.join(os.path.dirname(os.path.a
 MAX_LAYERS = 8
 MAX_STATE = 32
 MAX_ACTION = 16
+COMM_ID_BYTES = 128
 ABI_VERSION = 2
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
@@ -147,9 +148,6 @@ SIGNATURES = [
     ("bcmpc_get_action_mt19937", ctypes.c_int,
      [ctypes.c_void_p, _DP, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP,
       ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.POINTER(Result), _DP]),
-    ("bcmpc_mt19937_uniform_device", ctypes.c_int,
-     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int64,
-      ctypes.c_int64, _DP]),
     ("bcmpc_mt19937_uniform", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int32, ctypes.c_int64,
       _DP]),
@@ -183,6 +181,16 @@ SIGNATURES = [
     ("bcmpc_fit_run", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _FP]),
     ("bcmpc_fit_last_error", ctypes.c_char_p, []),
+    ("bcmpc_comm_unique_id", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint8)]),
+    ("bcmpc_comm_init", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+    ("bcmpc_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("bcmpc_engine_set_comm", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("bcmpc_select_results", ctypes.c_int, [ctypes.POINTER(Result), ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.POINTER(Result)]),
+    ("bcmpc_mt19937_uniform_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int64,
+      ctypes.c_int64, _DP]),
     ("bcmpc_engine_info", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
       ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),

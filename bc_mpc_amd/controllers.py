@@ -97,6 +97,27 @@ def _comm_device(ctrl) -> int:
     return _default_device() if ctrl._device is None else ctrl._device
 
 
+def _attach_comm(ctrl, eng: RolloutEngine, fused: bool = True) -> RolloutEngine:
+    """Under RCCL, give the engine the library's communicator (created once per controller, a
+    collective on the first call every rank makes together): its get_action then returns the global
+    best itself.  Only when every rank holds candidates (K >= world) and the cost is fused."""
+    rank, ws = _dist.world(ctrl._group)
+    if (fused and getattr(eng, "comm", None) is None and ws > 1 and int(ctrl.num_simulated_paths) >= ws
+            and _dist.use_library_comm(ctrl._group)):
+        if getattr(ctrl, "_comm", None) is None:
+            ctrl._comm = _dist.LibraryComm(eng.device, ctrl._group)
+        eng.set_comm(ctrl._comm)
+    return eng
+
+
+def _minloc(ctrl, eng, valid, cost, index, first, A):
+    """The ranks' agreement on (cost, index, first action): already made inside the library when the
+    engine has a communicator, else one torch all-gather of the records."""
+    if eng is not None and getattr(eng, "comm", None) is not None:
+        return float(cost), int(index), np.asarray(first, dtype=np.float64).copy()
+    return _dist.allgather_minloc(valid, cost, index, first, A, ctrl._group, device=_comm_device(ctrl))
+
+
 class MPCcontroller(Controller):
     """Random-shooting MPC (controllers.py:26-88) on the MI355X rollout engine."""
 
@@ -161,7 +182,7 @@ class MPCcontroller(Controller):
                                            np.asarray(self.env.action_space.high, dtype=np.float64))
             self._engine_key = key
             self._traj_buf = None
-        return self._engine
+        return _attach_comm(self, self._engine, fused)
 
     def _next_seed(self) -> int:
         src = self._seed_rng if self._seed_rng is not None else np.random
@@ -199,8 +220,7 @@ class MPCcontroller(Controller):
                                               return_costs=self.keep_costs)
             if res is not None:
                 self.last_costs = res.costs
-                cost, index, first_g = _dist.allgather_minloc(True, res.best_cost, res.best_index, res.first_action,
-                                                              A, self._group, device=_comm_device(self))
+                cost, index, first_g = _minloc(self, eng, True, res.best_cost, res.best_index, res.first_action, A)
                 self.last_cost, self.last_index = cost, index
                 return first_g                               # = action_paths[0, index] (controllers.py:84-85)
 
@@ -226,8 +246,7 @@ class MPCcontroller(Controller):
                 valid, cost, index, first = True, float(costs[i]), lo + i, local[0, i, :].copy()
                 self.last_costs = costs
 
-        cost, index, first_g = _dist.allgather_minloc(valid, cost, index, first, A, self._group,
-                                                      device=_comm_device(self))
+        cost, index, first_g = _minloc(self, self._engine, valid, cost, index, first, A)
         self.last_cost, self.last_index = cost, index
         if action_paths is not None:
             opt_action_path = action_paths[:, index, :]     # controllers.py:84-85
@@ -326,7 +345,7 @@ class MPCcontrollerPolicyNet(Controller):
             self._engine.set_action_bounds(np.asarray(self.env.action_space.low, dtype=np.float64),
                                            np.asarray(self.env.action_space.high, dtype=np.float64))
             self._engine_key = key
-        return self._engine
+        return _attach_comm(self, self._engine)
 
     _MODEL = "delta"     # NNDynamicsModel + cheetah cost, argmin
 
@@ -358,8 +377,8 @@ class MPCcontrollerPolicyNet(Controller):
                 res = eng.get_action_numpy_stream(state, self.env.action_space.low, self.env.action_space.high, K,
                                                   lo, return_costs=self.keep_costs, seed=seed)
                 self.last_costs = res.costs
-                cost, index, first_g = _dist.allgather_minloc(True, sign * res.best_cost, res.best_index,
-                                                              res.first_action, A, self._group, device=_comm_device(self))
+                cost, index, first_g = _minloc(self, eng, True, sign * res.best_cost, res.best_index,
+                                               res.first_action, A)
                 self.last_cost, self.last_index = sign * cost, index
                 return first_g
         exploration = self.sample_random_actions()           # every rank draws the full [H, K, A]
@@ -375,8 +394,7 @@ class MPCcontrollerPolicyNet(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, cost, index, first = True, res.best_cost, res.best_index, res.first_action
             self.last_costs = res.costs
-        cost, index, first_g = _dist.allgather_minloc(valid, sign * cost, index, first, A, self._group,
-                                                      device=_comm_device(self))
+        cost, index, first_g = _minloc(self, self._engine, valid, sign * cost, index, first, A)
         self.last_cost, self.last_index = sign * cost, index
         return first_g                                         # copy of action_paths[0, argmin] (:233-235)
 
@@ -464,7 +482,7 @@ class MPCcontrollerReward(Controller):
         if self._gamma_set != float(self.gamma):
             self._engine.set_discount(float(self.gamma))
             self._gamma_set = float(self.gamma)
-        return self._engine
+        return _attach_comm(self, self._engine)
 
     # controllers.py:121-158
     def get_action(self, state):
@@ -494,8 +512,7 @@ class MPCcontrollerReward(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, neg, index, first = True, -res.best_cost, res.best_index, res.first_action
             self.last_rewards = res.costs
-        neg, index, first_g = _dist.allgather_minloc(valid, neg, index, first, A, self._group,
-                                                     device=_comm_device(self))
+        neg, index, first_g = _minloc(self, self._engine, valid, neg, index, first, A)
         self.last_reward, self.last_index = -neg, index
         if action_paths is not None:
             return copy.copy(action_paths[:, index, :][0])    # controllers.py:154-156

@@ -115,6 +115,10 @@ float x3_scale(const float* W, size_t n) {
 
 }  // namespace
 
+namespace bcmpc {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace bcmpc
+
 struct bcmpc_engine {
     bcmpc_config cfg{};
     int HP = 0, T = 0, wpb = 4;
@@ -177,6 +181,7 @@ struct bcmpc_engine {
     MtChunk* d_mt_chunks = nullptr;
     uint32_t* d_mt_part = nullptr;      // [Cj][S][624]
     uint32_t* h_mt_io = nullptr;        // pinned mirror of d_mt_io (+ bounds at word 1280)
+    bcmpc_comm* comm = nullptr;         // attached communicator: results exchanged after every argmin
 };
 
 extern "C" {
@@ -794,6 +799,12 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[1], st));
     if (d_result && !fused) HIP_TRY(launch_argmin(m, st));
+    if (d_result && e->comm && !cem) {
+        // the one collective of a sharded control step: every rank's record, then np.argmin's rule
+        std::string err;
+        if (comm_exchange(e->comm, d_result, c.cost == BCMPC_COST_REWARD, st, &err) != BCMPC_OK)
+            return fail(BCMPC_ERR_HIP, err);
+    }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[2], st));
     e->timed = d_result != nullptr;
     return BCMPC_OK;
@@ -1231,6 +1242,16 @@ int bcmpc_cem_refit_async(bcmpc_engine* e, const bcmpc_elite* d_elite, const int
     if (!e) return fail(BCMPC_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(e->cfg.device));
     return refit_impl(e, d_elite, d_count, seed, iteration, alpha, d_mu, d_sigma, (hipStream_t)stream);
+}
+
+int bcmpc_engine_set_comm(bcmpc_engine* e, bcmpc_comm* comm) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    if (comm && comm_device(comm) != e->cfg.device)
+        return fail(BCMPC_ERR_ARG, "the communicator was created for another device");
+    if (comm && e->cfg.cost == BCMPC_COST_NONE)
+        return fail(BCMPC_ERR_ARG, "the exchange needs the fused objective (argmin records)");
+    e->comm = comm;
+    return BCMPC_OK;
 }
 
 int bcmpc_last_kernel_ms(bcmpc_engine* e, float* rollout_ms, float* argmin_ms) {

@@ -1,0 +1,188 @@
+// comm.hip -- the one per-control-step collective of a candidate-sharded get_action, owned by the
+// library (include/bcmpc.h, bcmpc_comm_*).
+//
+// The K candidates of a control step are independent rollouts of one state (controllers.py:63-71);
+// the only cross-candidate operation is np.argmin (controllers.py:82).  Each rank (one process per
+// GPU) runs its contiguous shard; its argmin launch leaves a 144-byte bcmpc_result (global index,
+// f64 cost, f64 first action).  With a communicator attached to the engine, the same stream then
+// runs ONE RCCL all-gather of those records over xGMI and a one-wave kernel that applies
+// np.argmin's rule to them (NaN first, smaller cost, lowest global index on ties; np.argmax for the
+// learned reward), so every rank's d_result holds the global answer before anything returns to the
+// host.  An exact min-loc needs the f64 cost and the index (128 bits), more than a 64-bit
+// all-reduce(MIN) key holds without rounding the cost -- hence an all-gather of tiny records
+// (latency-bound: 144 B x N), not an all-reduce.  The reference's only collective
+// (train_mpc_ppo.py:388, an mpi4py allgather of episode statistics) is not on this path.
+//
+// RCCL is loaded with dlopen on first use (librccl.so.1: the copy PyTorch-ROCm already mapped when
+// present, else /opt/rocm's), so libbcmpc itself has no link-time dependency on it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/bcmpc.h"
+#include "kernels.h"
+
+namespace bcmpc {
+
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string error;
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            r.error = std::string("cannot load librccl.so.1: ") + dlerror();
+            return;
+        }
+        r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        r.init_rank = reinterpret_cast<decltype(r.init_rank)>(dlsym(h, "ncclCommInitRank"));
+        r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
+        r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
+        r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+        if (!r.get_unique_id || !r.init_rank || !r.destroy || !r.all_gather || !r.error_string)
+            r.error = "librccl.so.1 lacks an expected symbol";
+    });
+    return r;
+}
+
+// np.argmin order on result records (cost already sign-flipped for argmax)
+__host__ __device__ inline bool record_better(double ca, int64_t ia, double cb, int64_t ib) {
+    const bool an = ca != ca, bn = cb != cb;
+    if (an != bn) return an;
+    if (!an && ca != cb) return ca < cb;
+    return ia < ib;
+}
+
+__host__ __device__ inline int select_index(const bcmpc_result* r, int n, int maximize) {
+    const double sg = maximize ? -1.0 : 1.0;
+    int best = 0;
+    for (int k = 1; k < n; ++k)
+        if (record_better(sg * r[k].best_cost, r[k].best_index, sg * r[best].best_cost, r[best].best_index)) best = k;
+    return best;
+}
+
+// one wave: d_out = the best of n gathered records (n is the communicator size: a handful)
+__global__ __launch_bounds__(64) void select_records_kernel(const bcmpc_result* __restrict__ recs, int n,
+                                                           int maximize, bcmpc_result* __restrict__ out) {
+    const int best = select_index(recs, n, maximize);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(recs + best);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(out);
+    constexpr int kWords = sizeof(bcmpc_result) / sizeof(uint64_t);
+    for (int w = threadIdx.x; w < kWords; w += 64) dst[w] = src[w];
+}
+
+int comm_fail(int code, const std::string& msg) { return set_error(code, msg); }   // -> bcmpc_last_error()
+
+}  // namespace
+
+}  // namespace bcmpc
+
+struct bcmpc_comm {
+    ncclComm_t nccl = nullptr;
+    int nranks = 0, rank = 0, device = 0;
+    bcmpc_result* d_gather = nullptr;   // [nranks] records
+};
+
+namespace bcmpc {
+
+// enqueue the exchange after the argmin launch: all-gather every rank's record, select in place
+int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream_t st, std::string* err) {
+    const Rccl& r = rccl();
+    const ncclResult_t rc = r.all_gather(d_result, c->d_gather, sizeof(bcmpc_result), ncclUint8, c->nccl, st);
+    if (rc != ncclSuccess) {
+        *err = std::string("ncclAllGather: ") + r.error_string(rc);
+        return BCMPC_ERR_HIP;
+    }
+    hipLaunchKernelGGL(select_records_kernel, dim3(1), dim3(64), 0, st, c->d_gather, c->nranks, maximize, d_result);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *err = std::string("select_records_kernel: ") + hipGetErrorString(e);
+        return BCMPC_ERR_HIP;
+    }
+    return BCMPC_OK;
+}
+
+int comm_rank(const bcmpc_comm* c) { return c->rank; }
+int comm_size(const bcmpc_comm* c) { return c->nranks; }
+int comm_device(const bcmpc_comm* c) { return c->device; }
+
+}  // namespace bcmpc
+
+extern "C" {
+
+int bcmpc_comm_unique_id(uint8_t* id) {
+    using namespace bcmpc;
+    if (!id) return comm_fail(BCMPC_ERR_ARG, "null argument");
+    const Rccl& r = rccl();
+    if (!r.error.empty()) return comm_fail(BCMPC_ERR_UNSUPPORTED, r.error);
+    ncclUniqueId u;
+    const ncclResult_t rc = r.get_unique_id(&u);
+    if (rc != ncclSuccess) return comm_fail(BCMPC_ERR_HIP, std::string("ncclGetUniqueId: ") + r.error_string(rc));
+    static_assert(sizeof(u.internal) == BCMPC_COMM_ID_BYTES, "RCCL unique id size");
+    std::memcpy(id, u.internal, BCMPC_COMM_ID_BYTES);
+    return BCMPC_OK;
+}
+
+int bcmpc_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, bcmpc_comm** out) {
+    using namespace bcmpc;
+    if (!id || !out) return comm_fail(BCMPC_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return comm_fail(BCMPC_ERR_ARG, "rank must be in [0, nranks)");
+    const Rccl& r = rccl();
+    if (!r.error.empty()) return comm_fail(BCMPC_ERR_UNSUPPORTED, r.error);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return comm_fail(BCMPC_ERR_ARG, "device ordinal out of range");
+    if (hipSetDevice(device) != hipSuccess) return comm_fail(BCMPC_ERR_HIP, "hipSetDevice failed");
+    bcmpc_comm* c = new bcmpc_comm();
+    c->nranks = nranks; c->rank = rank; c->device = device;
+    if (hipMalloc(&c->d_gather, (size_t)nranks * sizeof(bcmpc_result)) != hipSuccess) {
+        delete c;
+        return comm_fail(BCMPC_ERR_HIP, "device allocation failed");
+    }
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, BCMPC_COMM_ID_BYTES);
+    const ncclResult_t rc = r.init_rank(&c->nccl, nranks, u, rank);   // collective over the nranks
+    if (rc != ncclSuccess) {
+        (void)hipFree(c->d_gather);
+        delete c;
+        return comm_fail(BCMPC_ERR_HIP, std::string("ncclCommInitRank: ") + r.error_string(rc));
+    }
+    *out = c;
+    return BCMPC_OK;
+}
+
+int bcmpc_comm_destroy(bcmpc_comm* c) {
+    using namespace bcmpc;
+    if (!c) return BCMPC_OK;
+    (void)hipSetDevice(c->device);
+    if (c->nccl) (void)rccl().destroy(c->nccl);
+    if (c->d_gather) (void)hipFree(c->d_gather);
+    delete c;
+    return BCMPC_OK;
+}
+
+int bcmpc_select_results(const bcmpc_result* recs, int32_t n, int32_t maximize, bcmpc_result* out) {
+    using namespace bcmpc;
+    if (!recs || !out || n < 1) return comm_fail(BCMPC_ERR_ARG, "need n >= 1 records");
+    *out = recs[select_index(recs, n, maximize)];
+    return BCMPC_OK;
+}
+
+}  // extern "C"

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/bcmpc.h"
 
 namespace bcmpc {
@@ -132,6 +134,13 @@ struct MtDrawArgs {
     int32_t nchunks, Cj, S, A;
 };
 hipError_t launch_mt_draw(const MtDrawArgs& a, hipStream_t st);
+
+// ---- library-owned min-loc exchange (comm.hip) ----
+int set_error(int code, const std::string& msg);          // bcmpc_last_error() text (capi.cpp)
+int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream_t st, std::string* err);
+int comm_rank(const bcmpc_comm* c);
+int comm_size(const bcmpc_comm* c);
+int comm_device(const bcmpc_comm* c);
 
 constexpr int kPolParams = 96;
 

@@ -7,7 +7,13 @@ initial state (controllers.py:63-71); the only cross-candidate operation is
 contiguous global range ``shard_range(K, r, world)`` and after its local
 rollout contributes one record ``[valid, cost, index, first_action...]``.
 
-Exchange: a single ``all_gather_into_tensor`` of (3 + A) doubles per rank.
+Exchange, RCCL (backend "nccl"): ``LibraryComm`` -- libbcmpc's own communicator
+(bcmpc_comm_*, csrc/comm.hip), bootstrapped by broadcasting its 128-byte RCCL id
+through torch.distributed once; attached to the engine, every get_action
+all-gathers the 144-byte result records on the device right after the argmin
+launch and reduces them with np.argmin's rule there (no host round trip, no
+torch collective on the control step).  Other backends (gloo, the CPU tests):
+a single ``all_gather_into_tensor`` of (3 + A) doubles per rank.
 An exact min-loc needs the f64 cost AND the index (np.argmin tie-break:
 lowest index; NaN wins) -- 128 bits that do not fit a 64-bit
 ``all_reduce(MIN)`` key without rounding the cost, so the exchange is an
@@ -30,6 +36,66 @@ def world(group=None) -> Tuple[int, int]:
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(group), dist.get_world_size(group)
     return 0, 1
+
+
+class LibraryComm:
+    """libbcmpc's communicator (bcmpc_comm_init: one RCCL communicator over the group's ranks, on
+    this rank's GPU).  Collective: every rank of ``group`` constructs it together; rank 0's RCCL
+    unique id travels by ``torch.distributed.broadcast_object_list`` (bootstrap only)."""
+
+    def __init__(self, device: int, group=None):
+        import ctypes
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        self._lib = _lib.load()
+        self.rank, self.size = world(group)
+        self.device = int(device)
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+        if self.rank == 0:
+            _lib.check(self._lib.bcmpc_comm_unique_id(buf))
+        obj = [bytes(buf)]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(obj, src=src, group=group, device=torch.device("cuda", self.device))
+        ctypes.memmove(buf, obj[0], _lib.COMM_ID_BYTES)
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.bcmpc_comm_init(buf, self.size, self.rank, self.device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.bcmpc_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def use_library_comm(group=None) -> bool:
+    """The library exchanges the records itself under RCCL (backend "nccl"); BCMPC_LIBRARY_COMM=0
+    keeps the torch all-gather."""
+    import os
+    rank, ws = world(group)
+    if ws == 1 or os.environ.get("BCMPC_LIBRARY_COMM", "1") == "0":
+        return False
+    import torch.distributed as dist
+    return dist.get_backend(group) == "nccl"
+
+
+def select_results_host(records, maximize: bool = False) -> Tuple[float, int, np.ndarray]:
+    """np.argmin (np.argmax) over bcmpc_result records through the library's own rule
+    (bcmpc_select_results, the host twin of the device selection)."""
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    n = len(records)
+    arr = (_lib.Result * n)(*records)
+    out = _lib.Result()
+    _lib.check(lib.bcmpc_select_results(arr, n, int(bool(maximize)), ctypes.byref(out)))
+    return float(out.best_cost), int(out.best_index), np.array(out.first_action[:], dtype=np.float64)
 
 
 def shard_range(K: int, rank: int, world_size: int) -> Tuple[int, int]:
@@ -96,11 +162,13 @@ def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optiona
 
 
 def allgather_result(d_result, action_dim: int, maximize: bool = False, group=None) -> Tuple[float, int, np.ndarray]:
-    """The same exchange straight from the device: ``d_result`` is this rank's ``bcmpc_result``
+    """The torch-side form of the exchange (gloo rehearsals; nccl without the library communicator):
+    ``d_result`` is this rank's ``bcmpc_result``
     (144 bytes: int64 index, f64 cost, f64 first_action[16]) as a uint8 CUDA tensor, written by
     the argmin launch; the all-gather is stream-ordered after it, so there is no host round trip
     before the collective and one device-to-host copy after it.  Every rank must hold >= 1
-    candidate (K > 0).  ``maximize``: learned reward (np.argmax, controllers.py:152)."""
+    candidate (K > 0).  ``maximize``: learned reward (np.argmax, controllers.py:152).  The records
+    are reduced by bcmpc_select_results, the host twin of the library's device selection."""
     import torch
     import torch.distributed as dist
     rank, ws = world(group)
@@ -113,12 +181,7 @@ def allgather_result(d_result, action_dim: int, maximize: bool = False, group=No
         dist.all_gather_into_tensor(out, src, group=group)
         raw = out.cpu().numpy()
     raw = raw.reshape(max(ws, 1), nb)
-    sign = -1.0 if maximize else 1.0
-    recs = np.zeros((raw.shape[0], 3 + action_dim), dtype=np.float64)
-    for r in range(raw.shape[0]):
-        recs[r, 0] = 1.0
-        recs[r, 1] = sign * float(raw[r, 8:16].view(np.float64)[0])
-        recs[r, 2] = float(raw[r, 0:8].view(np.int64)[0])
-        recs[r, 3:] = raw[r, 16:16 + 8 * action_dim].view(np.float64)
-    best = select(recs)
-    return float(sign * best[1]), int(best[2]), best[3:].copy()
+    from . import _lib
+    recs = [_lib.Result.from_buffer_copy(raw[r].tobytes()) for r in range(raw.shape[0])]
+    cost, index, first = select_results_host(recs, maximize=maximize)   # the library's own rule
+    return cost, index, first[:action_dim].copy()

@@ -154,6 +154,7 @@ class RolloutEngine:
         self._keep = []
         self._wver = None
         self._pol = None
+        self.comm = None
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, spec: MLPSpec, normalization: Sequence, version: int) -> None:
@@ -394,6 +395,13 @@ class RolloutEngine:
             self._h, ctypes.c_void_p(d_elite), ctypes.c_void_p(d_count), ctypes.c_uint64(seed & (2**64 - 1)),
             int(iteration), float(alpha), ctypes.c_void_p(d_mu), ctypes.c_void_p(d_sigma), ctypes.c_void_p(stream)))
 
+    def set_comm(self, comm) -> None:
+        """Attach a ``distributed.LibraryComm`` (None detaches): every get_action of this engine then
+        exchanges the ranks' result records over RCCL inside the library and returns the GLOBAL best
+        (bcmpc_engine_set_comm)."""
+        _lib.check(self._lib.bcmpc_engine_set_comm(self._h, comm.handle if comm is not None else None))
+        self.comm = comm
+
     @property
     def stream(self) -> int:
         return int(self._lib.bcmpc_stream(self._h) or 0)
@@ -413,6 +421,7 @@ class RolloutEngine:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
+            self.comm = None
             self._lib.bcmpc_destroy(self._h)
             self._h = None
 

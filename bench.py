@@ -307,6 +307,12 @@ def main():
                    "group8": "rollout_grp<NW=8>", "split1": "rollout_x3<NC=1>", "split2": "rollout_x3<NC=2>",
                    "split4": "rollout_x3<NC=4>"}.get(
         info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
+    lib_comm = None
+    if world > 1 and backend == "nccl" and not wl.get("cem") and args.actions == "device":
+        # the library's own communicator: get_action all-gathers the ranks' result records over RCCL
+        # and selects on the device (csrc/comm.hip); torch.distributed only carried its RCCL id
+        lib_comm = bdist.LibraryComm(local)
+        eng.set_comm(lib_comm)
     d_state = torch.from_numpy(state).to(dev)
     d_actions = None
     if args.actions == "hbm":
@@ -352,7 +358,7 @@ def main():
         if d_actions is None:
             # the complete control step: state H2D, device-drawn actions, rollout, argmin, result D2H
             res = eng.get_action(state, None, seed=0xB0B + i, cand_offset=offset)
-            if world == 1:
+            if world == 1 or lib_comm is not None:     # (with the communicator: already the global best)
                 return res.best_cost, res.best_index, res.first_action
             sign = -1.0 if reward else 1.0              # learned reward: argmax == argmin of -r
             return bdist.allgather_minloc(True, sign * res.best_cost, res.best_index, res.first_action, A_DIM,
@@ -424,8 +430,10 @@ def main():
                                   if world > 1 else ", 1 GPU (no collective)"),
                    "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
                    "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
-                   "collective": f"{backend} all_gather min-loc, {3 + A_DIM} f64 per rank per step" if world > 1
-                   else "none (1 rank)"},
+                   "collective": ("libbcmpc RCCL all-gather of the 144-byte result records + device np.argmin "
+                                  "select, in get_action (bcmpc_engine_set_comm)" if lib_comm is not None else
+                                  f"torch {backend} all_gather min-loc, {3 + A_DIM} f64 per rank per step")
+                   if world > 1 else "none (1 rank)"},
         "p50_ms": float(np.percentile(step_s, 50) * 1e3),
         "dropin_parity_p50_ms": dropin["p50_ms"] if dropin else None,
         "dropin_parity": dropin if dropin else "n/a (MPCcontroller drop-in is timed for the plain delta-net "
@@ -461,6 +469,9 @@ def main():
                                            pol_arrays, wl.get("explore", 0.5), gamma, cem)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if lib_comm is not None:
+        eng.set_comm(None)
+        lib_comm.close()
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -330,6 +330,34 @@ int bcmpc_fit_run(bcmpc_fitter* f, const int64_t* indices, const int32_t* batch_
                   float* losses);
 const char* bcmpc_fit_last_error(void);
 
+/* ------------------------------------------------------------------------
+ * Candidate sharding over GPUs: one process per GPU, rank r owns the
+ * global candidates [cand_offset, cand_offset + K).  The library owns the one
+ * collective of a control step: a communicator attached to an engine makes every
+ * bcmpc_get_action / bcmpc_get_action_mt19937 / bcmpc_rollout_async (with d_result)
+ * of that engine all-gather the ranks' 144-byte result records over RCCL (xGMI)
+ * right after the argmin launch, stream-ordered, and reduce them on the device with
+ * np.argmin's rule (controllers.py:82: first NaN, else smallest cost, ties -> lowest
+ * global index; np.argmax for BCMPC_COST_REWARD, controllers.py:152): every rank
+ * returns the GLOBAL best.  All ranks must call with the same state and hold >= 1
+ * candidate.  No Python or torch is needed: rank 0 makes the id, any out-of-band
+ * channel (MPI, a file, a socket) carries its 128 bytes to the other ranks.
+ * RCCL (librccl.so.1) is loaded on first use.  Replaces nothing in the reference's
+ * hot path (single process); its only collective, train_mpc_ppo.py:388, gathers
+ * episode statistics. */
+#define BCMPC_COMM_ID_BYTES 128
+typedef struct bcmpc_comm bcmpc_comm;
+int bcmpc_comm_unique_id(uint8_t* id /* [BCMPC_COMM_ID_BYTES] */);             /* ncclGetUniqueId   */
+int bcmpc_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device,
+                    bcmpc_comm** out);                                          /* ncclCommInitRank  */
+int bcmpc_comm_destroy(bcmpc_comm* comm);
+/* attach (comm != NULL) or detach (NULL); the comm's device must be the engine's.
+ * CEM calls (bcmpc_cem_*) do not exchange. */
+int bcmpc_engine_set_comm(bcmpc_engine* eng, bcmpc_comm* comm);
+/* Host only: the np.argmin (maximize: np.argmax) winner of n result records, for hosts
+ * that exchange the records themselves (e.g. MPI / gloo). */
+int bcmpc_select_results(const bcmpc_result* recs, int32_t n, int32_t maximize, bcmpc_result* out);
+
 /* Device stream the engine launches on (hipStream_t as void*). */
 void* bcmpc_stream(bcmpc_engine* eng);
 

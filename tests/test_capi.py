@@ -78,3 +78,61 @@ int main(void) {
             t, f = key.split(".")
             cls = {"bcmpc_config": _lib.Config, "bcmpc_weights": _lib.Weights, "bcmpc_result": _lib.Result}[t]
             assert getattr(cls, f).offset == int(v), key
+
+
+def _record(index, cost, a0=0.0):
+    from bc_mpc_amd import _lib
+    r = _lib.Result()
+    r.best_index, r.best_cost = index, cost
+    r.first_action[0] = a0
+    return r
+
+
+@pytest.mark.parametrize("costs,indices,maximize,want", [
+    ([3.5, 1.25, 1.25], [7, 107, 207], False, 107),                  # tie across ranks: lower global index
+    ([3.5, 1.25, 1.25], [7, 207, 107], False, 107),                  # (order of the records does not matter)
+    ([2.0, float("nan"), float("nan")], [1, 900, 400], False, 400),  # a NaN wins, the first NaN (lowest index)
+    ([3.5, 1.25, 9.0], [7, 107, 5], True, 5),                        # np.argmax for the learned reward
+    ([-1.0], [42], False, 42),
+])
+def test_select_results_is_np_argmin_over_ranks(costs, indices, maximize, want):
+    """bcmpc_select_results (the host twin of the device selection after the RCCL all-gather,
+    csrc/comm.hip): the global np.argmin / np.argmax of the ranks' shard results."""
+    import numpy as np
+    from bc_mpc_amd import distributed as bd
+    recs = [_record(i, c, float(i)) for c, i in zip(costs, indices)]
+    cost, index, first = bd.select_results_host(recs, maximize=maximize)
+    assert index == want and first[0] == float(want)
+    # the same as np.argmin / np.argmax of the concatenated global cost vector
+    full = np.full(max(indices) + 1, np.inf if not maximize else -np.inf)
+    full[indices] = costs
+    assert index == int(np.argmax(full) if maximize else np.argmin(full))
+
+
+def test_comm_arguments_validated_without_gpu():
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    h = ctypes.c_void_p()
+    assert lib.bcmpc_comm_init(buf, 0, 0, 0, ctypes.byref(h)) == _lib.ERR_ARG
+    assert lib.bcmpc_comm_init(buf, 2, 2, 0, ctypes.byref(h)) == _lib.ERR_ARG
+    assert b"rank" in lib.bcmpc_last_error()
+    assert lib.bcmpc_engine_set_comm(None, None) == _lib.ERR_ARG
+    assert lib.bcmpc_select_results(None, 0, 0, None) == _lib.ERR_ARG
+
+
+def test_integration_stub_structs_match_the_library():
+    """The ctypes stub INTEGRATION.md shows a maintainer (no package import) declares the same struct
+    layouts as include/bcmpc.h."""
+    from bc_mpc_amd import _lib
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```python\n(.*?)```", text, flags=re.S)
+    stub = next(b for b in blocks if "class Cfg(ctypes.Structure)" in b)
+    defs = stub[stub.index("class Cfg"):stub.index("def make_controller")]
+    ns = {"ctypes": ctypes}
+    exec(defs, ns)
+    assert ctypes.sizeof(ns["Cfg"]) == ctypes.sizeof(_lib.Config)
+    assert ctypes.sizeof(ns["W"]) == ctypes.sizeof(_lib.Weights)
+    assert ctypes.sizeof(ns["Res"]) == ctypes.sizeof(_lib.Result)
+    assert [f[0] for f in ns["W"]._fields_] == [f[0] for f in _lib.Weights._fields_]
+    assert [f[0] for f in ns["Cfg"]._fields_] == [f[0] for f in _lib.Config._fields_]

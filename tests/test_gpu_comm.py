@@ -1,0 +1,136 @@
+"""The library-owned min-loc exchange (bcmpc_comm_*, csrc/comm.hip) on the GPU box.
+
+One rank: the RCCL all-gather + device selection leave the engine's own result unchanged (the
+path every multi-GPU get_action takes, exercised end to end on one card).  Two ranks on one card:
+RCCL refuses two ranks on the same GPU on most builds; when it accepts them, the two half-shard
+engines must both return the single engine's global argmin.  Multi-GPU scaling is measured by
+the driver's 8-GPU bench, not here."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(K, H=6):
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    w = orc.synthetic_weights(20, 6, 128, 2, "tanh", False)
+    norm = orc.synthetic_normalization(20, 6)
+    state = orc.synthetic_state(norm)
+
+    def make(k):
+        eng = RolloutEngine(20, 6, 128, 2, "tanh", False, H, k, device=0)
+        eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+        return eng
+    return make, state
+
+
+class _Comm:
+    """bcmpc_comm for tests (bootstrap by hand)."""
+
+    def __init__(self, idbuf, n, r):
+        from bc_mpc_amd import _lib
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        self.rc = self._lib.bcmpc_comm_init(idbuf, n, r, 0, ctypes.byref(h))
+        self.err = self._lib.bcmpc_last_error().decode()
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self._lib.bcmpc_comm_destroy(self.handle)
+            self.handle = None
+
+
+def test_single_rank_exchange_is_identity():
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    make, state = _setup(3000)
+    idbuf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    _lib.check(lib.bcmpc_comm_unique_id(idbuf))
+    comm = _Comm(idbuf, 1, 0)
+    assert comm.rc == 0, comm.err
+    plain, shared = make(3000), make(3000)
+    shared.set_comm(comm)
+    for seed in (1, 2, 3):
+        a = plain.get_action(state, None, seed=seed, cand_offset=500)
+        b = shared.get_action(state, None, seed=seed, cand_offset=500)
+        assert (a.best_index, a.best_cost) == (b.best_index, b.best_cost)
+        assert np.array_equal(a.first_action, b.first_action)
+    np.random.seed(4)
+    st = np.random.get_state()
+    a = plain.get_action_numpy_stream(state, -np.ones(6), np.ones(6), 3000)
+    np.random.set_state(st)
+    b = shared.get_action_numpy_stream(state, -np.ones(6), np.ones(6), 3000)
+    assert (a.best_index, a.best_cost) == (b.best_index, b.best_cost)
+    shared.set_comm(None)
+    plain.close(), shared.close()
+    comm.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _two_rank_worker(rank, port, q):
+    import sys
+    import torch.distributed as dist
+    from conftest import REPO
+    sys.path.insert(0, REPO)
+    from bc_mpc_amd import _lib
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    lib = _lib.load()
+    idbuf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    if rank == 0:
+        _lib.check(lib.bcmpc_comm_unique_id(idbuf))
+    t = torch.frombuffer(bytearray(bytes(idbuf)), dtype=torch.uint8)
+    dist.broadcast(t, 0)
+    ctypes.memmove(idbuf, bytes(t.numpy()), _lib.COMM_ID_BYTES)
+    comm = _Comm(idbuf, 2, rank)
+    if comm.rc != 0:
+        q.put((rank, "init-failed", comm.err))
+        dist.destroy_process_group()
+        return
+    make, state = _setup(2000)
+    eng = make(1000)
+    eng.set_comm(comm)
+    res = eng.get_action(state, None, seed=11, cand_offset=1000 * rank)
+    q.put((rank, "ok", (res.best_index, res.best_cost, res.first_action.tolist())))
+    eng.set_comm(None)
+    eng.close()
+    comm.close()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_one_card_agree_on_the_global_argmin():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_two_rank_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in range(2):
+        r, status, val = q.get(timeout=100)
+        out[r] = (status, val)
+    for p in ps:
+        p.join(timeout=60)
+    if any(s == "init-failed" for s, _ in out.values()):
+        pytest.skip(f"RCCL refuses two ranks on one GPU here: {out[0][1]}")
+    make, state = _setup(2000)
+    eng = make(2000)
+    want = eng.get_action(state, None, seed=11, cand_offset=0)
+    eng.close()
+    for r in (0, 1):
+        idx, cost, first = out[r][1]
+        assert (idx, cost) == (want.best_index, want.best_cost)
+        assert first == want.first_action.tolist()
