@@ -158,6 +158,9 @@ SIGNATURES = [
     ("bcmpc_rollout_async", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("bcmpc_rollout_policy_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("bcmpc_cem_get_action", ctypes.c_int,
      [ctypes.c_void_p, _DP, ctypes.POINTER(Cem), ctypes.c_uint64, _DP, _DP, ctypes.POINTER(Result)]),
     ("bcmpc_cem_rollout_async", ctypes.c_int,

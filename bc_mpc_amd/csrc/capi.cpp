@@ -673,7 +673,7 @@ struct CemLaunch {           // one CEM iteration's sampling distribution + resu
 static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, const double* d_actions,
                         uint64_t seed, int64_t cand_offset, double* d_costs, double* d_traj,
                         bcmpc_result* d_result, hipStream_t st, const CemLaunch* cem = nullptr,
-                        bool record_events = true) {
+                        bool record_events = true, double* act_out_all = nullptr) {
     const bcmpc_config& c = e->cfg;
     if (!e->has_weights) return fail(BCMPC_ERR_STATE, "bcmpc_set_weights has not been called");
     if (c.num_paths == 0) return fail(BCMPC_ERR_EMPTY, "attempt to get argmin of an empty sequence");
@@ -720,8 +720,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.phidden_padded = e->PHP;
         a.pol_mode = c.policy_mode;
         a.explore = e->explore;
-        a.act_out = e->d_first;
-        a.act_out_steps = 1;
+        a.act_out = act_out_all ? act_out_all : e->d_first;      // [H][K][A] or step 0 only
+        a.act_out_steps = act_out_all ? c.horizon : 1;
     }
     for (int l = 0; l < e->nwl; ++l) a.winv[l] = e->winv[l];
     for (int l = 0; l <= e->PL; ++l) a.pwinv[l] = e->pwinv[l];
@@ -736,7 +736,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     ArgminArgs m{};
     if (d_result) {
         m.costs = d_costs; m.actions = d_actions; m.consts = e->d_consts; m.out = d_result;
-        m.act_out = e->PL > 0 ? e->d_first : nullptr;
+        m.act_out = e->PL > 0 ? (act_out_all ? act_out_all : e->d_first) : nullptr;
         m.seed = seed; m.cand_offset = cand_offset; m.K = c.num_paths; m.A = c.action_dim;
         m.maximize = c.cost == BCMPC_COST_REWARD;
         m.scratch_c = e->d_amin_c;
@@ -857,6 +857,16 @@ int bcmpc_rollout_async(bcmpc_engine* e, const double* d_state, int64_t state_st
     // `stream` is used verbatim: NULL is HIP's null stream (bcmpc_stream() gives the engine's own)
     return rollout_impl(e, d_state, state_stride, d_actions, seed, cand_offset, d_costs, d_traj, d_result,
                         (hipStream_t)stream);
+}
+
+int bcmpc_rollout_policy_async(bcmpc_engine* e, const double* d_state, const double* d_actions, uint64_t seed,
+                               int64_t cand_offset, double* d_costs, double* d_traj, double* d_actions_out,
+                               bcmpc_result* d_result, void* stream) {
+    if (!e || !d_state || !d_actions_out) return fail(BCMPC_ERR_ARG, "null argument");
+    if (e->PL == 0) return fail(BCMPC_ERR_STATE, "engine was created without a policy (config.policy_hidden == 0)");
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    return rollout_impl(e, d_state, 0, d_actions, seed, cand_offset, d_costs, d_traj, d_result, (hipStream_t)stream,
+                        nullptr, true, d_actions_out);
 }
 
 int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions, uint64_t seed,

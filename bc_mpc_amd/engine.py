@@ -351,6 +351,18 @@ class RolloutEngine:
             ctypes.c_void_p(d_traj) if d_traj else None, ctypes.c_void_p(d_result) if d_result else None,
             ctypes.c_void_p(stream)))
 
+    def rollout_policy_async(self, d_state: int, d_actions: Optional[int], seed: int, cand_offset: int,
+                             d_costs: Optional[int], d_traj: Optional[int], d_actions_out: int,
+                             d_result: Optional[int], stream: Optional[int] = None) -> None:
+        """Policy engines: rollout_async plus every step's rolled-out actions ``d_actions_out``
+        ``[H, K, A]`` f64 (the reference's action_paths, controllers.py:208-213)."""
+        stream = self.stream if stream is None else stream
+        vp = lambda x: ctypes.c_void_p(x) if x else None   # noqa: E731
+        _lib.check(self._lib.bcmpc_rollout_policy_async(
+            self._h, ctypes.c_void_p(d_state), vp(d_actions), ctypes.c_uint64(seed & (2**64 - 1)),
+            ctypes.c_int64(cand_offset), vp(d_costs), vp(d_traj), ctypes.c_void_p(d_actions_out), vp(d_result),
+            ctypes.c_void_p(stream)))
+
     # ------------------------------------------------------------------ CEM
     def cem_get_action(self, state, mu, sigma, iterations: int, n_elite: int, alpha: float,
                        seed: int) -> Tuple[StepResult, np.ndarray, np.ndarray]:

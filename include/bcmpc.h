@@ -268,6 +268,15 @@ int bcmpc_rollout_async(bcmpc_engine* eng, const double* d_state, int64_t state_
                         const double* d_actions, uint64_t seed, int64_t cand_offset,
                         double* d_costs, double* d_traj, bcmpc_result* d_result, void* stream);
 
+/* MPCcontrollerPolicyNet engines: bcmpc_rollout_async plus the actions actually rolled out at
+ * EVERY step -- d_actions_out [H, K, A] f64, the reference's action_paths (controllers.py:208-213:
+ * the policy mean mixed with the exploration draw, or mean + exp(logstd) * N(0,1) when self_exp)
+ * -- and optionally the states (d_traj [H+1, K, S]), so a caller (or a test) can replay each step.
+ * d_actions: the [H, K, A] exploration draw or NULL (device Philox). */
+int bcmpc_rollout_policy_async(bcmpc_engine* eng, const double* d_state, const double* d_actions, uint64_t seed,
+                               int64_t cand_offset, double* d_costs, double* d_traj, double* d_actions_out,
+                               bcmpc_result* d_result, void* stream);
+
 /* CEM, single device, synchronous: all iterations on the engine's stream.
  *   mu, sigma : host [H][A] doubles, in: the initial distribution, out: the refit one
  *   out       : best_index = iteration * K + candidate, best_cost, first action

@@ -494,6 +494,33 @@ def device_rng_actions(seed: int, cand_offset: int, K: int, H: int, low, high) -
     return out
 
 
+POLICY_NORMAL_KEY_XOR = 0x9E3779B97F4A7C15
+
+
+def device_rng_normals(seed: int, cand_offset: int, K: int, h: int, A: int) -> np.ndarray:
+    """The N(0, 1) draws the engine's stochastic policy uses at step ``h`` (self_exp=True,
+    controllers.py:202-203 -> ppo_bc_policy.py:174-185 ``act(stochastic=True)`` = DiagGaussianPd.sample
+    = mean + exp(logstd) * N(0, 1); TF's own sampler is not restatable, so the engine draws with
+    Philox), as ``[K, A]`` f64.
+
+    Restates the kernel's ``rng_normal`` (csrc/device_common.h): key = seed ^ 0x9E3779B97F4A7C15,
+    counter (lo32(g), hi32(g), h, 0x80000000 | j) for global candidate g; u1 = ((c0 >> 8) + 0.5) / 2^24,
+    u2 = (c1 >> 8) / 2^24 (both exact); z = sqrt(-2 ln u1) cos(2 pi u2) (Box-Muller).  The kernel
+    evaluates the transcendentals in f32 (a few ulp); this restatement does so in f64, so the two agree
+    to ~1e-6 relative, not bitwise."""
+    key = (seed ^ POLICY_NORMAL_KEY_XOR) & 0xFFFFFFFFFFFFFFFF
+    k0, k1 = key & 0xFFFFFFFF, (key >> 32) & 0xFFFFFFFF
+    g = np.arange(K, dtype=np.uint64) + np.uint64(cand_offset)
+    out = np.empty((K, A), dtype=np.float64)
+    for j in range(A):
+        r = philox4x32_10(g & _M32, g >> np.uint64(32), np.full(K, h, np.uint64),
+                          np.full(K, 0x80000000 | j, np.uint64), k0, k1)
+        u1 = ((r[0] >> np.uint32(8)).astype(np.float64) + 0.5) / 16777216.0
+        u2 = (r[1] >> np.uint32(8)).astype(np.float64) / 16777216.0
+        out[:, j] = np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+    return out
+
+
 # ----------------------------------------------------------------------------
 # CEM outer loop (BASELINE cfg5; NOT in the reference -- semantics defined in
 # DESIGN.md "CEM" and restated here exactly as the engine computes them)

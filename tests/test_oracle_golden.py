@@ -111,3 +111,15 @@ def test_reward_sum_is_sequential_in_h():
     for i in range(1, 23):
         seq = seq + a[i]
     assert np.array_equal(np.sum(a, axis=0), seq)
+
+
+def test_device_rng_normals_restatement_is_standard_normal():
+    """oracle.device_rng_normals (the stochastic policy's Philox Box-Muller, csrc/device_common.h
+    rng_normal): deterministic, shard-consistent, and N(0, 1) over 1e5 draws (the GPU-side pin is
+    tests/test_gpu_parity.py::test_policy_stochastic_mode_pinned_every_step)."""
+    from oracle import mpc_oracle as orc
+    a = orc.device_rng_normals(42, 0, 20000, 3, 6)
+    b = orc.device_rng_normals(42, 5000, 1000, 3, 6)
+    assert np.array_equal(a[5000:6000], b)
+    assert not np.array_equal(a, orc.device_rng_normals(42, 0, 20000, 4, 6))
+    assert abs(a.mean()) < 0.01 and abs(a.std() - 1.0) < 0.01
