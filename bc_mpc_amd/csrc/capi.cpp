@@ -902,17 +902,17 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
 // ---- NumPy-stream draw on the device -------------------------------------------------------
 // Generator words per chunk (one workgroup each; BCMPC_MT_CHUNK_WORDS overrides) and coefficient
 // slices per jump polynomial (BCMPC_MT_SPLITS): chunks trade jump work (one 624 x 19937 GF(2)
-// correlation each, ~0.24 us of the whole chip, VALU-bound) against serial generation (~0.5 words
-// per ns per workgroup).  cfg3 (15.7M words): 2^15 words -> 480 chunks x 17 slices, draw ~0.2 ms
+// correlation each, ~0.35 us of the whole chip, VALU-bound) against serial generation (~0.9 words
+// per ns per workgroup).  cfg3 (15.7M words): 2^16 words -> 240 chunks x 17 slices, draw ~0.18 ms
 // (tools/mt_device_sweep.py, profiles/r02_mt_device_sweep.txt).
 static int64_t mt_chunk_words() {
     const char* v = std::getenv("BCMPC_MT_CHUNK_WORDS");
-    return (v && *v) ? std::max<int64_t>(2, std::atoll(v)) & ~int64_t(1) : int64_t(1) << 15;
+    return (v && *v) ? std::max<int64_t>(2, std::atoll(v)) & ~int64_t(1) : int64_t(1) << 16;
 }
 static int mt_splits(int cj) {
     const char* v = std::getenv("BCMPC_MT_SPLITS");
     if (v && *v) return std::max(1, std::min(64, std::atoi(v)));
-    return std::max(2, std::min(32, (8192 + cj - 1) / std::max(1, cj)));
+    return std::max(2, std::min(32, (4096 + cj - 1) / std::max(1, cj)));
 }
 static bool mt_device_path() {
     const char* v = std::getenv("BCMPC_MT_PATH");

@@ -34,7 +34,8 @@ namespace {
 constexpr int kWave = 64;                 // mt_jump_kernel: one wave per (chunk, coefficient slice)
 constexpr int kGen = 256;                 // generators: 4 waves (a phase is 227 independent words)
 constexpr int kLag = 227;                 // 624 - 397: words producible in parallel
-constexpr int kRing = 2048;               // generator ring (words), power of two
+constexpr int kRing = 4096;               // generator ring (words), power of two
+constexpr int kBatch = 12;                // generator phases between emission passes
 constexpr int kQ = 10;                    // jump: window words m per lane (64 x 10 >= 624)
 
 __device__ __forceinline__ uint32_t mix(uint32_t a, uint32_t b) {
@@ -50,30 +51,52 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
     return y;
 }
 
-// one phase: ring words [n0, n0 + 227) from the 624 before them (227 independent words)
-__device__ __forceinline__ void gen_phase(uint32_t* ring, int64_t n0) {
-    for (int t = threadIdx.x; t < kLag; t += kGen) {
-        const int64_t n = n0 + t;
-        ring[n & (kRing - 1)] = ring[(n - kLag) & (kRing - 1)] ^
-                                mix(ring[(n - kMtN) & (kRing - 1)], ring[(n - kMtN + 1) & (kRing - 1)]);
+// The register-chained generator.  Thread t < 227 owns word n = 624 + 227 P + t of every phase P
+// (local stream index): it keeps its previous word y[n - 227] in a register and has the two older
+// operands y[n - 624], y[n - 623] -- words of phases <= P - 1, i.e. published by the barrier that
+// ended the previous interval -- fetched one interval ahead.  An interval is then one mix + XOR and
+// one LDS store on the critical path, and one barrier per 227 words; the prefetch (and whatever work
+// the caller puts in the interval) hides the LDS latency.  Ring slots written in phase P alias words
+// >= 1400 older than anything read.
+struct Chain {
+    uint32_t prev = 0, a = 0, b = 0;
+    int64_t n = 0;
+    // ring words [0, 624) hold the start window
+    __device__ __forceinline__ void init(const uint32_t* ring, int t) {
+        n = kMtN + t;
+        if (t < kLag) {
+            prev = ring[kMtN - kLag + t];
+            a = ring[t];
+            b = ring[t + 1];
+        }
     }
-    __syncthreads();
-}
+    // produce word n (threads < 227), store it, fetch the operands of the next phase
+    __device__ __forceinline__ uint32_t step(uint32_t* ring, int t) {
+        uint32_t v = 0;
+        if (t < kLag) {
+            v = prev ^ mix(a, b);
+            ring[n & (kRing - 1)] = v;
+            prev = v;
+            a = ring[(n + kLag - kMtN) & (kRing - 1)];
+            b = ring[(n + kLag - kMtN + 1) & (kRing - 1)];
+        }
+        n += kLag;
+        return v;
+    }
+};
 
 // x[0 .. kMtStream) = y[624 ..): block 1 onwards, the stream every jump correlates with
 __global__ __launch_bounds__(kGen) void mt_stream_kernel(const uint32_t* __restrict__ in,
                                                          uint32_t* __restrict__ xs) {
     __shared__ uint32_t ring[kRing];
-    for (int i = threadIdx.x; i < kMtN; i += kGen) ring[i] = in[i];
+    const int t = threadIdx.x;
+    for (int i = t; i < kMtN; i += kGen) ring[i] = in[i];
     __syncthreads();
+    Chain ch;
+    ch.init(ring, t);
     for (int64_t n0 = kMtN; n0 < kMtN + kMtStream; n0 += kLag) {
-        for (int t = threadIdx.x; t < kLag; t += kGen) {
-            const int64_t n = n0 + t;
-            const uint32_t v = ring[(n - kLag) & (kRing - 1)] ^
-                               mix(ring[(n - kMtN) & (kRing - 1)], ring[(n - kMtN + 1) & (kRing - 1)]);
-            ring[n & (kRing - 1)] = v;
-            if (n - kMtN < kMtStream) xs[n - kMtN] = v;
-        }
+        const uint32_t v = ch.step(ring, t);
+        if (t < kLag && n0 + t - kMtN < kMtStream) xs[n0 + t - kMtN] = v;
         __syncthreads();
     }
 }
@@ -147,22 +170,23 @@ __global__ __launch_bounds__(kGen) void mt_gen_kernel(MtDrawArgs a) {
     int64_t avail = kMtN;                                 // local words [0, avail) generated
     int64_t e_done = 0;                                   // doubles emitted
     const int64_t need = o + 2 * nd;                      // words the chunk reads
+    Chain gen;
+    gen.init(ring, t);
     while (e_done < nd) {
-        // one interval: the next phase's 227 words (threads < 227) and, alongside, every double
-        // whose two words were generated before this interval (~114 in steady state) -- the
-        // emission fills the LDS-latency bubbles of the phase; one barrier per 227 words.  Ring
-        // slots written here alias words < avail - 1821, all emitted and older than the phase's
-        // reads (>= avail - 624).
+        // up to kBatch chain intervals (2724 words; the ring keeps them + 624 words of history +
+        // one pending word), then one emission pass over every double whose two words exist: the
+        // emission's latency chain (LDS, tempering, f64) overlaps across a thread's ~5 doubles
+        // instead of sitting in every interval
+        for (int k = 0; k < kBatch && avail < need; ++k) {
+            (void)gen.step(ring, t);
+            avail += kLag;
+            __syncthreads();
+        }
         const int64_t e_avail = avail > o ? (avail - o) / 2 : 0;
         const int64_t e_end = e_avail < nd ? e_avail : nd;
-        if (avail < need && t < kLag) {
-            const int64_t n = avail + t;
-            ring[n & (kRing - 1)] = ring[(n - kLag) & (kRing - 1)] ^
-                                    mix(ring[(n - kMtN) & (kRing - 1)], ring[(n - kMtN + 1) & (kRing - 1)]);
-        }
         if (ch.out0 >= 0) {
             int jj = (ch.j0 + (int)(e_done + t)) % A;      // action column, advanced by kGen per pass
-            const int step = kGen % A;
+            const int stride = kGen % A;
             for (int64_t e = e_done + t; e < e_end; e += kGen) {
                 const int64_t l = o + 2 * e;
                 const uint32_t wa = temper(ring[l & (kRing - 1)]) >> 5;
@@ -171,12 +195,11 @@ __global__ __launch_bounds__(kGen) void mt_gen_kernel(MtDrawArgs a) {
                 const double d = (double)(((uint64_t)wa << 26) | wb) * 0x1p-53;
                 const double lo = low[jj];
                 a.out[ch.out0 + e] = __dadd_rn(lo, __dmul_rn(__dsub_rn(high[jj], lo), d));
-                jj += step;
+                jj += stride;
                 if (jj >= A) jj -= A;
             }
         }
         e_done = e_end;
-        if (avail < need) avail += kLag;
         __syncthreads();
     }
     if (ch.final_) {
@@ -185,8 +208,9 @@ __global__ __launch_bounds__(kGen) void mt_gen_kernel(MtDrawArgs a) {
         const int64_t last = o + ch.n - 1;
         const int64_t b0 = (last / kMtN) * kMtN;
         while (avail < b0 + kMtN) {
-            gen_phase(ring, avail);
+            (void)gen.step(ring, t);
             avail += kLag;
+            __syncthreads();
         }
         for (int i = t; i < kMtN; i += kGen) a.final_state[i] = ring[(b0 + i) & (kRing - 1)];
         if (t == 0) a.final_state[kMtN] = (uint32_t)(last - b0 + 1);

@@ -25,8 +25,8 @@ def main():
     state = rs.randn(S) * 0.1
     low, high = -np.ones(A), np.ones(A)
     settings = [("default", None, None)]
-    for w in (1 << 14, 1 << 15, 1 << 16, 1 << 17):
-        for sp in (4, 8, 16, 32):
+    for w in (32768, 49152, 65536, 98304):
+        for sp in (8, 16, 32):
             settings.append((f"w{w}_s{sp}", w, sp))
     base = None
     for name, w, sp in settings:
