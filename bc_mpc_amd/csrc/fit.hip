@@ -400,6 +400,493 @@ __global__ void fit_adam(float* __restrict__ w, float* __restrict__ m, float* __
 }
 
 
+// ------------------------------------------------------------- fused step ---
+// One Adam iteration in two launches (BCMPC_FIT_FUSED, default on):
+//   fit_rows_kernel   one workgroup per 16 batch rows: gather, every forward layer (MFMA row-tile
+//                     GEMM + act + LayerNorm in LDS), output, loss partial, dP, and every backward
+//                     data gradient (dH_l = dZ_{l+1} W_{l+1}^T, LN / act backward -> dZ_l), plus the
+//                     LayerNorm column partials of its 16 rows -- all row-local given the weights,
+//                     so no workgroup waits for another;
+//   fit_params_kernel one workgroup per 16 x 16 weight tile (the bias is the tile row k == in, fed
+//                     by a column of ones: db = 1^T dZ on the same MFMAs) or per 64 LayerNorm
+//                     columns: the batch reduction in a fixed order, then TF1 ApplyAdam in place.
+// The kernel boundary is the only global synchronisation of the step.  Every global load after it
+// comes from HBM / MALL (the previous launch wrote it on other XCDs), ~1-2 us per dependent trip, so
+// the structure minimises dependent trips: all weights of a GEMM are requested before the first
+// MFMA needs them, the backward GEMMs read a transposed weight copy (coalesced rows; the params
+// kernel keeps it in step), LayerNorm parameters, activations and row statistics stay in LDS.
+// Same row arithmetic as the per-op kernels above (fit_act_fwd / fit_act_bwd / fit_loss verbatim);
+// only the GEMM and batch-sum orders differ.
+constexpr int kFR = 16;                     // batch rows per row-block workgroup (one MFMA row tile)
+constexpr int kFW = 16;                     // waves of the row-block workgroup
+constexpr int kFK = 8;                      // k-steps (of 4) per weight chunk
+constexpr int kFRing = 4;                   // weight chunks in flight per wave
+constexpr int kPK = 32;                     // batch steps (of 4) per load batch of a weight-gradient tile
+
+struct FitTile {                            // fit_params_kernel work item (one workgroup)
+    int32_t kind;                           // 0: weight tile (+ bias row), 1: LayerNorm columns, 3: loss
+    int32_t layer;
+    int32_t k0, n0;                         // weight tile origin / first column
+};
+
+struct FusedArgs {
+    const double* st; const double* ac; const double* de;
+    const int64_t* idx_base; int32_t stride; int32_t* iter;
+    const double* nc;
+    float* w; float* wt; float* m; float* v;            // params, transposed kernel copy, Adam slots
+    int32_t w_off[BCMPC_MAX_LAYERS + 1], b_off[BCMPC_MAX_LAYERS + 1];
+    int32_t g_off[BCMPC_MAX_LAYERS], be_off[BCMPC_MAX_LAYERS];
+    float* x0; float* t; float* p; float* dp;
+    float* act; float* hln;                             // [L][Bmax][h]
+    float* dzs;                                         // [L][Bmax][h]
+    float* lnpart;                                      // [L][nblk][2][h] LayerNorm column partials
+    float* loss_part; float* loss; float* bp;
+    const FitTile* tiles; int32_t ntiles;
+    int32_t B, Bmax, S, A, IN, L, h, act_kind, ln, ldw;
+    float lr, b1, b2, eps;
+};
+
+// one chunk of kFK k-steps of the B operand through a buffer descriptor: one 32-bit lane offset
+// (vo) for the whole GEMM, the chunk position in the scalar offset; rows past the matrix and the
+// masked columns (vo beyond the range) read 0
+__device__ __forceinline__ void rows_load(float* b, __amdgpu_buffer_rsrc_t rsrc, int vo, int kb, int kstride) {
+#pragma unroll
+    for (int s = 0; s < kFK; ++s)
+        b[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo, (kb + 4 * s) * kstride, 0));
+}
+
+__device__ __forceinline__ f4v rows_mma(f4v acc, const float* b, const float* X, int kb, int K, int r16, int k4,
+                                        int lds) {
+#pragma unroll
+    for (int s = 0; s < kFK; ++s) {
+        const int k = kb + 4 * s + k4;
+        const float x = k < K ? X[r16 * lds + k] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x, b[s], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+// Every weight load of a GEMM has been consumed by its end, but the compiler's wait analysis cannot
+// see it through the conditional prefetches and keeps them "pending": the row phase after the GEMM
+// then gets vmcnt(0) waits at register reuse -- which also wait for that phase's own global stores,
+// a full HBM write trip (~2 us) per phase.  A real s_waitcnt vmcnt(0) here (nothing is in flight by
+// then) clears the analysis.
+__device__ __forceinline__ void rows_drained() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
+}
+
+// acc += sum over k in [k0, k1) of X[r][k] W[k*ldw + n] for this lane's column n (a 16-wide tile),
+// kFRing chunks of weights in flight
+__device__ __forceinline__ f4v rows_tile(f4v acc, const float* X, int k0, int k1, __amdgpu_buffer_rsrc_t rsrc,
+                                         int vo, int ldw, int r16, int k4, int lds) {
+    constexpr int CK = 4 * kFK;
+    float ring[kFRing][kFK];
+#pragma unroll
+    for (int j = 0; j < kFRing; ++j)
+        if (k0 + j * CK < k1) rows_load(ring[j], rsrc, vo, k0 + j * CK, 4 * ldw);
+    for (int kb = k0; kb < k1; kb += kFRing * CK) {
+#pragma unroll
+        for (int j = 0; j < kFRing; ++j) {
+            const int kc = kb + j * CK;
+            if (kc < k1) {
+                acc = rows_mma(acc, ring[j], X, kc, k1, r16, k4, lds);
+                if (kc + kFRing * CK < k1) rows_load(ring[j], rsrc, vo, kc + kFRing * CK, 4 * ldw);
+            }
+        }
+    }
+    return acc;
+}
+
+// C[r][n] = sum_k X[r][k] W[k*ldw + n] (+ bias[n]) for the 16 LDS rows X (stride lds), n < N, W row-major
+// [K][ldw].  16-column tiles over the 16 waves; when there are fewer tiles than waves (the [h -> S]
+// output layer) the K range is split over the idle waves and the partials (LDS, `kp`) are added in
+// wave order.
+__device__ __forceinline__ void rows_gemm(const float* X, int K, const float* __restrict__ W, int ldw, int N,
+                          const float* __restrict__ bias, float* C, int lds, float* kp) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int r16 = lane & 15, k4 = lane >> 4;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W), 0, K * ldw * 4, 0x00020000);
+    const int nt = (N + 15) / 16;
+    if (nt * 2 > kFW) {
+        for (int n0 = 16 * wv; n0 < N; n0 += 16 * kFW) {
+            const int n = n0 + r16;
+            const int vo = n < N ? (k4 * ldw + n) * 4 : 0x40000000;
+            const float bv = bias && n < N ? bias[n] : 0.f;          // requested before the weights
+            f4v acc = rows_tile((f4v){0.f, 0.f, 0.f, 0.f}, X, 0, K, rsrc, vo, ldw, r16, k4, lds);
+            rows_drained();
+            if (n < N)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) C[(4 * k4 + r) * lds + n] = bias ? acc[r] + bv : acc[r];
+        }
+        return;
+    }
+    // K split: wave wv takes tile wv % nt, K slice wv / nt of ks (whole 4-k-steps)
+    const int ks = kFW / nt;
+    const int t = wv % nt, q = wv / nt;
+    const int n = 16 * t + r16;
+    if (q < ks) {
+        const int kq = ((K + 4 * ks - 1) / (4 * ks)) * 4;       // slice length, multiple of 4
+        const int k0 = min(K, q * kq), k1 = min(K, k0 + kq);
+        const int vo = n < N ? (k4 * ldw + n) * 4 : 0x40000000;
+        f4v acc = (f4v){0.f, 0.f, 0.f, 0.f};
+        if (k0 < k1) acc = rows_tile(acc, X, k0, k1, rsrc, vo, ldw, r16, k4, lds);
+        rows_drained();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) kp[(q * nt + t) * 256 + (4 * k4 + r) * 16 + r16] = acc[r];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 16 * nt * 16; i += 64 * kFW) {
+        const int tt = i / 256, e = i % 256, r = e / 16, c = 16 * tt + e % 16;
+        if (c < N) {
+            float s = 0.f;
+            for (int qq = 0; qq < ks; ++qq) s += kp[(qq * nt + tt) * 256 + e];
+            C[r * lds + c] = bias ? s + bias[c] : s;
+        }
+    }
+}
+
+// wave sum without the LDS crossbar: DPP butterflies inside each 16-lane row (quad_perm xor 1, xor 2,
+// row_ror 4, 8), then the four row totals in a fixed order (deterministic, wave-uniform)
+template <int CTRL>
+__device__ __forceinline__ float dpp_t(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_fast(float v) {
+    v += dpp_t<0xB1>(v);                    // quad_perm [1,0,3,2]
+    v += dpp_t<0x4E>(v);                    // quad_perm [2,3,0,1]
+    v += dpp_t<0x124>(v);                   // row_ror 4
+    v += dpp_t<0x128>(v);                   // row_ror 8
+    const int b = __builtin_bit_cast(int, v);
+    return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+           (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+            __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
+
+__device__ __forceinline__ float adam_elem(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                           size_t i, float gi, float w0, float m0, float v0, float lr_t, float b1,
+                                           float b2, float eps) {
+    const float mi = m0 + (gi - m0) * (1.0f - b1);
+    const float vi = v0 + (gi * gi - v0) * (1.0f - b2);
+    const float wi = w0 - (mi * lr_t) / (sqrtf(vi) + eps);
+    m[i] = mi;
+    v[i] = vi;
+    w[i] = wi;
+    return wi;
+}
+
+__global__ __launch_bounds__(1024) void fit_rows_kernel(const FusedArgs a) {
+    extern __shared__ float sm[];
+    const int ld = a.ldw, S = a.S, IN = a.IN, L = a.L, h = a.h;
+    float* bufA = sm;                       // [16][ld]: the current layer input / backward operand
+    float* bufB = bufA + kFR * ld;          // [16][ld]: GEMM output
+    float* bufC = bufB + kFR * ld;          // [16][ld]: dH * xhat (LayerNorm backward)
+    float* tsm = bufC + kFR * ld;           // [16][32] targets
+    float* red = tsm + kFR * 32;            // [kFW] loss partials per wave
+    float* kp = red + kFW;                  // [kFW][256] K-split partials
+    float* stat = kp + kFW * 256;           // [L][2][16] row mean / rs
+    float* prm = stat + L * 2 * kFR;        // [L][2][h] LayerNorm gamma, beta (LN nets)
+                                            // (every pointer the row phases read is LDS: no flat
+                                            //  loads, whose waits would include the pending stores)
+    float* acache = prm + 2 * L * h;        // [L][16][ld] activation rows A_l
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int r0 = blockIdx.x * kFR;
+    const int nr = min(kFR, a.B - r0);
+    const int it = *a.iter;
+    const int64_t* idx = a.idx_base + (int64_t)it * a.stride;
+#ifdef BCMPC_FIT_STAMPS     // timing-only build: phase boundaries of workgroup 0, printed for iteration 5
+    uint64_t stamps[40];
+    int nst = 0;
+    stamps[nst++] = __builtin_amdgcn_s_memrealtime();
+#define FIT_STAMP() do { if (nst < 40) stamps[nst++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define FIT_STAMP() do { } while (0)
+#endif
+    if (blockIdx.x == 0 && tid == 0 && it > 0) {          // (fit_loss: the previous iteration's finish)
+        a.bp[0] = __fmul_rn(a.bp[0], a.b1);
+        a.bp[1] = __fmul_rn(a.bp[1], a.b2);
+    }
+    // ---- gather (fit_gather), LayerNorm parameters into LDS ----
+    if (a.ln)
+        for (int i = tid; i < 2 * L * h; i += 64 * kFW) {
+            const int l = i / (2 * h), j = i % (2 * h);
+            prm[i] = j < h ? a.w[a.g_off[l] + j] : a.w[a.be_off[l] + j - h];
+        }
+    const double* nc = a.nc;
+    for (int i = tid; i < kFR * (IN + S); i += 64 * kFW) {
+        const int r = i / (IN + S), c = i % (IN + S);
+        float val = 0.f;
+        if (r < nr) {
+            const int64_t row = idx[r0 + r];
+            if (c < S) val = (float)__ddiv_rn(__dsub_rn(a.st[row * S + c], nc[0 * 32 + c]), nc[1 * 32 + c]);
+            else if (c < IN) val = (float)__ddiv_rn(__dsub_rn(a.ac[row * a.A + c - S], nc[2 * 32 + c - S]), nc[3 * 32 + c - S]);
+            else val = (float)__ddiv_rn(__dsub_rn(a.de[row * S + c - IN], nc[4 * 32 + c - IN]), nc[5 * 32 + c - IN]);
+        }
+        if (c < IN) {
+            bufA[r * ld + c] = val;
+            if (r < nr) a.x0[(size_t)(r0 + r) * IN + c] = val;
+        } else {
+            tsm[r * 32 + c - IN] = val;
+            if (r < nr) a.t[(size_t)(r0 + r) * S + c - IN] = val;
+        }
+    }
+    __syncthreads();
+    FIT_STAMP();
+    const size_t BH = (size_t)a.Bmax * h;
+    // ---- forward (fit_act_fwd per row: one row per wave) ----
+    for (int l = 0; l < L; ++l) {
+        rows_gemm(bufA, l == 0 ? IN : h, a.w + a.w_off[l], h, h, a.w + a.b_off[l], bufB, ld, kp);
+        __syncthreads();
+        FIT_STAMP();
+        {
+            const int r = wv;
+            float* z = bufB + r * ld;
+            float* hx = bufA + r * ld;
+            float* ac = acache + (l * kFR + r) * ld;
+            const size_t go = (size_t)l * BH + (size_t)(r0 + r) * h;
+            float s = 0.f;
+#pragma unroll 4
+            for (int f = lane; f < h; f += 64) {
+                float v = z[f];
+                v = a.act_kind == BCMPC_ACT_RELU ? fmaxf(v, 0.f) : tanhf(v);
+                z[f] = v;
+                s += v;
+                ac[f] = v;
+                if (r < nr) a.act[go + f] = v;
+            }
+            if (!a.ln) {
+                for (int f = lane; f < h; f += 64) hx[f] = z[f];
+            } else {
+                const float mean = wave_sum_fast(s) / (float)h;
+                float ss = 0.f;
+    #pragma unroll 4
+            for (int f = lane; f < h; f += 64) {
+                    const float d = z[f] - mean;
+                    ss += d * d;
+                }
+                const float var = wave_sum_fast(ss) / (float)h;
+                const float rs = 1.0f / sqrtf(var + 1e-12f);
+                const float* g = prm + 2 * l * h;
+                const float* be = prm + 2 * l * h + h;
+    #pragma unroll 4
+            for (int f = lane; f < h; f += 64) {
+                    const float inv = rs * g[f];
+                    const float hv = z[f] * inv + (be[f] - mean * inv);
+                    hx[f] = hv;
+                    if (r < nr) a.hln[go + f] = hv;
+                }
+                if (lane == 0) {
+                    stat[(l * 2 + 0) * kFR + r] = mean;
+                    stat[(l * 2 + 1) * kFR + r] = rs;
+                }
+            }
+        }
+        __syncthreads();
+        FIT_STAMP();
+    }
+    // ---- output, loss partial, dP = -((2 * (1/N)) * (T - P)) (fit_loss) ----
+    rows_gemm(bufA, h, a.w + a.w_off[L], S, S, a.w + a.b_off[L], bufB, ld, kp);
+    __syncthreads();
+    FIT_STAMP();
+    const float inv = 1.0f / (float)(a.B * S);
+    float sl = 0.f;
+    for (int i = tid; i < kFR * S; i += 64 * kFW) {
+        const int r = i / S, c = i % S;
+        float g = 0.f;
+        if (r < nr) {
+            const float pv = bufB[r * ld + c];
+            const float d = tsm[r * 32 + c] - pv;
+            sl += d * d;
+            g = -((2.0f * inv) * d);
+            a.p[(size_t)(r0 + r) * S + c] = pv;
+            a.dp[(size_t)(r0 + r) * S + c] = g;
+        }
+        bufA[r * ld + c] = g;
+    }
+    sl = wave_sum_fast(sl);
+    if (lane == 0) red[wv] = sl;
+    __syncthreads();
+    FIT_STAMP();
+    if (tid == 0) {
+        float t = 0.f;
+        for (int w = 0; w < kFW; ++w) t += red[w];
+        a.loss_part[blockIdx.x] = t;
+    }
+    // ---- backward data gradients (fit_act_bwd per row), LayerNorm column partials ----
+    const int nblk = (a.B + kFR - 1) / kFR;
+    for (int l = L - 1; l >= 0; --l) {
+        const int out = l + 1 == L ? S : h;                 // dZ_{l+1} width; W_{l+1}^T is [out][h]
+        rows_gemm(bufA, out, a.wt + a.w_off[l + 1], h, h, nullptr, bufB, ld, kp);
+        __syncthreads();
+        FIT_STAMP();
+        {
+            const int r = wv;
+            float* dh = bufB + r * ld;
+            float* dz = bufA + r * ld;
+            float* gx = bufC + r * ld;
+            const size_t go = (size_t)l * BH + (size_t)(r0 + r) * h;
+            if (r >= nr) {
+    #pragma unroll 4
+            for (int f = lane; f < h; f += 64) {
+                    dz[f] = 0.f;
+                    dh[f] = 0.f;
+                    gx[f] = 0.f;
+                }
+            } else {
+                const float* av = acache + (l * kFR + r) * ld;
+                const float* g = prm + 2 * l * h;
+                float dmean = 0.f, drs = 0.f, mean = 0.f, rs = 0.f;
+                if (a.ln) {
+                    mean = stat[(l * 2 + 0) * kFR + r];
+                    rs = stat[(l * 2 + 1) * kFR + r];
+                    float s1 = 0.f, s2 = 0.f;
+        #pragma unroll 4
+            for (int f = lane; f < h; f += 64) {
+                        s1 += dh[f] * rs * g[f];
+                        s2 += dh[f] * (av[f] - mean) * g[f];
+                    }
+                    dmean = -wave_sum_fast(s1);
+                    drs = wave_sum_fast(s2);
+                }
+                const float dvar = -0.5f * drs * rs * rs * rs;
+    #pragma unroll 4
+            for (int f = lane; f < h; f += 64) {
+                    float da = dh[f];
+                    const float avv = av[f];
+                    if (a.ln) {
+                        da = dh[f] * rs * g[f] + dmean / (float)h + dvar * 2.0f * (avv - mean) / (float)h;
+                        gx[f] = dh[f] * (avv - mean) * rs;            // (fit_colsum's gamma term)
+                    }
+                    const float dzv = a.act_kind == BCMPC_ACT_RELU ? (avv > 0.f ? da : 0.f) : da * (1.0f - avv * avv);
+                    a.dzs[go + f] = dzv;
+                    dz[f] = dzv;
+                }
+            }
+        }
+        __syncthreads();
+        FIT_STAMP();
+        if (a.ln) {                                       // this block's 16-row column sums, rows in order
+            for (int f = tid; f < h; f += 64 * kFW) {
+                float sb = 0.f, sg = 0.f;
+                for (int r = 0; r < kFR; ++r) {
+                    sb += bufB[r * ld + f];
+                    sg += bufC[r * ld + f];
+                }
+                float* lp = a.lnpart + ((size_t)(l * nblk + blockIdx.x) * 2) * h;
+                lp[f] = sb;
+                lp[h + f] = sg;
+            }
+            __syncthreads();                              // (bufB is the next GEMM's output)
+        }
+    }
+#ifdef BCMPC_FIT_STAMPS
+    if (blockIdx.x == 0 && tid == 0 && it == 5) {
+        for (int k = 1; k < nst; ++k) printf("stamp %d %.2f us\n", k, (double)(stamps[k] - stamps[0]) * 0.01);
+    }
+#endif
+#undef FIT_STAMP
+}
+
+// one workgroup per task; its 4 waves take contiguous quarters of the batch (of the row blocks for
+// LayerNorm columns) and their partials are added in wave order (deterministic)
+__global__ __launch_bounds__(256) void fit_params_kernel(const FusedArgs a) {
+    __shared__ float part[4][2][64];        // column-sum partials per wave
+    __shared__ float tp[4][4][64];          // weight-tile partials per wave
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int B = a.B, S = a.S, IN = a.IN, L = a.L, h = a.h;
+    const size_t BH = (size_t)a.Bmax * h;
+    const FitTile tl = a.tiles[blockIdx.x];
+    const int l = tl.layer;
+    if (tl.kind == 3) {
+        // the loss (fixed row-block order) and the iteration counter (fit_loss)
+        if (threadIdx.x == 0) {
+            const int it = *a.iter;
+            float tot = 0.f;
+            for (int k = 0; k < (B + kFR - 1) / kFR; ++k) tot += a.loss_part[k];
+            a.loss[it] = tot * (1.0f / (float)(B * S));
+            *a.iter = it + 1;
+        }
+        return;
+    }
+    const float lr_t = __fdiv_rn(__fmul_rn(a.lr, __fsqrt_rn(__fsub_rn(1.0f, a.bp[1]))), __fsub_rn(1.0f, a.bp[0]));
+    if (tl.kind == 0) {
+        // dW_l[k][n] = sum_b Hin[b][k] dZ[b][n], row k == in of the tile: the bias (Hin = 1)
+        // (A = Hin^T: lane (k = r16, b = k4); B = dZ: (b = k4, n = r16))
+        const int in = l == 0 ? IN : h, out = l == L ? S : h;
+        const float* Hin = l == 0 ? a.x0 : (a.ln ? a.hln : a.act) + (size_t)(l - 1) * BH;
+        const float* dZ = l == L ? a.dp : a.dzs + (size_t)l * BH;
+        const int r16 = lane & 15, k4 = lane >> 4;
+        const int k = tl.k0 + r16, n = tl.n0 + r16;
+        // this lane's Adam operands (wave 0 updates), requested with the gradient operands
+        float w0[4], m0[4], v0[4];
+        size_t pi[4];
+        if (wv == 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int kk = tl.k0 + 4 * k4 + r;
+                pi[r] = kk < in ? (size_t)a.w_off[l] + (size_t)kk * out + n : (size_t)a.b_off[l] + n;
+                const bool ok = kk <= in && n < out;
+                w0[r] = ok ? a.w[pi[r]] : 0.f;
+                m0[r] = ok ? a.m[pi[r]] : 0.f;
+                v0[r] = ok ? a.v[pi[r]] : 0.f;
+            }
+        const int q0 = (B * wv) / 4, q1 = (B * (wv + 1)) / 4;
+        f4v acc = (f4v){0.f, 0.f, 0.f, 0.f};
+        for (int bb = q0; bb < q1; bb += 4 * kPK) {
+            float x[kPK], y[kPK];
+#pragma unroll
+            for (int s = 0; s < kPK; ++s) {
+                const int b = bb + 4 * s + k4;
+                x[s] = b < q1 ? (k < in ? Hin[(size_t)b * in + k] : (k == in ? 1.f : 0.f)) : 0.f;
+                y[s] = (b < q1 && n < out) ? dZ[(size_t)b * out + n] : 0.f;
+            }
+#pragma unroll
+            for (int s = 0; s < kPK; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], y[s], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tp[wv][r][lane] = acc[r];
+        __syncthreads();
+        if (wv == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float gsum = ((tp[0][r][lane] + tp[1][r][lane]) + tp[2][r][lane]) + tp[3][r][lane];
+                const int kk = tl.k0 + 4 * k4 + r;
+                if (kk <= in && n < out) {
+                    const float wn = adam_elem(a.w, a.m, a.v, pi[r], gsum, w0[r], m0[r], v0[r], lr_t, a.b1, a.b2, a.eps);
+                    if (kk < in && l > 0) a.wt[(size_t)a.w_off[l] + (size_t)n * in + kk] = wn;   // W^T copy
+                }
+            }
+        }
+        return;
+    }
+    // LayerNorm columns: beta = colsum dH, gamma = colsum dH xhat over the row blocks' partials
+    const int nblk = (B + kFR - 1) / kFR;
+    const int q0 = (nblk * wv) / 4, q1 = (nblk * (wv + 1)) / 4;
+    const int n = tl.n0 + lane;
+    const bool ok = n < h;
+    const size_t ib = (size_t)a.be_off[l] + n, ig = (size_t)a.g_off[l] + n;
+    float wb = 0.f, mb = 0.f, vb = 0.f, wg = 0.f, mg = 0.f, vg = 0.f;
+    if (wv == 0 && ok) {
+        wb = a.w[ib]; mb = a.m[ib]; vb = a.v[ib];
+        wg = a.w[ig]; mg = a.m[ig]; vg = a.v[ig];
+    }
+    float s1 = 0.f, s2 = 0.f;
+    if (ok)
+        for (int k = q0; k < q1; ++k) {
+            const float* lp = a.lnpart + ((size_t)(l * nblk + k) * 2) * h;
+            s1 += lp[n];
+            s2 += lp[h + n];
+        }
+    part[wv][0][lane] = s1;
+    part[wv][1][lane] = s2;
+    __syncthreads();
+    if (wv != 0 || !ok) return;
+    const float t1 = ((part[0][0][lane] + part[1][0][lane]) + part[2][0][lane]) + part[3][0][lane];
+    const float t2 = ((part[0][1][lane] + part[1][1][lane]) + part[2][1][lane]) + part[3][1][lane];
+    adam_elem(a.w, a.m, a.v, ib, t1, wb, mb, vb, lr_t, a.b1, a.b2, a.eps);
+    adam_elem(a.w, a.m, a.v, ig, t2, wg, mg, vg, lr_t, a.b1, a.b2, a.eps);
+}
+
 }  // namespace bcmpc
 
 using namespace bcmpc;
@@ -441,6 +928,13 @@ struct bcmpc_fitter {
     const void* graph_loss = nullptr;
     int64_t step = 0;
     bool has_weights = false;
+    // the fused two-launch iteration (fit_rows_kernel + fit_params_kernel)
+    bool fused = false;
+    float *d_wt = nullptr;                        // transposed kernels (layers >= 1), kept by the Adam tiles
+    float *d_dzs = nullptr, *d_lnpart = nullptr, *d_lpart = nullptr;   // [L][B][h], [L][nblk][2][h], [nblk]
+    FitTile* d_tiles = nullptr;
+    int32_t ntiles = 0, rows_ld = 0;
+    size_t rows_lds = 0;
 };
 
 extern "C" {
@@ -492,6 +986,41 @@ int bcmpc_fit_create(const bcmpc_fit_config* c, bcmpc_fitter** out) {
               al((void**)&f->d_cpart, (size_t)kColChunks * 2 * std::max(f->h, f->S) * 4) &&
               al((void**)&f->d_tickets, 64 * 4);
     if (!ok) { bcmpc_fit_destroy(f); return ffail(BCMPC_ERR_HIP, "device allocation failed"); }
+    const char* fe = std::getenv("BCMPC_FIT_FUSED");
+    f->fused = !(fe && fe[0] == '0');
+    if (f->fused) {
+        // LDS of fit_rows_kernel: bufA/B/C, targets, loss partials, K-split partials, row statistics,
+        // then (when it fits) LayerNorm parameters and every hidden layer's activation rows
+        const int wmax = std::max(f->h, std::max(f->IN, f->S));
+        f->rows_ld = (wmax + 3) / 4 * 4 + 4;
+        const size_t base = (size_t)3 * kFR * f->rows_ld + kFR * 32 + kFW + kFW * 256 + 2 * kFR * f->L;
+        const size_t cache = (size_t)2 * f->L * f->h + (size_t)f->L * kFR * f->rows_ld;
+        constexpr size_t kLdsMax = 160 * 1024 / 4;
+        f->rows_lds = (base + cache) * 4;
+        f->fused = base + cache <= kLdsMax;               // (otherwise the per-op kernels)
+    }
+    if (f->fused) {
+        std::vector<FitTile> tl;
+        for (int l = 0; l <= f->L; ++l) {                 // weight tiles incl. the bias row k == in
+            const int in = l == 0 ? f->IN : f->h, o = l == f->L ? f->S : f->h;
+            for (int k0 = 0; k0 <= in; k0 += 16)
+                for (int n0 = 0; n0 < o; n0 += 16) tl.push_back({0, l, k0, n0});
+        }
+        if (c->layer_norm)
+            for (int l = 0; l < f->L; ++l)
+                for (int n0 = 0; n0 < f->h; n0 += 64) tl.push_back({1, l, 0, n0});
+        tl.push_back({3, 0, 0, 0});                       // loss + iteration counter
+        f->ntiles = (int32_t)tl.size();
+        const size_t nblk = (B + kFR - 1) / kFR;
+        ok = al((void**)&f->d_wt, off * 4) && al((void**)&f->d_dzs, L * B * H * 4) &&
+             al((void**)&f->d_lnpart, L * nblk * 2 * H * 4) && al((void**)&f->d_lpart, nblk * 4) &&
+             al((void**)&f->d_tiles, tl.size() * sizeof(FitTile)) &&
+             hipMemcpy(f->d_tiles, tl.data(), tl.size() * sizeof(FitTile), hipMemcpyHostToDevice) == hipSuccess &&
+             (f->rows_lds <= 65536 ||
+              hipFuncSetAttribute((const void*)fit_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)f->rows_lds) == hipSuccess);
+        if (!ok) { bcmpc_fit_destroy(f); return ffail(BCMPC_ERR_HIP, "fused-step allocation failed"); }
+    }
     (void)hipMemset(f->d_m, 0, off * 4);
     (void)hipMemset(f->d_v, 0, off * 4);
     (void)hipMemset(f->d_g, 0, off * 4);
@@ -509,7 +1038,8 @@ int bcmpc_fit_destroy(bcmpc_fitter* f) {
     for (void* p : {(void*)f->d_iter, (void*)f->d_bp, (void*)f->d_cpart, (void*)f->d_tickets, (void*)f->d_w, (void*)f->d_m, (void*)f->d_v, (void*)f->d_g, (void*)f->d_x0, (void*)f->d_t,
                     (void*)f->d_p, (void*)f->d_dp, (void*)f->d_act, (void*)f->d_hln, (void*)f->d_mean,
                     (void*)f->d_rs, (void*)f->d_dh, (void*)f->d_dz, (void*)f->d_loss, (void*)f->d_st,
-                    (void*)f->d_ac, (void*)f->d_de, (void*)f->d_nc, (void*)f->d_idx, (void*)f->d_split})
+                    (void*)f->d_ac, (void*)f->d_de, (void*)f->d_nc, (void*)f->d_idx, (void*)f->d_split,
+                    (void*)f->d_wt, (void*)f->d_dzs, (void*)f->d_lnpart, (void*)f->d_lpart, (void*)f->d_tiles})
         if (p) (void)hipFree(p);
     if (f->stream) (void)hipStreamDestroy(f->stream);
     delete f;
@@ -543,8 +1073,18 @@ int bcmpc_fit_set_params(bcmpc_fitter* f, const bcmpc_weights* w) {
         nc[4 * 32 + i] = i < f->S ? w->mean_deltas[i] : 0.0;
         nc[5 * 32 + i] = i < f->S ? w->std_deltas[i] + 1e-10 : 1.0;
     }
+    std::vector<float> hwt;
+    if (f->fused) {                                   // W_l^T [out][in] at the same offsets (fit_rows_kernel)
+        hwt.assign(f->n_params, 0.f);
+        for (int l = 1; l <= f->L; ++l) {
+            const int in = f->h, o = l == f->L ? f->S : f->h;
+            for (int i = 0; i < in; ++i)
+                for (int j = 0; j < o; ++j) hwt[f->w_off[l] + (size_t)j * in + i] = hw[f->w_off[l] + (size_t)i * o + j];
+        }
+    }
     if (hipSetDevice(f->cfg.device) != hipSuccess ||
         hipMemcpyAsync(f->d_w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice, f->stream) != hipSuccess ||
+        (f->fused && hipMemcpyAsync(f->d_wt, hwt.data(), hwt.size() * 4, hipMemcpyHostToDevice, f->stream) != hipSuccess) ||
         hipMemcpyAsync(f->d_nc, nc, sizeof(nc), hipMemcpyHostToDevice, f->stream) != hipSuccess ||
         hipStreamSynchronize(f->stream) != hipSuccess)
         return ffail(BCMPC_ERR_HIP, "parameter upload failed");
@@ -597,7 +1137,31 @@ int bcmpc_fit_set_data(bcmpc_fitter* f, const double* states, const double* acti
     return BCMPC_OK;
 }
 
+// fused iteration: 2 launches (see fit_rows_kernel / fit_params_kernel)
+static int fit_iteration_fused(bcmpc_fitter* f, const int64_t* d_idx, int stride, int B, float* d_loss) {
+    FusedArgs a{};
+    a.st = f->d_st; a.ac = f->d_ac; a.de = f->d_de;
+    a.idx_base = d_idx; a.stride = stride; a.iter = f->d_iter; a.nc = f->d_nc;
+    a.w = f->d_w; a.wt = f->d_wt; a.m = f->d_m; a.v = f->d_v;
+    for (int l = 0; l <= f->L; ++l) { a.w_off[l] = (int32_t)f->w_off[l]; a.b_off[l] = (int32_t)f->b_off[l]; }
+    for (int l = 0; l < f->L; ++l) { a.g_off[l] = (int32_t)f->g_off[l]; a.be_off[l] = (int32_t)f->be_off[l]; }
+    a.x0 = f->d_x0; a.t = f->d_t; a.p = f->d_p; a.dp = f->d_dp;
+    a.act = f->d_act; a.hln = f->d_hln;
+    a.dzs = f->d_dzs; a.lnpart = f->d_lnpart;
+    a.loss_part = f->d_lpart; a.loss = d_loss; a.bp = f->d_bp;
+    a.tiles = f->d_tiles; a.ntiles = f->ntiles;
+    a.B = B; a.Bmax = f->Bmax; a.S = f->S; a.A = f->A; a.IN = f->IN; a.L = f->L; a.h = f->h;
+    a.act_kind = f->cfg.activation; a.ln = f->cfg.layer_norm ? 1 : 0; a.ldw = f->rows_ld;
+    a.lr = f->cfg.learning_rate; a.b1 = f->cfg.beta1; a.b2 = f->cfg.beta2; a.eps = f->cfg.epsilon;
+    hipLaunchKernelGGL(fit_rows_kernel, dim3((B + kFR - 1) / kFR), dim3(64 * kFW), f->rows_lds, f->stream, a);
+    if (hipGetLastError() != hipSuccess) return ffail(BCMPC_ERR_HIP, "fit_rows_kernel launch failed");
+    hipLaunchKernelGGL(fit_params_kernel, dim3(f->ntiles), dim3(256), 0, f->stream, a);
+    if (hipGetLastError() != hipSuccess) return ffail(BCMPC_ERR_HIP, "fit_params_kernel launch failed");
+    return BCMPC_OK;
+}
+
 static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int stride, int B, float* d_loss) {
+    if (f->fused) return fit_iteration_fused(f, d_idx, stride, B, d_loss);
     hipStream_t st = f->stream;
     const int S = f->S, IN = f->IN, L = f->L, h = f->h, act = f->cfg.activation, ln = f->cfg.layer_norm;
     const size_t BH = (size_t)f->Bmax * h;

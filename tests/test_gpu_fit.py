@@ -25,7 +25,11 @@ def _data(n, S=20, A=6, seed=5):
 
 @pytest.mark.parametrize("hidden,L,act,ln,B", [(64, 2, "tanh", False, 128), (256, 2, "relu", True, 512),
                                               (500, 2, "tanh", False, 512), (96, 3, "tanh", True, 77)])
-def test_fit_matches_oracle(hidden, L, act, ln, B):
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_fit_matches_oracle(hidden, L, act, ln, B, fused, monkeypatch):
+    """fused: the two-launch iteration (fit_rows_kernel + fit_params_kernel, the default);
+    "0": the per-op kernels (BCMPC_FIT_FUSED=0)."""
+    monkeypatch.setenv("BCMPC_FIT_FUSED", fused)
     from bc_mpc_amd.engine import MLPSpec
     from bc_mpc_amd.fit import GPUFitter
     lr, iters = 1e-3, 6
