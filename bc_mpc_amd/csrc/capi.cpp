@@ -149,6 +149,10 @@ struct bcmpc_engine {
     size_t amin_cap = 0;                // records the scratch holds
     unsigned* d_amin_ticket = nullptr;  // fused argmin (split kernel): last-workgroup ticket
     bcmpc_result* h_result = nullptr;   // pinned
+    // the synchronous control steps' result: pinned, mapped, coherent host memory the argmin kernel
+    // writes directly (no device-to-host copy; the stream synchronisation orders it)
+    bcmpc_result* h_result_map = nullptr;
+    bcmpc_result* d_result_map = nullptr;
     double h_consts[kConstRows * kConstCols]{};
     uint64_t version = 0;
     bool has_weights = false;
@@ -362,7 +366,9 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         hipMalloc(&e->d_amin_i, e->amin_cap * sizeof(int64_t)) != hipSuccess ||
         hipMalloc(&e->d_amin_ticket, sizeof(unsigned)) != hipSuccess ||
         hipMemset(e->d_amin_ticket, 0, sizeof(unsigned)) != hipSuccess ||
-        hipHostMalloc(&e->h_result, sizeof(bcmpc_result), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&e->h_result, sizeof(bcmpc_result), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&e->h_result_map, sizeof(bcmpc_result), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&e->d_result_map, e->h_result_map, 0) != hipSuccess) {
         g_last_error = "device allocation failed";
         return cleanup(BCMPC_ERR_HIP);
     }
@@ -412,6 +418,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
                     (void*)e->d_mt_polys, (void*)e->d_mt_chunks, (void*)e->d_mt_part})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
+    if (e->h_result_map) (void)hipHostFree(e->h_result_map);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
     for (auto& ev : e->ev)
@@ -673,7 +680,8 @@ struct CemLaunch {           // one CEM iteration's sampling distribution + resu
 static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, const double* d_actions,
                         uint64_t seed, int64_t cand_offset, double* d_costs, double* d_traj,
                         bcmpc_result* d_result, hipStream_t st, const CemLaunch* cem = nullptr,
-                        bool record_events = true, double* act_out_all = nullptr) {
+                        bool record_events = true, double* act_out_all = nullptr,
+                        const double* state_inline = nullptr) {
     const bcmpc_config& c = e->cfg;
     if (!e->has_weights) return fail(BCMPC_ERR_STATE, "bcmpc_set_weights has not been called");
     if (c.num_paths == 0) return fail(BCMPC_ERR_EMPTY, "attempt to get argmin of an empty sequence");
@@ -702,6 +710,10 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     }
     a.consts = e->d_consts;
     a.state = d_state; a.state_stride = stride;
+    if (state_inline) {                       // the tiled state by value in the kernel arguments
+        a.state_inline = 1;
+        for (int i = 0; i < c.state_dim; ++i) a.state_v[i] = state_inline[i];
+    }
     a.actions = d_actions; a.costs = d_costs; a.traj = d_traj;
     a.seed = seed; a.cand_offset = cand_offset; a.K = c.num_paths;
     a.H = c.horizon; a.S = c.state_dim; a.A = c.action_dim; a.L = c.n_layers;
@@ -875,7 +887,11 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
     const bcmpc_config& c = e->cfg;
     if (c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "get_action needs a fused objective (cheetah cost or learned reward)");
     HIP_TRY(hipSetDevice(c.device));
-    HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
+    // one launch chain per control step: the state travels in the kernel arguments and the argmin
+    // writes the result record straight into mapped host memory (a communicator all-gathers the
+    // device record instead)
+    const bool lean = e->comm == nullptr;
+    if (!lean) HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
     const double* d_act = nullptr;
     if (actions) {
         const size_t n = (size_t)c.horizon * (size_t)c.num_paths * (size_t)c.action_dim;
@@ -889,13 +905,15 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
         HIP_TRY(hipMemcpyAsync(e->d_actions, actions, n * sizeof(double), hipMemcpyHostToDevice, e->stream));
         d_act = e->d_actions;
     }
-    int rc = rollout_impl(e, e->d_state, 0, d_act, seed, cand_offset, e->d_costs, nullptr, e->d_result, e->stream);
+    int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, d_act, seed, cand_offset, e->d_costs, nullptr,
+                          lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
+                          lean ? state : nullptr);
     if (rc != BCMPC_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream));
+    if (!lean) HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream));
     if (costs_out)
         HIP_TRY(hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    *out = *e->h_result;
+    *out = lean ? *e->h_result_map : *e->h_result;
     return BCMPC_OK;
 }
 
@@ -1044,12 +1062,15 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     if (mt_device_path()) {
         // the draw on the device: state + (key, pos) up, draw, rollout, argmin, result + final state down,
         // one synchronisation.  NumPy's state is handed back only when the whole call succeeded.
-        HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
+        const bool lean = e->comm == nullptr;         // (as bcmpc_get_action)
+        if (!lean)
+            HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
         int rc = mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
         if (rc == BCMPC_OK)
-            rc = rollout_impl(e, e->d_state, 0, e->d_actions, seed, cand_offset, e->d_costs, nullptr, e->d_result,
-                              e->stream);
-        if (rc == BCMPC_OK &&
+            rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_actions, seed, cand_offset, e->d_costs, nullptr,
+                              lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
+                              lean ? state : nullptr);
+        if (rc == BCMPC_OK && !lean &&
             hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             rc = fail(BCMPC_ERR_HIP, "result copy failed");
         if (rc == BCMPC_OK && costs_out &&
@@ -1060,7 +1081,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
         std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
         *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];
-        *out = *e->h_result;
+        *out = lean ? *e->h_result_map : *e->h_result;
         return BCMPC_OK;
     }
     const int64_t K = c.num_paths;
@@ -1075,7 +1096,6 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     }
     if (n > e->stage_cap) {                       // pinned staging: the generator writes, the DMA reads
         if (e->h_stage) (void)hipHostFree(e->h_stage);
-    if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
         e->h_stage = nullptr;
         e->stage_cap = 0;
         HIP_TRY(hipHostMalloc(&e->h_stage, n * sizeof(double), hipHostMallocDefault));

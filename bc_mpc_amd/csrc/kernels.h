@@ -46,6 +46,8 @@ struct RolloutArgs {
     const double* consts;
     const double* state;
     int64_t state_stride;                    // 0 (tiled, controllers.py:63) or S (per-candidate)
+    int32_t state_inline;                    // 1: the (tiled) state is state_v, carried in the kernel
+    double state_v[BCMPC_MAX_STATE];         //    arguments (no host-to-device copy per control step)
     const double* actions;                   // [H][K][A] or nullptr => Philox
     double* costs;                           // [K] or nullptr
     double* traj;                            // [H+1][K][S] or nullptr

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void rollout_fp32(const RolloutArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int d = 16 * v + 4 * q + r;
-            s[v][r] = (valid && d < S) ? a.state[cand * a.state_stride + d] : 0.0;
+            s[v][r] = (valid && d < S) ? (a.state_inline ? a.state_v[d] : a.state[cand * a.state_stride + d]) : 0.0;
         }
     if (a.traj && valid) {
 #pragma unroll
@@ -363,6 +363,20 @@ __global__ __launch_bounds__(256) void argmin_final(const ArgminArgs a) {
     if (threadIdx.x == 0) argmin_write(a, best);
 }
 
+// argmin_partial + argmin_final in one block (nparts == 1)
+__global__ __launch_bounds__(256) void argmin_single(const ArgminArgs a) {
+    __shared__ double sc[4];
+    __shared__ int64_t si[4];
+    Best best{__builtin_inf(), INT64_MAX};
+    for (int64_t i = threadIdx.x; i < a.K; i += blockDim.x) {
+        const double v = a.costs[i];
+        const Best c{a.maximize ? -v : v, i};
+        if (better(c, best)) best = c;
+    }
+    best = block_best(best, sc, si);
+    if (threadIdx.x == 0) argmin_write(a, best);
+}
+
 // ------------------------------------------------------------ launchers ----
 static size_t slab_bytes(int HP) { return (size_t)(HP / 16 + 4) * 64 * sizeof(f4); }
 
@@ -409,6 +423,10 @@ hipError_t launch_rollout(const RolloutArgs& a, int hidden_padded, int waves_per
 
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st) {
     if (a.nparts < 1 || a.nparts > kArgminParts) return hipErrorInvalidValue;
+    if (a.nparts == 1) {                           // small K: one block scans and writes (one launch)
+        hipLaunchKernelGGL(argmin_single, dim3(1), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(argmin_partial, dim3(a.nparts), dim3(256), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -417,6 +435,7 @@ hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st) {
 }
 
 int argmin_parts(int64_t K) {
+    if (K <= 4096) return 1;                       // one block: a launch saved beats the wider scan
     const int64_t p = (K + 511) / 512;             // >= 512 costs per block
     return (int)(p < 1 ? 1 : (p > kArgminParts ? kArgminParts : p));
 }

@@ -402,7 +402,7 @@ void rollout_grp(const RolloutArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int d = 16 * v + 4 * q + r;
-            s[v][r] = (valid && d < S) ? a.state[cand * a.state_stride + d] : 0.0;
+            s[v][r] = (valid && d < S) ? (a.state_inline ? a.state_v[d] : a.state[cand * a.state_stride + d]) : 0.0;
         }
     const bool writer = (w == 0) && valid;
     if (a.traj && writer) {

@@ -473,6 +473,9 @@ __device__ __forceinline__ void epi_colx(f4 (&acc)[TW][NC], const float (&f)[NC]
         }
 }
 
+#ifndef X3_NW256                // waves per workgroup at hidden 256 (4, or 8: one tile pair per wave)
+#define X3_NW256 4
+#endif
 #ifndef X3_NW512                // waves per workgroup at hidden 512 (8: one 64-candidate group per CU;
 #define X3_NW512 8               // 4: two 32-candidate groups per CU, out of phase)
 #endif
@@ -596,7 +599,7 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int d = 16 * (hv0 + k) + 4 * q + r;
-            s[k][r] = (valid && d < S) ? a.state[cand * a.state_stride + d] : 0.0;
+            s[k][r] = (valid && d < S) ? (a.state_inline ? a.state_v[d] : a.state[cand * a.state_stride + d]) : 0.0;
         }
     if (a.traj && valid) {
 #pragma unroll
@@ -1287,7 +1290,7 @@ int x3_waves(int hidden_padded) {
     switch (hidden_padded) {
         case 64: return 2;
         case 128: return 4;
-        case 256: return 4;
+        case 256: return X3_NW256;
         case 512: return X3_NW512;
         default: return 8;          // 768, 1024
     }
@@ -1327,7 +1330,7 @@ static hipError_t launch_x3_plain_nc(const RolloutArgs& a, int hidden_padded, hi
     switch (hidden_padded) {
         case 64: return launch_x3_t<64, NC, 2>(a, st);
         case 128: return launch_x3_t<128, NC, 4>(a, st);
-        case 256: return launch_x3_t<256, NC, 4>(a, st);
+        case 256: return launch_x3_t<256, NC, X3_NW256>(a, st);
         case 512: return launch_x3_t<512, NC, X3_NW512>(a, st);
         case 768:
             if constexpr (NC <= 2) return launch_x3_t<768, NC, 8>(a, st);
@@ -1357,7 +1360,7 @@ static hipError_t launch_x3_ak(const RolloutArgs& a, int hidden_padded, hipStrea
     switch (hidden_padded) {
         case 64: return launch_x3_t<64, NC, 2, 0, false, AK>(a, st);
         case 128: return launch_x3_t<128, NC, 4, 0, false, AK>(a, st);
-        case 256: return launch_x3_t<256, NC, 4, 0, false, AK>(a, st);
+        case 256: return launch_x3_t<256, NC, X3_NW256, 0, false, AK>(a, st);
         case 512: return launch_x3_t<512, NC, X3_NW512, 0, false, AK>(a, st);
         default: return hipErrorInvalidValue;
     }
@@ -1368,6 +1371,16 @@ static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStrea
 #ifdef X3_ONLY          // variant builds (tools/build_variants.sh): one width, NC = 4 only
     if constexpr (NC == X3_ONLY_NC) {
         if (hidden_padded != X3_ONLY || a.model == BCMPC_MODEL_REWARD) return hipErrorInvalidValue;
+        if constexpr (X3_ONLY <= 512) {   // relu / LayerNorm delta nets (the ppo_defaults net at 256)
+            constexpr int NWO = X3_ONLY == 256 ? X3_NW256 : X3_ONLY == 512 ? X3_NW512 : X3_ONLY == 64 ? 2 : 4;
+            if (a.act == BCMPC_ACT_RELU || a.ln) {
+                if (a.pL > 0) return hipErrorInvalidValue;
+                if (a.act == BCMPC_ACT_RELU)
+                    return a.ln ? launch_x3_t<X3_ONLY, X3_ONLY_NC, NWO, 0, false, 3>(a, st)
+                                : launch_x3_t<X3_ONLY, X3_ONLY_NC, NWO, 0, false, 1>(a, st);
+                return launch_x3_t<X3_ONLY, X3_ONLY_NC, NWO, 0, false, 2>(a, st);
+            }
+        }
         if (a.pL > 0) {                   // the delta net with a fused policy (8-wave groups only)
             if constexpr (X3_NW512 == 8 && X3_ONLY >= 512) return launch_x3_t<X3_ONLY, X3_ONLY_NC, 8, 128>(a, st);
             return hipErrorInvalidValue;
@@ -1391,7 +1404,7 @@ static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStrea
         switch (hidden_padded) {
             case 64: return launch_x3_t<64, NC, 2, 0, true>(a, st);
             case 128: return launch_x3_t<128, NC, 4, 0, true>(a, st);
-            case 256: return launch_x3_t<256, NC, 4, 0, true>(a, st);
+            case 256: return launch_x3_t<256, NC, X3_NW256, 0, true>(a, st);
             case 512: return launch_x3_t<512, NC, X3_NW512, 0, true>(a, st);
             default: return hipErrorInvalidValue;
         }
