@@ -453,7 +453,10 @@ def main():
     prof = os.path.join(REPO, "profiles", "traffic_per_launch.json")
     if os.path.exists(prof):
         try:
-            tr = json.load(open(prof)).get(args.workload + ("" if eng.precision == "fp32" else ":split"))
+            # PMC traffic of this kernel in this action mode (device: Philox actions in-kernel, hbm: read)
+            key = args.workload + ("" if eng.precision == "fp32" else ":split") + \
+                (":device" if args.actions == "device" else "")
+            tr = json.load(open(prof)).get(key)
             if tr:
                 out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
         except Exception:
