@@ -90,6 +90,35 @@ def _dp(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
+_MT_STATE = [None]          # (bit generator, key pointer, pos pointer) of the verified global MT19937
+
+
+def _legacy_mt_state():
+    """NumPy's global legacy RandomState, when it runs MT19937: its bit generator and pointers to the C
+    state behind ``np.random.get_state()`` -- numpy's ``mt19937_state {uint32 key[624]; int pos}`` at
+    ``MT19937.ctypes.state_address`` -- which bcmpc_get_action_mt19937 reads and advances in place
+    (only on success, as with the tuple path).  The layout is verified once against get_state() per
+    generator object; None (the get_state / set_state path) when anything does not match."""
+    bg = getattr(getattr(np.random.mtrand, "_rand", None), "_bit_generator", None)
+    if type(bg) is not np.random.MT19937:
+        return None
+    cached = _MT_STATE[0]
+    if cached is not None and cached[0] is bg:
+        return cached if cached[1] is not None else None
+    try:
+        addr = bg.ctypes.state_address
+        key_p = ctypes.cast(addr, ctypes.POINTER(ctypes.c_uint32))
+        pos_p = ctypes.cast(addr + 624 * 4, ctypes.POINTER(ctypes.c_int32))
+        with bg.lock:
+            st = np.random.get_state()
+            ok = (st[0] == "MT19937" and pos_p[0] == int(st[2])
+                  and np.array_equal(np.ctypeslib.as_array(key_p, shape=(624,)), np.asarray(st[1], np.uint32)))
+    except Exception:
+        ok = False
+    _MT_STATE[0] = (bg, key_p, pos_p) if ok else (bg, None, None)
+    return _MT_STATE[0] if ok else None
+
+
 class RolloutEngine:
     """Owns one bcmpc_engine (one device, one candidate shard of size K)."""
 
@@ -276,6 +305,14 @@ class RolloutEngine:
         return StepResult(int(res.best_index), float(res.best_cost),
                           np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
 
+    def _numpy_bounds(self, low, high):
+        """Per-action f64 bounds with a finite range (np.random.uniform would not raise), else None."""
+        lo = np.asarray(low, dtype=np.float64)
+        hi = np.asarray(high, dtype=np.float64)
+        if lo.shape != (self.action_dim,) or hi.shape != (self.action_dim,) or not np.all(np.isfinite(hi - lo)):
+            return None
+        return np.ascontiguousarray(lo), np.ascontiguousarray(hi)
+
     def numpy_stream_available(self, low, high) -> bool:
         """The global generator is NumPy's legacy MT19937 and the bounds are per-action vectors
         with a finite range (np.random.uniform would not raise)."""
@@ -294,6 +331,26 @@ class RolloutEngine:
         exactly as that one NumPy call advances it -- only when the call succeeds (a failing call
         raises and leaves the stream untouched).  Returns None (nothing drawn) when the global
         generator is not the legacy MT19937 or the bounds are not per-action vectors."""
+        mt = _legacy_mt_state()
+        if mt is not None:
+            # NumPy's own MT19937 state struct, read and advanced in place by the library (under the
+            # generator's lock): no get_state / set_state tuple round trips (~30 us each)
+            bounds = self._numpy_bounds(low, high)
+            if bounds is None:
+                return None
+            s = _f64(state).reshape(-1)
+            if s.shape[0] != self.state_dim:
+                raise ValueError(f"state has {s.shape[0]} dims, expected {self.state_dim}")
+            bg, key_p, pos_p = mt
+            res = _lib.Result()
+            costs = np.empty(self.num_paths, dtype=np.float64) if return_costs else None
+            with bg.lock:
+                _lib.check(self._lib.bcmpc_get_action_mt19937(
+                    self._h, _dp(s), key_p, pos_p, _dp(bounds[0]), _dp(bounds[1]), ctypes.c_int64(k_global),
+                    ctypes.c_int64(cand_offset), ctypes.c_uint64(seed & (2**64 - 1)), ctypes.byref(res),
+                    _dp(costs) if costs is not None else None))
+            return StepResult(int(res.best_index), float(res.best_cost),
+                              np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
         if not self.numpy_stream_available(low, high):
             return None
         st = np.random.get_state()

@@ -205,7 +205,9 @@ int bcmpc_set_action_bounds(bcmpc_engine* eng, const double* low, const double* 
  *   cand_offset : global index of this device's first candidate (multi-GPU shard)
  *   out      : best index (global) / cost / first action
  *   costs_out: optional K doubles, per-candidate trajectory cost (cost_functions.py:59-63),
- *              or discounted reward sum (BCMPC_COST_REWARD, controllers.py:150) */
+ *              or discounted reward sum (BCMPC_COST_REWARD, controllers.py:150)
+ * Without a communicator the state travels in the kernel arguments and the argmin writes the
+ * result into mapped host memory: one rollout + one argmin launch, one stream synchronisation. */
 int bcmpc_get_action(bcmpc_engine* eng, const double* state, const double* actions,
                      uint64_t seed, int64_t cand_offset, bcmpc_result* out, double* costs_out);
 

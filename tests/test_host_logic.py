@@ -167,3 +167,24 @@ def test_stock_samplers_take_the_library_draw(monkeypatch, cls):
     _RecordingEngine.calls = []
     ctrl.get_action(orc.synthetic_state(norm))
     assert _RecordingEngine.calls == ["host_array"]
+
+
+def test_legacy_mt_state_pointers_are_numpys_own_state():
+    """bcmpc_get_action_mt19937 advances NumPy's MT19937 state in place through these pointers
+    (engine._legacy_mt_state): they must address exactly what get_state() / set_state() see."""
+    import ctypes
+    from bc_mpc_amd import engine
+    np.random.seed(99)
+    np.random.random(17)
+    mt = engine._legacy_mt_state()
+    assert mt is not None
+    bg, key_p, pos_p = mt
+    st = np.random.get_state()
+    key = np.ctypeslib.as_array(key_p, shape=(624,))
+    assert np.array_equal(key, st[1]) and pos_p[0] == st[2] == 34      # two words per double
+    # an in-place write is NumPy's next state (what the library does after a successful draw)
+    want = np.random.RandomState(5).get_state()
+    ctypes.memmove(key_p, want[1].ctypes.data, 624 * 4)
+    pos_p[0] = want[2]
+    assert np.array_equal(np.random.random(4), np.random.RandomState(5).random_sample(4))
+    assert engine._legacy_mt_state() is mt                      # cached per generator object
