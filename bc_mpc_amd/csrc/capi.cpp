@@ -113,6 +113,27 @@ float x3_scale(const float* W, size_t n) {
     return std::ldexp(1.0f, std::max(-100, std::min(100, 12 - e)));
 }
 
+// Weight image of the resident-column split kernel (rollout_rr.hip RrGeom): NS = 2 + T slots per
+// step of 2P + 4 1-KiB pieces (P = HP / 32 k-steps, T = HP / 16 tiles, one piece = 512 halves):
+// slot 0 = layer-0 tiles [0, P) (x3 fragment pairs, hi | lo) + output tile 0 hi, lo, tile 1 hi,
+// lo at k-step P-1; slot 1 = layer-0 tiles [P, 2P) + four zero pieces; slot 2 + t = layer-1 tile
+// t (P k-steps, hi | lo) + output tile t & 1 (hi, lo) at k-step t/2 - 1 (zero for t < 2) + two
+// zero pieces.  l0 / l1 / lo are pack_x3_layer outputs with TWp = 1 ([tile][k-step][hi|lo][lane][8]).
+void pack_rr_image(const _Float16* l0, const _Float16* l1, const _Float16* lo, int HP, _Float16* img) {
+    const int P = HP / 32, T = HP / 16, SLOTH = (2 * P + 4) * 512;
+    auto out_frag = [&](int v, int p) { return lo + ((size_t)v * P + p) * 1024; };     // hi | lo, 1024 halves
+    std::memset(img, 0, sizeof(_Float16) * (size_t)(2 + T) * SLOTH);
+    for (int half = 0; half < 2; ++half)
+        std::memcpy(img + (size_t)half * SLOTH, l0 + (size_t)half * P * 1024, sizeof(_Float16) * P * 1024);
+    std::memcpy(img + (size_t)2 * P * 512, out_frag(0, P - 1), sizeof(_Float16) * 1024);
+    std::memcpy(img + (size_t)(2 * P + 2) * 512, out_frag(1, P - 1), sizeof(_Float16) * 1024);
+    for (int t = 0; t < T; ++t) {
+        _Float16* d = img + (size_t)(2 + t) * SLOTH;
+        std::memcpy(d, l1 + (size_t)t * P * 1024, sizeof(_Float16) * P * 1024);
+        if (t >= 2) std::memcpy(d + (size_t)2 * P * 512, out_frag(t & 1, t / 2 - 1), sizeof(_Float16) * 1024);
+    }
+}
+
 }  // namespace
 
 namespace bcmpc {
@@ -231,8 +252,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                                                "delta net without a policy, hidden <= 512 (use FP32)");
         if (reward && c.state_dim < 16)
             return fail(BCMPC_ERR_UNSUPPORTED, "split reward engines need state_dim >= 16 (reward row in tile 1)");
-        if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLIT4))
-            return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4 kernels");
+        if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLITR))
+            return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4/splitr kernels");
     } else if (c.kernel >= BCMPC_KERNEL_SPLIT1) {
         return fail(BCMPC_ERR_ARG, "split kernels need precision SPLIT_F16");
     }
@@ -277,7 +298,28 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->TP = 8;
         e->PL = c.policy_layers;
     }
-    if (split) {
+    // resident-column split kernel (rollout_rr.hip): the 2-layer tanh delta net at hidden <= 512.
+    // Opt-in (kernel = splitr, or BCMPC_SPLITR=1 under auto): measured 2.03 ms at cfg3 against the
+    // slab kernel's 1.90 ms -- LDS-read-bound at one column per wave
+    const bool rr_ok = split && !reward && e->PL == 0 && c.activation == BCMPC_ACT_TANH && !c.layer_norm &&
+                       c.n_layers == 2 && e->HP <= 512 && c.state_dim + c.action_dim <= 32;
+    bool use_rr = c.kernel == BCMPC_KERNEL_SPLITR;
+    if (use_rr && !rr_ok) {
+        delete e;
+        return fail(BCMPC_ERR_UNSUPPORTED, "splitr kernel: 2-layer tanh NNDynamicsModel, hidden <= 512, no "
+                                           "LayerNorm / policy / reward net");
+    }
+    if (c.kernel == BCMPC_KERNEL_AUTO && rr_ok) {
+        const char* ev = std::getenv("BCMPC_SPLITR");
+        use_rr = ev && *ev && ev[0] == '1';
+    }
+    if (use_rr) {
+        e->split = true;
+        e->nc = 4;
+        e->kernel = BCMPC_KERNEL_SPLITR;
+        e->nw = 4;
+        kern = e->kernel;
+    } else if (split) {
         // widest workgroup (most candidates per weight read) that still gives every CU work and fits LDS
         const int64_t cols = (c.num_paths + 15) / 16;
         int nc = c.kernel == BCMPC_KERNEL_SPLIT1 ? 1 : c.kernel == BCMPC_KERNEL_SPLIT2 ? 2
@@ -305,7 +347,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->nw = nwx;
         kern = e->kernel;
     }
-    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_SPLIT4) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
+    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_SPLITR) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
     const int nw = split ? e->nw : kern_waves(kern);
     if (!split && kern != BCMPC_KERNEL_SOLO &&
         (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw, e->PHP, e->PL, c.model) > 160 * 1024)) {
@@ -342,6 +384,12 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->w_off[1] = off; off += (size_t)2 * T * T * 64 * 4;
         e->w_off[2] = off; off += (size_t)2 * 2 * T * 64 * 4;
         e->b_off[0] = 0; e->b_off[1] = e->HP; e->b_off[2] = 3 * e->HP; boff = 3 * e->HP + 32;
+    } else if (kern == BCMPC_KERNEL_SPLITR) {
+        // one slot image (pack_rr_image) streamed by every workgroup; layers 1, 2 are inside it
+        off = rr_image_bytes(e->HP) / sizeof(float);
+        e->w_off[0] = 0; e->w_off[1] = off; e->w_off[2] = off;
+        for (int l = 0; l < L; ++l) { e->b_off[l] = boff; boff += e->HP; }
+        e->b_off[L] = boff; boff += 32;
     } else {
         e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;                   // [S+A -> h]
         for (int l = 1; l < L; ++l) { e->w_off[l] = off; off += (size_t)T * T * 64 * 4; }
@@ -476,6 +524,22 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         hb[e->b_off[3] + S] = w->biases[4][0];
         e->mean_reward = w->mean_reward[0];
         e->std_reward = w->std_reward[0];
+    } else if (e->kernel == BCMPC_KERNEL_SPLITR) {
+        // rollout_rr: per-layer x3 fragment pairs (TWp = 1), then the slot image
+        const int P = T / 2;
+        std::vector<_Float16> l0((size_t)T * 1024), l1((size_t)T * P * 1024), lo((size_t)2 * P * 1024);
+        const float s0 = x3_scale(w->kernels[0], (size_t)(S + A) * h);
+        const float s1 = x3_scale(w->kernels[1], (size_t)h * h);
+        const float so = x3_scale(w->kernels[2], (size_t)h * S);
+        pack_x3_layer(w->kernels[0], S + A, h, 1, T, 1, s0, l0.data());
+        pack_x3_layer(w->kernels[1], h, h, P, T, 1, s1, l1.data());
+        pack_x3_layer(w->kernels[2], h, S, P, 2, 1, so, lo.data());
+        pack_rr_image(l0.data(), l1.data(), lo.data(), HP, reinterpret_cast<_Float16*>(hw.data()));
+        e->winv[0] = 1.0f / s0;                            // (layer 0's input scale is per candidate)
+        e->winv[1] = (1.0f / s1) / 4096.0f;                // hidden inputs are tanh x 2^12
+        e->winv[2] = (1.0f / so) / 4096.0f;
+        for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
+        std::memcpy(hb.data() + e->b_off[L], w->biases[L], sizeof(float) * S);
     } else if (e->split) {
         // same sizes as the f32 layout (4 bytes per weight: two halves)
         _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
@@ -763,14 +827,44 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     // get_action).  Off by default: the tail's ticket + acquire cost ~6 us in-kernel, as much as the
     // two argmin launches it replaces, and p50 did not move (cfg1/cfg2/run.sh recipe)
     const char* fa = std::getenv("BCMPC_FUSED_ARGMIN");
-    const bool fused = e->split && d_result && fa && fa[0] == '1';
+    const bool fused = e->split && e->kernel != BCMPC_KERNEL_SPLITR && d_result && fa && fa[0] == '1';
     if (fused) {
         a.fused_argmin = 1;
         a.amin = m;
         a.amin_ticket = e->d_amin_ticket;
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
-    if (e->split) {
+    if (e->kernel == BCMPC_KERNEL_SPLITR) {
+        // diagnostics: RR_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
+        static uint64_t* d_rst = nullptr;
+        static size_t rst_n = 0;
+        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
+        const int cpb = rr_candidates_per_block(), nwv = cpb / 16;
+        const size_t blocks = (size_t)((c.num_paths + cpb - 1) / cpb);
+        if (stamps) {
+            if (rst_n < blocks * nwv * 10) {
+                if (d_rst) (void)hipFree(d_rst);
+                rst_n = blocks * nwv * 10;
+                HIP_TRY(hipMalloc(&d_rst, rst_n * sizeof(uint64_t)));
+            }
+            HIP_TRY(hipMemsetAsync(d_rst, 0, rst_n * sizeof(uint64_t), st));
+            a.stamps = d_rst;
+        }
+        HIP_TRY(launch_rollout_rr(a, e->HP, st));
+        if (stamps) {
+            std::vector<uint64_t> h(blocks * nwv * 10);
+            HIP_TRY(hipMemcpyAsync(h.data(), d_rst, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            const char* names[6] = {"barrier", "layer0", "layer1", "head/tail", "dma-wait", "dma-issue"};
+            std::fprintf(stderr, "rr stamps (per step, s_memtime ticks):");
+            for (int k = 0; k < 6; ++k) {
+                double sum = 0;
+                for (size_t b = 0; b < blocks * nwv; ++b) sum += (double)h[b * 10 + k];
+                std::fprintf(stderr, " %s=%.0f", names[k], sum / (blocks * nwv) / c.horizon);
+            }
+            std::fprintf(stderr, "\n");
+        }
+    } else if (e->split) {
         // diagnostics: X3_STAMP builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_st = nullptr;
         static size_t st_n = 0;

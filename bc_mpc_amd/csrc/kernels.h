@@ -159,6 +159,9 @@ size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int polic
               int ak = 0);
 bool x3_policy_ok(int hidden_padded, int nc);
 hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
+size_t rr_image_bytes(int hidden_padded);
+int rr_candidates_per_block();
+hipError_t launch_rollout_rr(const RolloutArgs& a, int hidden_padded, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 hipError_t launch_select(const SelectArgs& a, hipStream_t st);
 hipError_t launch_refit(const RefitArgs& a, hipStream_t st);

@@ -162,7 +162,7 @@ class RolloutEngine:
             split_ok = ((plain or (model == "delta" and not policy_hidden and hidden <= 512))
                         and (model == "delta" or state_dim >= 16)
                         and (not policy_hidden or 448 < hidden <= top)
-                        and kernel in ("auto", "split1", "split2", "split4"))
+                        and kernel in ("auto", "split1", "split2", "split4", "splitr"))
             precision = "split" if split_ok else "fp32"
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"unknown precision {precision!r}; one of {sorted(_lib.PRECISIONS)}")

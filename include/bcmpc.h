@@ -78,7 +78,11 @@ typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")  
     BCMPC_KERNEL_GROUP8 = 4,    /* 8 waves share 16 candidates (small K)                 */
     BCMPC_KERNEL_SPLIT1 = 5,    /* BCMPC_PREC_SPLIT_F16: one workgroup = 1 x 16 candidates  */
     BCMPC_KERNEL_SPLIT2 = 6,    /*                                      2 x 16 candidates  */
-    BCMPC_KERNEL_SPLIT4 = 7     /*                                      4 x 16 candidates  */
+    BCMPC_KERNEL_SPLIT4 = 7,    /*                                      4 x 16 candidates  */
+    BCMPC_KERNEL_SPLITR = 8     /* BCMPC_PREC_SPLIT_F16, 2-layer tanh NNDynamicsModel, hidden
+                                   <= 512, no policy: one wave = 16 candidates with its
+                                   layer-1 input in registers, weights streamed through an
+                                   LDS ring, two workgroups per CU (rollout_rr.hip)          */
 } bcmpc_kernel;
 
 typedef enum bcmpc_policy_mode {   /* MPCcontrollerPolicyNet.self_exp (controllers.py:201-208) */

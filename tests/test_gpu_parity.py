@@ -24,12 +24,15 @@ pytestmark = pytest.mark.gpu
 ATOL, RTOL = 1e-4, 1e-5
 
 
-KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4"]
+KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4", "splitr"]
 
 
 def _skip_unsupported(g: Golden, kernel: str):
     if kernel == "group8" and g.meta["hidden"] <= 64:
         pytest.skip("group8 needs >= 8 hidden tiles")
+    if kernel == "splitr" and (g.meta["act"] != "tanh" or g.meta["ln"] or g.weights.n_layers != 2
+                               or g.meta["hidden"] > 512):
+        pytest.skip("splitr: the 2-layer tanh delta net, hidden <= 512")
     if kernel.startswith("split"):
         if (g.meta["act"] != "tanh" or g.meta["ln"]) and g.meta["hidden"] > 512:
             pytest.skip("split precision: relu / LayerNorm nets up to hidden 512")
@@ -202,7 +205,7 @@ def test_non_fused_cost_goes_through_trajectory_mode():
     assert ctrl.last_index == i and np.array_equal(a, want)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "solo", "group8", "split4", "split1"])
+@pytest.mark.parametrize("kernel", ["auto", "solo", "group8", "split4", "split1", "splitr"])
 def test_full_size_cfg3_properties(kernel):
     """K=65536, H=20, 2x500 tanh (BASELINE cfg3 dims) at full size: shard
     invariance (bitwise), argmin consistency, determinism, and a 256-candidate
