@@ -29,7 +29,9 @@ The siblings run on the same engine:
 * ``MPCcontrollerReward`` (controllers.py:90-158) and
   ``MPCcontrollerPolicyNetReward`` (controllers.py:289-363): the two-head
   ``NNDynamicsRewardModel`` net (dynamics.py:121-238) in the kernel, objective =
-  argmax of the (discounted) predicted reward sum.
+  argmax of the (discounted) predicted reward sum;
+* ``MCTScontrollerPolicyNetReward`` (controllers.py:365-457): two engine
+  launches per step (first-stage actions, then the policy-guided follow-up paths).
 """
 from __future__ import annotations
 
@@ -554,3 +556,140 @@ class MPCcontrollerPolicyNetReward(MPCcontrollerPolicyNet):
                                             size=[self.horizon, self.num_simulated_paths,
                                                   len(self.env.action_space.high)])
         return np_action_paths
+
+
+class MCTScontrollerPolicyNetReward(Controller):
+    """Two-stage policy-guided search (controllers.py:365-457) on the engine.
+
+    Stage 1 (controllers.py:403-425): ``num_first_stage_actions`` (N) first actions from the root
+    state -- the policy's stochastic sample (``self_exp=True``, Philox normals as in
+    ``MPCcontrollerPolicyNet``), its mean (``self_exp=False``), or ``env.action_space.sample()``
+    (``random_first_stage_action``) -- each scored by one ``predict`` step of the two-head
+    ``NNDynamicsRewardModel``: one engine launch of N candidates, horizon 1, returning the first
+    actions, the rewards and the next states.  Stage 2 (controllers.py:427-449): every next state
+    tiled ``random_path_per_action`` (R) times and rolled ``horizon`` steps with the DETERMINISTIC
+    policy (the reference's ``stochastic=False``): one launch of N*R candidates with per-candidate
+    initial states and the fused policy at ``explore = 0``, returning the reward sums.  The mean over
+    the R paths, the sum with the first reward and the argmax stay NumPy (:442-451).  Returns the
+    chosen first action with the reference's shape ``[1, A]`` (float32 for the policy's actions).
+    The reference's follow-up paths of one first action are identical (deterministic policy and
+    model), so the engine computes N*R equal rows exactly as the reference does.
+    """
+
+    def __init__(self,
+                 env,
+                 dyn_model,
+                 policy_net,
+                 explore=1.,
+                 self_exp=True,
+                 horizon=5,
+                 cost_fn=None,
+                 num_first_stage_actions=10,
+                 random_path_per_action=10,
+                 random_first_stage_action=False,
+                 *,
+                 seed: Optional[int] = None,
+                 device: Optional[int] = None):
+        self.env = env
+        self.dyn_model = dyn_model
+        self.policy_net = policy_net
+        self.horizon = horizon
+        self.cost_fn = cost_fn
+        self.num_first_stage_actions = num_first_stage_actions
+        self.random_path_per_action = random_path_per_action
+        self.self_exp = self_exp
+        self.explore = explore
+        self.random_first_stage_action = random_first_stage_action
+        self._seed_rng = np.random.RandomState(0x5EEDC0DE if seed is None else seed)
+        self._device = device
+        self._engines = {}
+        self.last_index = None
+        self.last_total_rewards = None
+        self.last_first_actions = None
+        self.last_seeds = None
+
+    # controllers.py:390-395, verbatim: __init__ never sets num_simulated_paths, so (as in the
+    # reference) calling it raises AttributeError; get_action does not use it
+    def sample_random_actions(self):
+        np_action_paths = np.random.uniform(low=self.env.action_space.low, high=self.env.action_space.high,
+                                            size=[self.horizon, self.num_simulated_paths,
+                                                  len(self.env.action_space.high)])
+        return np_action_paths
+
+    def _engine_for(self, stage, spec, pspec, S, A, K, H, mode, dev) -> RolloutEngine:
+        key = (S, A, spec.hidden, spec.layer_norm, pspec.hidden, pspec.n_layers, int(K), int(H), mode, dev)
+        eng, old = self._engines.get(stage, (None, None))
+        if eng is None or old != key:
+            if eng is not None:
+                eng.close()
+            eng = RolloutEngine(S, A, spec.hidden, 2, "tanh", spec.layer_norm, int(H), int(K), device=dev,
+                                cost="reward", model="reward", policy_hidden=pspec.hidden,
+                                policy_layers=pspec.n_layers, policy_mode=mode)
+            eng.set_action_bounds(np.asarray(self.env.action_space.low, dtype=np.float64),
+                                  np.asarray(self.env.action_space.high, dtype=np.float64))
+            self._engines[stage] = (eng, key)
+        return eng
+
+    # controllers.py:397-457
+    def get_action(self, state):
+        import torch
+        S = int(np.prod(self.env.observation_space.shape))
+        A = len(self.env.action_space.high)
+        N, R = int(self.num_first_stage_actions), int(self.random_path_per_action)
+        state = np.asarray(state, dtype=np.float64).reshape(-1)
+        spec, norm, version = _weights.extract(self.dyn_model)
+        _check_model(spec, "reward", type(self).__name__)
+        pspec, pversion = _policy.extract(self.policy_net)
+        dev = _default_device() if self._device is None else self._device
+        tdev = torch.device("cuda", dev)
+        stream = torch.cuda.current_stream(tdev).cuda_stream
+        if N == 0:
+            raise ValueError("attempt to get argmax of an empty sequence")
+        # ---- first stage (controllers.py:403-418) ----
+        action_1s, d_act = None, None
+        if self.random_first_stage_action:
+            action_1s = [np.expand_dims(self.env.action_space.sample(), axis=0) for _ in range(N)]
+            mode, explore = "explore", 1.0                       # (1 - 1) * mean + 1 * U = U exactly
+            d_act = torch.from_numpy(np.concatenate(action_1s).astype(np.float64)[None]).to(tdev)
+        elif self.self_exp:
+            mode, explore = "stochastic", float(self.explore)    # mean + exp(logstd) * N(0, 1)
+        else:
+            mode, explore = "explore", 0.0                       # the mean
+        seed1 = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+        e1 = self._engine_for("first", spec, pspec, S, A, N, 1, mode, dev)
+        e1.set_weights(spec, norm, version)
+        e1.set_policy(pspec, explore, pversion)
+        d_state = torch.from_numpy(state).to(tdev)
+        d_r1 = torch.empty(N, dtype=torch.float64, device=tdev)
+        d_traj = torch.empty((2, N, S), dtype=torch.float64, device=tdev)
+        e1.rollout_async(d_state.data_ptr(), 0, d_act.data_ptr() if d_act is not None else None, seed1, 0,
+                         d_r1.data_ptr(), d_traj.data_ptr(), None, stream)
+        reward_1s = d_r1.cpu().numpy()                           # reward_1[0][0] of each predict (:418)
+        first = e1.first_actions()
+        if action_1s is None:                                    # policy.act's f32 [1, A] rows
+            action_1s = [first[i:i + 1].astype(np.float32) for i in range(N)]
+        # ---- following stages (controllers.py:421-440): next states tiled R times, action-major ----
+        if self.horizon >= 1 and R >= 1:
+            seed2 = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+            e2 = self._engine_for("follow", spec, pspec, S, A, N * R, self.horizon, "explore", dev)
+            e2.set_weights(spec, norm, version)
+            e2.set_policy(pspec, 0.0, pversion)                  # stochastic=False: the mean
+            d_states = torch.repeat_interleave(d_traj[1], R, dim=0).contiguous()
+            d_rsum = torch.empty(N * R, dtype=torch.float64, device=tdev)
+            e2.rollout_async(d_states.data_ptr(), S, None, seed2, 0, d_rsum.data_ptr(), None, None, stream)
+            rewards_all = d_rsum.cpu().numpy().reshape((-1, 1))  # sum over steps of [N*R, 1] (:442-443)
+        else:
+            seed2 = None
+            rewards_all = np.sum(np.asarray([]), axis=0)         # the reference's empty horizon
+        rewards_all = rewards_all.reshape((N, -1))              # (:445)
+        rewards_all_mean = np.mean(rewards_all, axis=1)
+        total_rewards = np.asarray(reward_1s) + rewards_all_mean
+        best_action1_idx = int(np.argmax(total_rewards))
+        self.last_index, self.last_total_rewards = best_action1_idx, total_rewards
+        self.last_first_actions, self.last_seeds = first, (seed1, seed2)
+        return action_1s[best_action1_idx]
+
+    def close(self):
+        for eng, _ in self._engines.values():
+            eng.close()
+        self._engines = {}

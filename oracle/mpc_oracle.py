@@ -22,6 +22,9 @@ It is a NumPy restatement of the reference path, function by function:
 * ``NumpyRewardDynamics``     <- ``dynamics.py:121-238`` (NNDynamicsRewardModel two-head net).
 * ``reward_get_action``       <- ``controllers.py:90-158`` (MPCcontrollerReward, argmax).
 * ``policy_reward_get_action``<- ``controllers.py:289-363`` (MPCcontrollerPolicyNetReward).
+* ``mcts_get_action``         <- ``controllers.py:365-457`` (MCTScontrollerPolicyNetReward), given the
+  first-stage actions (the stochastic policy's TF draws are not restatable; the engine's Philox
+  normals are, ``device_rng_normals``).
 * ``cem_*``                   <- no reference (BASELINE cfg5 CEM): the engine's own CEM semantics
   (DESIGN.md "CEM"), restated exactly; parity there is self-consistency, not reference-pinned.
 
@@ -418,6 +421,31 @@ def policy_reward_get_action(dyn: NumpyRewardDynamics, policy, state, horizon: i
     rewards = np.sum(np.asarray(rewards_all), axis=0).reshape([-1])
     i = int(np.argmax(rewards))
     return action_paths[:, i, :][0].copy(), i, rewards, action_paths
+
+
+def mcts_get_action(dyn: NumpyRewardDynamics, policy, state, horizon: int, action_1s, random_path_per_action: int):
+    """``MCTScontrollerPolicyNetReward.get_action`` (controllers.py:397-457) with the first-stage
+    actions given (``action_1s``: N arrays of shape [1, A], controllers.py:405-414).  Each first
+    action is scored by ``predict`` from the root (:416-418), its next state tiled R times (:421-424),
+    the follow-up paths rolled with the DETERMINISTIC policy (:430-440), reward sums averaged over
+    the R paths and added to the first reward (:442-449).  Returns ``(best, total_rewards,
+    reward_1s, rewards_all [N, R])``."""
+    state_init = np.expand_dims(state, axis=0)
+    reward_1s, states_all_actions = [], []
+    for action_1 in action_1s:
+        state_1, reward_1 = dyn.predict(state_init, action_1)
+        reward_1s.append(reward_1[0][0])
+        states_all_actions.append(np.tile(state_1, [random_path_per_action, 1]))
+    states = np.asarray(states_all_actions).reshape((-1, state.shape[0]))
+    rewards_all = []
+    for i in range(horizon):
+        actions, _ = policy.act(states, stochastic=False)
+        states, reward = dyn.predict(states, actions)
+        rewards_all.append(reward)
+    rewards_all = np.sum(np.asarray(rewards_all), axis=0)
+    rewards_all = rewards_all.reshape((len(action_1s), -1))
+    total_rewards = np.asarray(reward_1s) + np.mean(rewards_all, axis=1)
+    return int(np.argmax(total_rewards)), total_rewards, np.asarray(reward_1s), rewards_all
 
 
 def synthetic_reward_weights(state_dim=20, action_dim=6, hidden=500, layer_norm=False,

@@ -123,3 +123,21 @@ def test_device_rng_normals_restatement_is_standard_normal():
     assert np.array_equal(a[5000:6000], b)
     assert not np.array_equal(a, orc.device_rng_normals(42, 0, 20000, 4, 6))
     assert abs(a.mean()) < 0.01 and abs(a.std() - 1.0) < 0.01
+
+
+def test_mcts_restatement_properties():
+    """oracle.mcts_get_action (controllers.py:397-457): the R follow-up paths of one first action agree
+    (deterministic policy and model; to BLAS rounding, which depends on a row's position in the batch),
+    each total is the first reward plus the mean path sum, and the argmax is np.argmax's."""
+    S, A, H, R = 20, 6, 4, 3
+    norm = orc.synthetic_normalization(S, A, seed=5, reward=True)
+    dyn = orc.NumpyRewardDynamics(orc.synthetic_reward_weights(S, A, 32, False, seed_base=321), norm)
+    pol = orc.NumpyPolicy(orc.synthetic_policy(S, A, 16, 2, seed=9))
+    state = orc.synthetic_state(norm, seed=6)
+    rs = np.random.RandomState(0)
+    a1 = [rs.uniform(-1, 1, (1, A)).astype(np.float32) for _ in range(4)]
+    a1.append(a1[1].copy())
+    best, total, r1, rall = orc.mcts_get_action(dyn, pol, state, H, a1, R)
+    assert rall.shape == (5, R) and np.allclose(rall, rall[:, :1], rtol=1e-6, atol=1e-6)
+    assert np.array_equal(total, r1 + np.mean(rall, axis=1))
+    assert abs(total[4] - total[1]) < 1e-5 and best == int(np.argmax(total))
