@@ -1209,7 +1209,10 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     };
     if (mt_uniform_rows_par(g, low, high, A, (int64_t)H * k_global, k_global, cand_offset, cand_offset + K,
                             e->h_stage, mt_default_threads(), mt_min_words(), copy_chunk, &chunk_rc) > 0) {
-        if (chunk_rc) return fail(BCMPC_ERR_HIP, "hipMemcpyAsync of a drawn action slice failed");
+        if (chunk_rc) {
+            (void)hipStreamSynchronize(e->stream);     // slices already enqueued still read the staging buffer
+            return fail(BCMPC_ERR_HIP, "hipMemcpyAsync of a drawn action slice failed");
+        }
     } else {
         // copies go out in pieces of >= 2 MiB (one per call for small draws: each copy costs ~5-10 us
         // of runtime overhead)
@@ -1218,9 +1221,13 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         for (int h = 0; h < H; ++h) {
             mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_stage + h * row);
             if ((size_t)(h + 1 - h_sent) * row >= kPiece || h + 1 == H) {
-                HIP_TRY(hipMemcpyAsync(e->d_actions + h_sent * row, e->h_stage + h_sent * row,
-                                       (size_t)(h + 1 - h_sent) * row * sizeof(double), hipMemcpyHostToDevice,
-                                       e->stream));
+                const hipError_t ce = hipMemcpyAsync(e->d_actions + h_sent * row, e->h_stage + h_sent * row,
+                                                     (size_t)(h + 1 - h_sent) * row * sizeof(double),
+                                                     hipMemcpyHostToDevice, e->stream);
+                if (ce != hipSuccess) {
+                    (void)hipStreamSynchronize(e->stream);   // (earlier pieces still read the staging buffer)
+                    return fail(BCMPC_ERR_HIP, std::string("hipMemcpyAsync: ") + hipGetErrorString(ce));
+                }
                 h_sent = h + 1;
             }
         }
