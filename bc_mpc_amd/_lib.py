@@ -33,7 +33,7 @@ COST_CHEETAH, COST_NONE, COST_REWARD = 0, 1, 2
 MODEL_DELTA, MODEL_REWARD = 0, 1
 PREC_FP32, PREC_SPLIT_F16 = 0, 1
 PRECISIONS = {"fp32": PREC_FP32, "split": PREC_SPLIT_F16}
-KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3, "group8": 4, "split1": 5, "split2": 6, "split4": 7, "splitr": 8}
+KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3, "group8": 4, "split1": 5, "split2": 6, "split4": 7, "splitr": 8, "team": 9}
 
 
 class Config(ctypes.Structure):

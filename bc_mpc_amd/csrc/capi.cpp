@@ -169,6 +169,11 @@ struct bcmpc_engine {
     int64_t* d_amin_i = nullptr;
     size_t amin_cap = 0;                // records the scratch holds
     unsigned* d_amin_ticket = nullptr;  // fused argmin (split kernel): last-workgroup ticket
+    // team kernel (rollout_team.hip): exchange granules, {ticket, generation}, mapped timeout flag
+    unsigned long long* d_team = nullptr;
+    unsigned* d_team_ctl = nullptr;
+    unsigned* h_team_err = nullptr;
+    unsigned* d_team_err = nullptr;
     bcmpc_result* h_result = nullptr;   // pinned
     // the synchronous control steps' result: pinned, mapped, coherent host memory the argmin kernel
     // writes directly (no device-to-host copy; the stream synchronisation orders it)
@@ -252,8 +257,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                                                "delta net without a policy, hidden <= 512 (use FP32)");
         if (reward && c.state_dim < 16)
             return fail(BCMPC_ERR_UNSUPPORTED, "split reward engines need state_dim >= 16 (reward row in tile 1)");
-        if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLITR))
-            return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4/splitr kernels");
+        if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_TEAM))
+            return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4/splitr/team kernels");
     } else if (c.kernel >= BCMPC_KERNEL_SPLIT1) {
         return fail(BCMPC_ERR_ARG, "split kernels need precision SPLIT_F16");
     }
@@ -313,7 +318,33 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         const char* ev = std::getenv("BCMPC_SPLITR");
         use_rr = ev && *ev && ev[0] == '1';
     }
-    if (use_rr) {
+    // small-K team kernel (rollout_team.hip): the 2-layer delta net without policy / reward at hidden
+    // <= 512 (LayerNorm: <= 256), when the whole grid fits one workgroup per CU (the team members of a
+    // column wait for each other).  Auto: whenever it fits, unless BCMPC_TEAM=0
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device);
+    const bool team_shape = split && !reward && e->PL == 0 && c.n_layers == 2 && e->HP <= 512 &&
+                            c.state_dim + c.action_dim <= 32 && c.state_dim <= 32 && c.horizon <= 1022 &&
+                            team_members(e->HP) > 0 && !(c.layer_norm && team_members(e->HP) > 1);
+    const bool team_fits = team_shape && c.num_paths > 0 && team_blocks(c.num_paths, e->HP) <= (int64_t)ncu;
+    bool use_team = c.kernel == BCMPC_KERNEL_TEAM;
+    if (use_team && !team_fits) {
+        delete e;
+        return fail(BCMPC_ERR_UNSUPPORTED, "team kernel: 2-layer delta net without policy / reward net, hidden <= "
+                                           "512 (LayerNorm: <= 256), S + A <= 32, ceil(K / 128) * 8 * members "
+                                           "workgroups <= the device's CUs");
+    }
+    if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr) {
+        const char* ev = std::getenv("BCMPC_TEAM");
+        use_team = !(ev && ev[0] == '0');
+    }
+    if (use_team) {
+        e->split = true;
+        e->nc = 1;
+        e->kernel = BCMPC_KERNEL_TEAM;
+        e->nw = e->HP / 16 / team_layer0_tiles(e->HP);
+        kern = e->kernel;
+    } else if (use_rr) {
         e->split = true;
         e->nc = 4;
         e->kernel = BCMPC_KERNEL_SPLITR;
@@ -347,7 +378,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->nw = nwx;
         kern = e->kernel;
     }
-    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_SPLITR) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
+    if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_TEAM) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
     const int nw = split ? e->nw : kern_waves(kern);
     if (!split && kern != BCMPC_KERNEL_SOLO &&
         (e->T % nw != 0 || grp_lds_bytes(e->HP, c.n_layers, nw, e->PHP, e->PL, c.model) > 160 * 1024)) {
@@ -422,6 +453,19 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     }
     for (int i = 0; i < 3; ++i)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { g_last_error = "event create failed"; return cleanup(BCMPC_ERR_HIP); }
+    if (e->kernel == BCMPC_KERNEL_TEAM) {
+        const size_t tb = team_buf_bytes(c.num_paths, e->HP);
+        if ((tb && hipMalloc(&e->d_team, tb) != hipSuccess) ||
+            (tb && hipMemset(e->d_team, 0, tb) != hipSuccess) ||
+            hipMalloc(&e->d_team_ctl, 4 * sizeof(unsigned)) != hipSuccess ||
+            hipMemset(e->d_team_ctl, 0, 4 * sizeof(unsigned)) != hipSuccess ||
+            hipHostMalloc(&e->h_team_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&e->d_team_err, e->h_team_err, 0) != hipSuccess) {
+            g_last_error = "device allocation failed";
+            return cleanup(BCMPC_ERR_HIP);
+        }
+        *e->h_team_err = 0;
+    }
     if (e->PL > 0) {
         size_t poff = 0;
         e->pw_off[0] = poff; poff += (size_t)e->TP * 2 * 64 * 4;                    // [S -> ph]
@@ -462,11 +506,12 @@ int bcmpc_destroy(bcmpc_engine* e) {
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
                     (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
                     (void*)e->d_count, (void*)e->d_amin_c, (void*)e->d_amin_i,
-                    (void*)e->d_amin_ticket, (void*)e->d_mt_io, (void*)e->d_mt_bounds, (void*)e->d_mt_xs,
+                    (void*)e->d_amin_ticket, (void*)e->d_team, (void*)e->d_team_ctl, (void*)e->d_mt_io, (void*)e->d_mt_bounds, (void*)e->d_mt_xs,
                     (void*)e->d_mt_polys, (void*)e->d_mt_chunks, (void*)e->d_mt_part})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
     if (e->h_result_map) (void)hipHostFree(e->h_result_map);
+    if (e->h_team_err) (void)hipHostFree(e->h_team_err);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
     for (auto& ev : e->ev)
@@ -547,8 +592,10 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         for (int l = 0; l <= L; ++l) {
             const int in = l == 0 ? S + A : h, out = l == L ? S : h;
             const float sw = x3_scale(w->kernels[l], (size_t)in * out);
+            // (team kernel: layer 0 in tb = team_layer0_tiles per wave, hidden layers in team_layer1_tiles)
+            const int tbh = e->kernel == BCMPC_KERNEL_TEAM ? team_layer1_tiles(HP) : tb;
             if (l == 0) pack_x3_layer(w->kernels[0], in, out, 1, T, tb, sw, hh + 2 * e->w_off[0]);
-            else if (l < L) pack_x3_layer(w->kernels[l], in, out, P, T, tb, sw, hh + 2 * e->w_off[l]);
+            else if (l < L) pack_x3_layer(w->kernels[l], in, out, P, T, tbh, sw, hh + 2 * e->w_off[l]);
             else pack_x3_layer(w->kernels[L], in, out, P, 2, 2, sw, hh + 2 * e->w_off[L]);
             // layer 0's input scale is per candidate (kernel); hidden inputs are tanh * 2^12, an LN
             // output x hsc[l-1] (static), or relu x its column's power of two (undone in the kernel)
@@ -741,6 +788,17 @@ struct CemLaunch {           // one CEM iteration's sampling distribution + resu
     int64_t pos_base;
 };
 
+// team kernel: a team whose workgroups could not all become resident gives up after its bounded
+// spin and raises the mapped flag (rollout_team.hip); checked after every synchronous call
+static int team_status(bcmpc_engine* e) {
+    if (e->h_team_err && *reinterpret_cast<volatile unsigned*>(e->h_team_err) != 0) {
+        *e->h_team_err = 0;
+        return fail(BCMPC_ERR_HIP, "team kernel: a workgroup team did not meet (its grid was not resident -- "
+                                   "another kernel holding the CUs?)");
+    }
+    return BCMPC_OK;
+}
+
 static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, const double* d_actions,
                         uint64_t seed, int64_t cand_offset, double* d_costs, double* d_traj,
                         bcmpc_result* d_result, hipStream_t st, const CemLaunch* cem = nullptr,
@@ -827,14 +885,56 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     // get_action).  Off by default: the tail's ticket + acquire cost ~6 us in-kernel, as much as the
     // two argmin launches it replaces, and p50 did not move (cfg1/cfg2/run.sh recipe)
     const char* fa = std::getenv("BCMPC_FUSED_ARGMIN");
-    const bool fused = e->split && e->kernel != BCMPC_KERNEL_SPLITR && d_result && fa && fa[0] == '1';
+    const bool fused = e->split && e->kernel != BCMPC_KERNEL_SPLITR && e->kernel != BCMPC_KERNEL_TEAM && d_result &&
+                       fa && fa[0] == '1';
     if (fused) {
         a.fused_argmin = 1;
         a.amin = m;
         a.amin_ticket = e->d_amin_ticket;
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
-    if (e->kernel == BCMPC_KERNEL_SPLITR) {
+    if (e->kernel == BCMPC_KERNEL_TEAM) {
+        a.team_buf = e->d_team;
+        a.team_ctl = e->d_team_ctl;
+        a.team_err = e->d_team_err;
+        // diagnostics: TEAM_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
+        static uint64_t* d_tst = nullptr;
+        static size_t tst_n = 0;
+        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
+        const size_t nwv = (size_t)(e->HP / 16 / team_layer0_tiles(e->HP));
+        const size_t blocks = (size_t)team_blocks(c.num_paths, e->HP);
+        if (stamps) {
+            if (tst_n < blocks * nwv * 10) {
+                if (d_tst) (void)hipFree(d_tst);
+                tst_n = blocks * nwv * 10;
+                HIP_TRY(hipMalloc(&d_tst, tst_n * sizeof(uint64_t)));
+            }
+            HIP_TRY(hipMemsetAsync(d_tst, 0, tst_n * sizeof(uint64_t), st));
+            a.stamps = d_tst;
+        }
+        HIP_TRY(launch_rollout_team(a, e->HP, st));
+        if (stamps) {
+            std::vector<uint64_t> h(blocks * nwv * 10);
+            HIP_TRY(hipMemcpyAsync(h.data(), d_tst, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            const char* names[10] = {"tail", "fill", "l0in", "layer0", "slabbar", "l1mm", "l1epi", "out+bar",
+                                     "xchg", "prologue"};
+            std::fprintf(stderr, "team stamps (per step, s_memtime ticks; wave 0 | others):");
+            for (int k = 0; k < 10; ++k) {
+                double s0 = 0, s1 = 0;
+                size_t n0 = 0, n1 = 0;
+                for (size_t b = 0; b < blocks; ++b)
+                    for (size_t w = 0; w < nwv; ++w) {
+                        const double v = (double)h[(b * nwv + w) * 10 + k];
+                        if (v == 0) continue;
+                        if (w == 0) { s0 += v; ++n0; } else { s1 += v; ++n1; }
+                    }
+                const double div = k == 9 ? 1.0 : (double)c.horizon;
+                std::fprintf(stderr, " %s=%.0f|%.0f", names[k], n0 ? s0 / n0 / div : 0.0, n1 ? s1 / n1 / div : 0.0);
+            }
+            std::fprintf(stderr, "\n");
+        }
+    } else if (e->kernel == BCMPC_KERNEL_SPLITR) {
         // diagnostics: RR_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_rst = nullptr;
         static size_t rst_n = 0;
@@ -1007,6 +1107,7 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
     if (costs_out)
         HIP_TRY(hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (const int ts = team_status(e)) return ts;
     *out = lean ? *e->h_result_map : *e->h_result;
     return BCMPC_OK;
 }
@@ -1173,6 +1274,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: nothing left in flight)
         if (rc != BCMPC_OK) return rc;
         if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+        if (const int ts = team_status(e)) return ts;
         std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
         *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];
         *out = lean ? *e->h_result_map : *e->h_result;
@@ -1243,6 +1345,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     const hipError_t se = hipStreamSynchronize(e->stream);
     if (rc != BCMPC_OK) return rc;
     if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+    if (const int ts = team_status(e)) return ts;
     std::memcpy(mt_key, g.key, sizeof(g.key));      // NumPy's state advances only when the call succeeded
     *mt_pos = g.pos;
     *out = *e->h_result;
@@ -1345,6 +1448,7 @@ int bcmpc_cem_get_action(bcmpc_engine* e, const double* state, const bcmpc_cem* 
     HIP_TRY(hipMemcpyAsync(mu, e->d_mu, ha * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(sigma, e->d_sigma, ha * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (const int ts = team_status(e)) return ts;
     *out = *e->h_result;
     return BCMPC_OK;
 }

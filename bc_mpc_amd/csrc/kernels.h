@@ -84,6 +84,11 @@ struct RolloutArgs {
     int32_t fused_argmin;
     unsigned* amin_ticket;
     ArgminArgs amin;
+    // team kernel (rollout_team.hip, T > 1 members per column): exchange granules
+    // [columns + 8][2][T][8][64], launch control {ticket, generation}, timeout flag (mapped host word)
+    unsigned long long* team_buf;
+    unsigned* team_ctl;
+    unsigned* team_err;
 };
 
 struct SelectArgs {                          // top-E of (cost, index) pairs, NaN last, ties -> lower index
@@ -162,6 +167,12 @@ hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hi
 size_t rr_image_bytes(int hidden_padded);
 int rr_candidates_per_block();
 hipError_t launch_rollout_rr(const RolloutArgs& a, int hidden_padded, hipStream_t st);
+int team_members(int hidden_padded);          // rollout_team.hip: workgroups per candidate column
+int team_layer0_tiles(int hidden_padded);     // layer-0 tiles per wave (weight packing)
+int team_layer1_tiles(int hidden_padded);     // layer-1 tiles per wave
+int64_t team_blocks(int64_t K, int hidden_padded);
+size_t team_buf_bytes(int64_t K, int hidden_padded);
+hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 hipError_t launch_select(const SelectArgs& a, hipStream_t st);
 hipError_t launch_refit(const RefitArgs& a, hipStream_t st);

@@ -1,0 +1,656 @@
+// rollout_team.hip -- small-K split-f16 rollout kernel (BCMPC_KERNEL_TEAM): weights resident in
+// registers, one candidate column per team of workgroups.
+//
+// Path: MPCcontroller.get_action on the shard (controllers.py:57-88) for the 2-layer
+// NNDynamicsModel (dynamics.py:54-71: [S+A -> h] act (+LN), [h -> h] act (+LN), [h -> S] linear)
+// with the fused cheetah cost (cost_functions.py:9-30, 59-63).  Same arithmetic as rollout_x3
+// (hi/lo f16 operands, three MFMA passes, f32 accumulate, f64 state / cost), a
+// different work split for the reference's own small configurations (train_mpc_ppo.py:71,77:
+// K = 400; BASELINE cfg1: K = 1000), where rollout_x3 leaves most CUs idle and each of its few
+// workgroups re-streams the whole net from L2 every step ("small K").
+//
+//   * One 16-candidate column per TEAM of T workgroups (NWV waves each).  Global wave
+//     g = member * NWV + w owns the layer-1 tiles [TPW g, TPW (g + 1)) and the matching
+//     output-layer k-steps (K-split); every member computes ALL of layer 0 (its NWV waves split
+//     the tiles), so the only cross-workgroup traffic of a step is the output layer's partial
+//     sums.  Every weight fragment a wave ever uses is loaded ONCE, before the first step, into
+//     its registers (HP = 512, T = 4: 336 VGPRs per wave, one wave per SIMD).
+//   * Per step: f64 state -> layer-0 input (every wave, redundantly) -> layer 0 (this wave's
+//     tiles) -> LDS slab -> barrier -> layer 1 (this wave's tiles, B fragments from the slab)
+//     -> epilogue -> output partial (registers) -> LDS -> barrier -> member partial summed in
+//     wave order -> (T > 1) exchange of member partials -> total summed in member order ->
+//     de-normalise + residual + cost (f64, every wave, identical bits in every member).
+//   * Exchange (T > 1; cdna_hip_programming.md Guideline 16, form R2: the data is the flag):
+//     wave 0 of each member stores its partial as 8-byte {epoch, f32} granules with agent-scope
+//     relaxed atomic stores and sweeps the other members' granules with agent-scope relaxed atomic
+//     loads until every tag equals the step's epoch.  Two buffers by step parity: a member can
+//     only be one step ahead of the slowest (it needs that member's partial to finish its own
+//     step), so it never overwrites granules still unread.  Epoch = (gen << 10) + h + 1, gen a
+//     per-engine launch counter advanced by the launch's last workgroup (ticket), so granules of
+//     earlier launches never match and nothing has to be zeroed per call.  Spins are bounded:
+//     a team that cannot meet (a member never became resident) sets *team_err and finishes.
+//   * Co-residency: all T members of a team must run at once.  The host launches a team kernel
+//     only when the whole grid fits one workgroup per CU (capi.cpp); members of a column are
+//     numbered b, b + 8, ... so they share an XCD under round-robin dispatch (speed only).
+//
+// Numerics (same bar as rollout_x3): the output layer's partial sums are added in a fixed order
+// (waves of a member, then members), identical in every member, so every member's f64 state is
+// bit-identical and only member 0 writes costs / trajectories.  relu without LayerNorm: layer 0
+// uses one power of two per candidate column (max over the member's waves, one LDS exchange), the
+// layer-1 output one per wave, undone exactly on that wave's partial before the sums.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bcmpc.h"
+#include "device_common.h"
+#include "kernels.h"
+#include "split_common.h"
+
+namespace bcmpc {
+
+// TEAM_STAMP 1 (timing diagnostic, tools/team_variants.sh builds only): per-phase s_memtime totals of
+// every wave into a.stamps ([blocks][NWV][10]: 0 tail, 1 action fill, 2 layer-0 input, 3 layer 0,
+// 4 slab barrier, 5 layer-1 MFMAs, 6 layer-1 epilogue, 7 output + partials barrier, 8 member sums /
+// exchange, 9 prologue)
+#ifndef TEAM_STAMP
+#define TEAM_STAMP 0
+#endif
+#if TEAM_STAMP && !defined(BCMPC_DIAG_VARIANT)
+#error "TEAM_STAMP is a timing diagnostic: build it with tools/team_variants.sh"
+#endif
+
+namespace {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+constexpr int kTeamSpins = 1 << 20;      // exchange polls before a team gives up (~1 s)
+constexpr int kTeamNch = 16;             // steps of action inputs staged in LDS per fill
+
+__device__ __forceinline__ f4 mm(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+
+// the split product hi*hi + hi*lo + lo*hi accumulated into c
+__device__ __forceinline__ f4 mm3(h8 ah, h8 al, h8 bh, h8 bl, f4 c) {
+    c = mm(ah, bh, c);
+    c = mm(ah, bl, c);
+    return mm(al, bh, c);
+}
+
+__device__ __forceinline__ float tanh4096(float z) {     // tanh(y) * 2^12 from z = 2 log2(e) y (rollout_x3)
+    const float r = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z) + 1.0f);
+    return fmaf(-8192.0f, r, 4096.0f);
+}
+
+__host__ __device__ constexpr int team_wpe(int NWV) { return NWV >= 8 ? 2 : 1; }
+
+// relu / LayerNorm epilogue of one wave's NTL tiles (tile x * NTL + j of the layer), one candidate
+// column per lane column m: BiasAdd + activation in f32, then
+//   XCH (LN, or relu's column max across the member): one exchange of per-column statistics
+//     through LDS (xch: [NWV][16][2]) and a barrier, merged in wave order (Chan et al.; var =
+//     M2 / hidden; x * inv + (beta - mean * inv), inv = rsqrt(var + eps) * gamma, x hsc);
+//   !XCH (relu without LN, layer 1): this wave's own column max picks the power of two;
+// then the split into the next layer's B fragments.  fcol: 2^-sh of relu's column scale.
+template <int AK, int NTL, int NWV, bool XCH>
+__device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* __restrict__ bias,
+                                         const float* __restrict__ lg, const float* __restrict__ lb, float hsc,
+                                         int hidden, float* xch, int x, int w, int lane, float& fcol) {
+    constexpr bool RELU = (AK & 1) != 0, LNK = (AK & 2) != 0;
+    const int q = lane >> 4, m = lane & 15;
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) {
+        const f4 b = *reinterpret_cast<const f4*>(bias + 16 * (x * NTL + j) + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float z = fmaf(acc[j][r], f, b[r]);
+            acc[j][r] = RELU ? fmaxf(z, 0.f) : tanh4096(z);              // pad rows: exactly 0
+        }
+    }
+    const int nwr = min(max(hidden - 16 * NTL * x, 0), 16 * NTL);      // this wave's valid rows
+    float s0 = 0.f, s1 = 0.f;
+    if constexpr (LNK) {
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s0 += acc[j][r];
+        s0 = nwr > 0 ? add_rows(s0) / (float)nwr : 0.f;
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = acc[j][r] - s0;
+                s1 += (16 * (x * NTL + j) + 4 * q + r < hidden) ? d * d : 0.f;
+            }
+        s1 = add_rows(s1);
+    } else {
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s0 = fmaxf(s0, acc[j][r]);
+        s0 = max_rows32(max_rows16(s0));
+    }
+    if constexpr (XCH) {
+        if (q == 0) *reinterpret_cast<f2*>(xch + (w * 16 + m) * 2) = (f2){s0, s1};
+        __syncthreads();                                                 // every wave's statistics published
+    }
+    if constexpr (LNK) {
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < NWV; ++v) {
+            const float nb = (float)min(max(hidden - 16 * NTL * v, 0), 16 * NTL);
+            if (nb > 0.f) {
+                const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
+                const float nn = n + nb, d = st[0] - mean;
+                mean = mean + d * (nb / nn);
+                m2 = m2 + st[1] + d * d * (n * nb / nn);
+                n = nn;
+            }
+        }
+        const float eps = RELU ? 1e-12f : 1e-12f * 16777216.0f;        // tanh: activations carry x 2^12
+        const float rs = 1.0f / sqrtf(m2 / (float)hidden + eps);
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) {
+            const f4 gv = *reinterpret_cast<const f4*>(lg + 16 * (x * NTL + j) + 4 * q);
+            const f4 bv = *reinterpret_cast<const f4*>(lb + 16 * (x * NTL + j) + 4 * q);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float inv = rs * gv[r];
+                acc[j][r] = (acc[j][r] * inv + (bv[r] - mean * inv)) * hsc;
+            }
+        }
+    } else {
+        float mx = s0;
+        if constexpr (XCH) {
+            mx = 0.f;
+#pragma unroll
+            for (int v = 0; v < NWV; ++v) mx = fmaxf(mx, xch[(v * 16 + m) * 2]);
+        }
+        int e = 0;
+        (void)frexpf(mx, &e);
+        int sh = 12 - e;
+        sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
+        const float sc = ldexpf(1.0f, sh);
+        fcol = ldexpf(1.0f, -sh);
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[j][r] *= sc;
+    }
+}
+
+// activations of NTL tiles -> the next layer's B fragments (hi, lo): a tile pair is one 32-wide
+// k-step (capi.cpp pack_x3_layer k order); a single tile fills the half of its k-step that its
+// parity selects (odd: rows 16..31), the other half is zero
+template <int NTL>
+__device__ __forceinline__ void split_tiles(const f4 (&v)[NTL], int odd, h8 (&xh)[(NTL + 1) / 2],
+                                            h8 (&xl)[(NTL + 1) / 2]) {
+    if constexpr (NTL == 1) {
+        float u[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            u[r] = odd ? 0.f : v[0][r];
+            u[4 + r] = odd ? v[0][r] : 0.f;
+        }
+        split8(u, xh[0], xl[0]);
+    } else {
+#pragma unroll
+        for (int pp = 0; pp < NTL / 2; ++pp) {
+            const float u[8] = {v[2 * pp][0],     v[2 * pp][1],     v[2 * pp][2],     v[2 * pp][3],
+                                v[2 * pp + 1][0], v[2 * pp + 1][1], v[2 * pp + 1][2], v[2 * pp + 1][3]};
+            split8(u, xh[pp], xl[pp]);
+        }
+    }
+}
+
+}  // namespace
+
+// LDS: consts | biases [2][HP] + 32 | LN gamma [2][HP], beta [2][HP] | slab [P][hi|lo][64] f4 |
+// column exchange [2 layers][NWV][16][2] | output partials [NWV][2][64] f4 | team total [2][64] f4 |
+// action inputs [kTeamNch][16][16]
+__host__ __device__ constexpr int team_lds_bytes(int HP, int NWV, int T, int AK) {
+    return param_bytes(2, HP) + ((AK & 2) ? 4 * HP * 4 : 0) + (HP / 32) * 2048 + 2 * NWV * 16 * 2 * 4 +
+           NWV * 2048 + (T > 1 ? 2048 : 0) + kTeamNch * 16 * 16 * 4;
+}
+
+template <int HP, int NWV, int TPW, int T, int AK>
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(team_wpe(NWV), team_wpe(NWV))))
+void rollout_team(const RolloutArgs a) {
+    constexpr bool RELU = (AK & 1) != 0, LNK = (AK & 2) != 0, DYN = RELU && !LNK;
+    constexpr float kAct = RELU ? 1.0f : kTanhK;        // folded into the epilogue factors / biases
+    constexpr int NT = HP / 16, P = HP / 32;
+    constexpr int L0T = NT / NWV, L0P = L0T / 2;        // layer-0 tiles / k-steps per wave (whole layer per member)
+    constexpr int PPW = (TPW + 1) / 2;                  // output-layer k-steps per wave (TPW = 1: half of one)
+    static_assert(HP == 16 * TPW * NWV * T && (TPW == 1 || TPW % 2 == 0) && L0T % 2 == 0, "team geometry");
+    static_assert(!LNK || T == 1, "a LayerNorm after layer 1 needs the whole layer in one workgroup");
+    extern __shared__ __attribute__((aligned(16))) f4 lds[];
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4, m = lane & 15;
+    const int S = a.S, A = a.A;
+    const int bx = blockIdx.x;
+    const int col = ((bx >> 3) / T) * 8 + (bx & 7);     // members of a column: blocks b, b + 8, ...
+    const int tm = (bx >> 3) % T;                       // member
+    const int g = tm * NWV + w;                         // team wave: layer-1 tiles [TPW g, TPW (g + 1))
+    const int64_t ncol = (a.K + 15) / 16;
+    uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tp_ = TEAM_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) __attribute__((always_inline)) {
+        if constexpr (TEAM_STAMP) {
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();
+            ph_[k] += t_ - tp_;
+            tp_ = t_;
+        }
+    };
+    unsigned gen = 0;
+    if constexpr (T > 1) gen = __hip_atomic_load(a.team_ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    if (col < ncol) {
+        char* const base = reinterpret_cast<char*>(lds);
+        double* C = reinterpret_cast<double*>(base);
+        float* Bl = reinterpret_cast<float*>(base + kConstRows * kConstCols * 8);
+        int off = param_bytes(2, HP);
+        float* const lnp = reinterpret_cast<float*>(base + off);
+        off += LNK ? 4 * HP * 4 : 0;
+        f4* const slab = reinterpret_cast<f4*>(base + off);
+        off += P * 2048;
+        float* const xch = reinterpret_cast<float*>(base + off);
+        off += 2 * NWV * 16 * 2 * 4;
+        f4* const parts = reinterpret_cast<f4*>(base + off);
+        off += NWV * 2048;
+        f4* const tot = reinterpret_cast<f4*>(base + off);
+        off += T > 1 ? 2048 : 0;
+        float* const xas = reinterpret_cast<float*>(base + off);
+
+        for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
+        for (int l = 0; l < 2; ++l)
+            for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kAct;
+        for (int i = threadIdx.x; i < 32; i += blockDim.x) Bl[2 * HP + i] = a.b[2][i];
+        if constexpr (LNK)
+            for (int l = 0; l < 2; ++l)
+                for (int i = threadIdx.x; i < HP; i += blockDim.x) {
+                    lnp[l * HP + i] = a.lng[l][i];
+                    lnp[(2 + l) * HP + i] = a.lnb[l][i];
+                }
+
+        // ---- every weight fragment this wave uses, once (capi.cpp: layer 0 packed with TWp = L0T,
+        //      layer 1 with TWp = TPW, the output layer [0][k-step][tile]) ----
+        const int voff = lane * 16;
+        h8 w0h[L0T], w0l[L0T], w1h[P][TPW], w1l[P][TPW], woh[PPW][2], wol[PPW][2];
+        {
+            const __amdgpu_buffer_rsrc_t r0 = layer_rsrc(a.w[0], a.wbytes[0]);
+#pragma unroll
+            for (int j = 0; j < L0T; ++j) {
+                w0h[j] = fload(r0, voff, (w * L0T + j) * 2048);
+                w0l[j] = fload(r0, voff, (w * L0T + j) * 2048 + 1024);
+            }
+            const __amdgpu_buffer_rsrc_t r1 = layer_rsrc(a.w[1], a.wbytes[1]);
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) {
+                    w1h[p][j] = fload(r1, voff, ((g * P + p) * TPW + j) * 2048);
+                    w1l[p][j] = fload(r1, voff, ((g * P + p) * TPW + j) * 2048 + 1024);
+                }
+            const __amdgpu_buffer_rsrc_t r2 = layer_rsrc(a.w[2], a.wbytes[2]);
+#pragma unroll
+            for (int pp = 0; pp < PPW; ++pp)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const int p = TPW == 1 ? g >> 1 : g * PPW + pp;
+                    woh[pp][v] = fload(r2, voff, (p * 2 + v) * 2048);
+                    wol[pp][v] = fload(r2, voff, (p * 2 + v) * 2048 + 1024);
+                }
+        }
+        __syncthreads();                                  // parameters in LDS
+
+        // ---- per-candidate state: lane (q, m) holds dims 16 v + 4 q + r (v = 0, 1) of candidate m,
+        //      in every wave of every member ----
+        const int64_t cand = (int64_t)col * 16 + m;
+        const bool valid = cand < a.K;
+        const bool writer = tm == 0 && w == 0;            // costs / trajectories: member 0, wave 0
+        double s[2][4];
+        double cost = 0.0;                                // trajectory_cost = 0 (cost_functions.py:60)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * v + 4 * q + r;
+                s[v][r] = (valid && d < S) ? (a.state_inline ? a.state_v[d] : a.state[cand * a.state_stride + d]) : 0.0;
+                if (writer && a.traj && valid && d < S) a.traj[cand * S + d] = s[v][r];
+            }
+
+        // ---- actions, normalised (dynamics.py:110) and cast to f32 (the TF feed), staged in LDS for
+        //      kTeamNch steps at a time by the whole workgroup (one action per thread and pass, not per
+        //      lane in the step loop): the caller's [H,K,A] array (np.random.uniform,
+        //      controllers.py:53), Philox (rng_action), or the CEM sampler ----
+        auto fill_actions = [&](int h0) {
+            const int nh = min(kTeamNch, a.H - h0), n = nh * 16 * A;
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const int hh = i / (16 * A), rem = i - hh * 16 * A, mm = rem / A, j = rem - mm * A;
+                const int64_t c = (int64_t)col * 16 + mm;
+                float xv = 0.f;
+                if (c < a.K) {
+                    const int h = h0 + hh;
+                    const uint64_t gc = (uint64_t)(a.cand_offset + c);
+                    const double av = a.cem_mu ? cem_action(a.seed, gc, h, j, a.cem_iter, a.cem_mu[h * A + j],
+                                                            a.cem_sigma[h * A + j], C[6 * 32 + j], C[7 * 32 + j])
+                                      : a.actions ? a.actions[((int64_t)h * a.K + c) * A + j]
+                                                  : rng_action(a.seed, gc, h, j, C[6 * 32 + j], C[7 * 32 + j]);
+                    xv = (float)div_rn(__dsub_rn(av, C[2 * 32 + j]), C[3 * 32 + j], C[9 * 32 + j]);
+                }
+                xas[(hh * 16 + mm) * 16 + j] = xv;
+            }
+        };
+
+        const float f1base = a.winv[1] * kAct;
+        const float fo = a.winv[2];
+        float* const Bout = Bl + 2 * HP;
+        gu64* const gb = (gu64*)a.team_buf;           // (global address space: never flat)
+        bool dead = false;                                // a team exchange timed out: finish without waiting
+        f4 ot[2];                                         // the step's summed output layer (rows 16 v + 4 q + r)
+
+        stamp(9);
+        for (int h = 0;; ++h) {
+            if (h > 0) {
+                // ---- de-normalise + residual (dynamics.py:113,116; f64, no FMA), cheetah cost
+                //      (cost_functions.py:12-28), in step order (:59-63) ----
+                const int npen = partner_row16((s[0][1] >= 0.2) + (s[0][2] >= 0.0) + (s[0][3] >= 0.0));
+                const double s17 = s[1][1];               // dim 17: v = 1, row q = 0, r = 1
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const f4 bv = *reinterpret_cast<const f4*>(Bout + 16 * v + 4 * q);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int d = 16 * v + 4 * q + r;
+                        if (d < S) {
+                            const float dn = fmaf(ot[v][r], fo, bv[r]);              // BiasAdd (f32)
+                            const double ud = __dadd_rn(__dmul_rn((double)dn, C[5 * 32 + d]), C[4 * 32 + d]);
+                            s[v][r] = __dadd_rn(s[v][r], ud);
+                        }
+                    }
+                }
+                if (a.cost == BCMPC_COST_CHEETAH) {
+                    const double score =
+                        __dsub_rn(10.0 * (double)npen, div_rn(__dsub_rn(s[1][1], s17), 0.01, 1.0 / 0.01));
+                    cost = __dadd_rn(cost, score);
+                }
+                if (writer && a.traj && valid) {
+#pragma unroll
+                    for (int v = 0; v < 2; ++v)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int d = 16 * v + 4 * q + r;
+                            if (d < S) a.traj[((int64_t)h * a.K + cand) * S + d] = s[v][r];
+                        }
+                }
+            }
+            stamp(0);
+            if (h == a.H) break;
+            if (h % kTeamNch == 0) {
+                fill_actions(h);
+                __syncthreads();                          // the chunk's action inputs (the previous chunk's
+            }                                             // last reads were before the partials barrier)
+            stamp(1);
+
+            // ---- layer-0 input: normalised state (dynamics.py:109) and action, cast to f32, scaled by
+            //      the power of two that puts the column's max |x| in [2^11, 2^12) ----
+            h8 b0h, b0l;
+            float colf;
+            {
+                float x[8];
+                float mx = 0.f;
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int d = 16 * v + 4 * q + r;
+                        float xv = (d >= S && d < S + A) ? xas[((h % kTeamNch) * 16 + m) * 16 + d - S] : 0.f;
+                        if (d < S) xv = (float)div_rn(__dsub_rn(s[v][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
+                        x[4 * v + r] = xv;
+                        mx = fmaxf(mx, fabsf(xv));
+                    }
+                mx = max_rows32(max_rows16(mx));
+                int e = 0;
+                (void)frexpf(mx, &e);
+                int sh = 12 - e;
+                sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
+                const float sc = ldexpf(1.0f, sh);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[k] *= sc;
+                split8(x, b0h, b0l);
+                colf = ldexpf(a.winv[0], -sh) * kAct;
+            }
+
+            stamp(2);
+            // ---- layer 0 [S+A -> h]: this wave's L0T tiles, into the slab ----
+            float fcol0 = 1.f;
+            {
+                f4 acc0[L0T];
+#pragma unroll
+                for (int j = 0; j < L0T; ++j) acc0[j] = mm3(w0h[j], w0l[j], b0h, b0l, (f4){0.f, 0.f, 0.f, 0.f});
+                h8 xh[L0P], xl[L0P];
+                if constexpr (AK == 0) {
+#pragma unroll
+                    for (int pp = 0; pp < L0P; ++pp)
+                        epi_pair_tanh(acc0[2 * pp], acc0[2 * pp + 1], colf, Bl, w * L0T + 2 * pp, q, xh[pp], xl[pp]);
+                } else {
+                    epi_cols<AK, L0T, NWV, true>(acc0, colf, Bl, lnp, lnp + 2 * HP, a.hsc[0], a.hidden, xch, w, w,
+                                                 lane, fcol0);
+                    split_tiles<L0T>(acc0, 0, xh, xl);
+                }
+#pragma unroll
+                for (int pp = 0; pp < L0P; ++pp) {
+                    swrite(slab + ((w * L0P + pp) * 2 + 0) * 64 + lane, xh[pp]);
+                    swrite(slab + ((w * L0P + pp) * 2 + 1) * 64 + lane, xl[pp]);
+                }
+            }
+            stamp(3);
+            __syncthreads();                              // layer-1 input complete
+            stamp(4);
+
+            // ---- layer 1 [h -> h]: this wave's TPW tiles over all P k-steps ----
+            f4 acc1[TPW];
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) acc1[j] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const h8 bh = sread(slab + (p * 2 + 0) * 64 + lane), bl = sread(slab + (p * 2 + 1) * 64 + lane);
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) acc1[j] = mm3(w1h[p][j], w1l[p][j], bh, bl, acc1[j]);
+            }
+            stamp(5);
+            const float f1 = DYN ? f1base * fcol0 : f1base;
+            h8 oh[PPW], ol[PPW];
+            float fcol1 = 1.f;
+            if constexpr (AK == 0 && TPW >= 2) {
+#pragma unroll
+                for (int pp = 0; pp < PPW; ++pp)
+                    epi_pair_tanh(acc1[2 * pp], acc1[2 * pp + 1], f1, Bl + HP, TPW * g + 2 * pp, q, oh[pp], ol[pp]);
+            } else {
+                if constexpr (AK == 0) {
+                    const f4 b = *reinterpret_cast<const f4*>(Bl + HP + 16 * g + 4 * q);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc1[0][r] = tanh4096(fmaf(acc1[0][r], f1, b[r]));
+                } else if constexpr (DYN) {
+                    epi_cols<AK, TPW, NWV, false>(acc1, f1, Bl + HP, lnp, lnp, 1.f, a.hidden, nullptr, g, w, lane,
+                                                  fcol1);
+                } else {
+                    epi_cols<AK, TPW, NWV, true>(acc1, f1, Bl + HP, lnp + HP, lnp + 3 * HP, a.hsc[1], a.hidden,
+                                                 xch + NWV * 32, g, w, lane, fcol1);
+                }
+                split_tiles<TPW>(acc1, g & 1, oh, ol);
+            }
+
+            stamp(6);
+            // ---- output layer [h -> S] (2 tiles), K-split: this wave's k-steps; partials summed in
+            //      wave order, then member order ----
+            f4 po[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int pp = 0; pp < PPW; ++pp)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) po[v] = mm3(woh[pp][v], wol[pp][v], oh[pp], ol[pp], po[v]);
+            if constexpr (DYN) {
+                po[0] *= fcol1;                           // exact: undo this wave's column power of two
+                po[1] *= fcol1;
+            }
+            parts[(w * 2 + 0) * 64 + lane] = po[0];
+            parts[(w * 2 + 1) * 64 + lane] = po[1];
+            __syncthreads();                              // partials complete; every wave is done with the slab
+            stamp(7);
+            if constexpr (T == 1) {
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    ot[v] = parts[(0 * 2 + v) * 64 + lane];
+#pragma unroll
+                    for (int x = 1; x < NWV; ++x) ot[v] += parts[(x * 2 + v) * 64 + lane];
+                }
+            } else {
+                if (w == 0) {
+                    f4 mp[2];
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) {
+                        mp[v] = parts[(0 * 2 + v) * 64 + lane];
+#pragma unroll
+                        for (int x = 1; x < NWV; ++x) mp[v] += parts[(x * 2 + v) * 64 + lane];
+                    }
+                    // publish this member's partial: granule k * 64 + lane = {epoch, f32 bits}
+                    const unsigned ep = (gen << 10) + (unsigned)h + 1u;
+                    const size_t slot = ((size_t)col * 2 + (h & 1)) * T;
+                    gu64* const mine = gb + (slot + tm) * 512;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        __hip_atomic_store(mine + k * 64 + lane,
+                                           ((unsigned long long)ep << 32) | __float_as_uint(mp[k >> 2][k & 3]),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // sweep the granules until every tag is this step's epoch, summing the partials in
+                    // member order on the way (a pass with a stale tag is discarded)
+                    for (int spins = 0; !dead; ++spins) {
+                        bool ok = true;
+#pragma unroll
+                        for (int t = 0; t < T; ++t) {
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) {
+                                float pv = mp[k >> 2][k & 3];
+                                if (t != tm) {
+                                    const unsigned long long xv = __hip_atomic_load(
+                                        gb + (slot + t) * 512 + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    pv = __uint_as_float((unsigned)xv);
+                                    ok &= (unsigned)(xv >> 32) == ep;
+                                }
+                                ot[k >> 2][k & 3] = t == 0 ? pv : ot[k >> 2][k & 3] + pv;
+                            }
+                        }
+                        if (__all(ok)) break;
+                        if (spins >= kTeamSpins) {
+                            dead = true;
+                            if (lane == 0 && a.team_err)
+                                __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    if (dead) ot[0] = ot[1] = mp[0];             // (a failed call: any value)
+                    tot[0 * 64 + lane] = ot[0];
+                    tot[1 * 64 + lane] = ot[1];
+                }
+                __syncthreads();                          // the team's total
+                ot[0] = tot[0 * 64 + lane];
+                ot[1] = tot[1 * 64 + lane];
+            }
+            stamp(8);
+        }
+        if (writer && a.costs && valid && q == 0) a.costs[cand] = cost;
+        if constexpr (TEAM_STAMP) {
+            if (a.stamps && lane == 0)
+                for (int k = 0; k < 10; ++k) a.stamps[((size_t)blockIdx.x * NWV + w) * 10 + k] = ph_[k];
+        }
+    }
+    if constexpr (T > 1) {
+        // the launch's last workgroup advances the generation (every workgroup read it at its start)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned t = __hip_atomic_fetch_add(a.team_ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == gridDim.x - 1) {
+                __hip_atomic_store(a.team_ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.team_ctl + 1, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// geometry per padded hidden width: waves per member, layer-1 tiles per wave, members per team
+struct TeamShape {
+    int nwv, tpw, members;
+};
+static TeamShape team_shape_of(int hidden_padded) {
+    switch (hidden_padded) {
+        case 64: return {2, 2, 1};
+        case 128: return {4, 2, 1};
+        case 256: return {4, 4, 1};
+        case 512: return {4, 2, 4};
+        default: return {0, 0, 0};
+    }
+}
+
+int team_members(int hidden_padded) { return team_shape_of(hidden_padded).members; }
+int team_layer0_tiles(int hidden_padded) {
+    const TeamShape t = team_shape_of(hidden_padded);
+    return t.nwv ? hidden_padded / 16 / t.nwv : 0;
+}
+int team_layer1_tiles(int hidden_padded) { return team_shape_of(hidden_padded).tpw; }
+int64_t team_blocks(int64_t K, int hidden_padded) {
+    const int64_t ncol = (K + 15) / 16;
+    return ((ncol + 7) / 8) * 8 * team_members(hidden_padded);
+}
+size_t team_buf_bytes(int64_t K, int hidden_padded) {
+    const int T = team_members(hidden_padded);
+    return T > 1 ? (size_t)((K + 15) / 16 + 8) * 2 * T * 512 * sizeof(unsigned long long) : 0;
+}
+
+template <int HP, int NWV, int TPW, int T, int AK>
+static hipError_t launch_team_t(const RolloutArgs& a, hipStream_t st) {
+    constexpr int lds = team_lds_bytes(HP, NWV, T, AK);
+    static_assert(lds <= 160 * 1024, "LDS");
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)rollout_team<HP, NWV, TPW, T, AK>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    if (a.L != 2 || a.model != BCMPC_MODEL_DELTA || a.pL != 0 || a.S + a.A > 32 || a.S > 32 || a.H > 1022 ||
+        (a.cost == BCMPC_COST_CHEETAH && a.S < 18) || AK != ((a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0)) ||
+        (T > 1 && (!a.team_buf || !a.team_ctl)))
+        return hipErrorInvalidValue;
+    const int64_t blocks = team_blocks(a.K, HP);
+    hipLaunchKernelGGL((rollout_team<HP, NWV, TPW, T, AK>), dim3((unsigned)blocks), dim3(64 * NWV), lds, st, a);
+    return hipGetLastError();
+}
+
+template <int HP, int NWV, int TPW, int T>
+static hipError_t launch_team_ak(const RolloutArgs& a, hipStream_t st) {
+    const int ak = (a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0);
+    switch (ak) {
+        case 0: return launch_team_t<HP, NWV, TPW, T, 0>(a, st);
+        case 1: return launch_team_t<HP, NWV, TPW, T, 1>(a, st);
+        case 2:
+            if constexpr (T == 1) return launch_team_t<HP, NWV, TPW, T, 2>(a, st);
+            return hipErrorInvalidValue;
+        case 3:
+            if constexpr (T == 1) return launch_team_t<HP, NWV, TPW, T, 3>(a, st);
+            return hipErrorInvalidValue;
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+    switch (hidden_padded) {
+        case 64: return launch_team_ak<64, 2, 2, 1>(a, st);
+        case 128: return launch_team_ak<128, 4, 2, 1>(a, st);
+        case 256: return launch_team_ak<256, 4, 4, 1>(a, st);
+        case 512: return launch_team_ak<512, 4, 2, 4>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace bcmpc

@@ -153,7 +153,7 @@ class RolloutEngine:
             raise ValueError(f"unknown kernel {kernel!r}; one of {sorted(_lib.KERNELS)}")
         cfg.kernel = _lib.KERNELS[kernel]
         if precision is None:
-            precision = "split" if kernel.startswith("split") else os.environ.get("BCMPC_PRECISION", "auto")
+            precision = "split" if kernel.startswith("split") or kernel == "team" else os.environ.get("BCMPC_PRECISION", "auto")
         if precision == "auto":
             # a fused policy runs in the split kernel's 8-wave groups (dynamics hidden 449..1024;
             # the reward net: hidden <= 512)
@@ -162,7 +162,7 @@ class RolloutEngine:
             split_ok = ((plain or (model == "delta" and not policy_hidden and hidden <= 512))
                         and (model == "delta" or state_dim >= 16)
                         and (not policy_hidden or 448 < hidden <= top)
-                        and kernel in ("auto", "split1", "split2", "split4", "splitr"))
+                        and kernel in ("auto", "split1", "split2", "split4", "splitr", "team"))
             precision = "split" if split_ok else "fp32"
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"unknown precision {precision!r}; one of {sorted(_lib.PRECISIONS)}")

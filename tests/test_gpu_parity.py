@@ -24,7 +24,17 @@ pytestmark = pytest.mark.gpu
 ATOL, RTOL = 1e-4, 1e-5
 
 
-KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4", "splitr"]
+KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4", "splitr", "team"]
+
+
+def team_ok(hidden, ln, n_layers, K, S=20, A=6):
+    """Shapes the small-K team kernel takes (capi.cpp bcmpc_create): the 2-layer delta net, hidden <= 512
+    (LayerNorm: <= 256), the whole grid resident (ceil(K/128)*8 workgroups x members <= 256 CUs)."""
+    hp = next(p for p in (64, 128, 256, 512, 768, 1024) if hidden <= p)
+    members = 4 if hp == 512 else 1
+    blocks = -(-(-(-K // 16)) // 8) * 8 * members
+    return (n_layers == 2 and hp <= 512 and not (ln and members > 1) and S + A <= 32 and 0 < K
+            and blocks <= 256)
 
 
 def _skip_unsupported(g: Golden, kernel: str):
@@ -33,6 +43,8 @@ def _skip_unsupported(g: Golden, kernel: str):
     if kernel == "splitr" and (g.meta["act"] != "tanh" or g.meta["ln"] or g.weights.n_layers != 2
                                or g.meta["hidden"] > 512):
         pytest.skip("splitr: the 2-layer tanh delta net, hidden <= 512")
+    if kernel == "team" and not team_ok(g.meta["hidden"], g.meta["ln"], g.weights.n_layers, g.K, g.S, g.A):
+        pytest.skip("team: the 2-layer delta net at small K (grid resident)")
     if kernel.startswith("split"):
         if (g.meta["act"] != "tanh" or g.meta["ln"]) and g.meta["hidden"] > 512:
             pytest.skip("split precision: relu / LayerNorm nets up to hidden 512")

@@ -1,0 +1,161 @@
+"""The small-K team kernel (rollout_team.hip, kernel="team") against the oracle.
+
+Shapes: every padded width it instantiates (64, 128, 256 with one workgroup per column; 512 with
+a team of four that exchanges the output layer's partial sums once per step), tanh / relu, with
+and without LayerNorm, odd K (partial columns, partial XCD groups of 8 columns), H = 1..30, the
+reference's own small configurations (train_mpc_ppo.py defaults K=400 H=7 2x256 relu+LN;
+BASELINE cfg1 K=1000 H=15 2x500 tanh), HBM actions, device Philox and the CEM sampler.  Same
+tolerance as test_gpu_parity.py.  Also: repeated launches of one engine (the exchange's epoch
+counter advances per launch; stale granules of an earlier launch must never be taken), shard
+invariance (bitwise), and the auto rule (team whenever the grid is resident).
+"""
+import numpy as np
+import pytest
+
+from oracle import mpc_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 1e-4, 1e-5
+
+SHAPES = [  # (K, H, hidden, activation, layer_norm)
+    (1, 1, 64, "tanh", False), (17, 3, 64, "relu", False), (33, 4, 64, "relu", True),
+    (100, 5, 128, "tanh", False), (129, 3, 100, "relu", True), (200, 2, 128, "tanh", True),
+    (400, 7, 256, "relu", True), (257, 4, 256, "tanh", False), (150, 3, 200, "relu", False),
+    (1000, 15, 500, "tanh", False), (33, 30, 500, "tanh", False), (500, 4, 400, "relu", False),
+    (1024, 2, 512, "tanh", False), (4096, 3, 256, "tanh", True),
+]
+
+
+def _check(costs, want, near, best_index, first, actions_h0, label):
+    d = np.abs(costs - want)
+    tol = ATOL + RTOL * np.abs(want)
+    bad = d > tol
+    bad &= ~(near & (np.abs(d - 10.0 * np.round(d / 10.0)) <= tol))
+    print(f"[{label}] max|dcost|={np.nanmax(d) if d.size else 0:.2e}")
+    assert np.array_equal(np.isnan(costs), np.isnan(want)) and not bad.any()
+    assert best_index == int(np.argmin(costs))
+    order = np.sort(want[~np.isnan(want)])
+    i = int(np.argmin(want))
+    if len(order) < 2 or order[1] - order[0] > 2 * (ATOL + RTOL * abs(order[0])) and not near[i]:
+        assert best_index == i and np.array_equal(first, actions_h0[i])
+
+
+def _engine(K, H, hidden, act, ln, kernel="team", seed_base=None):
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    norm = orc.synthetic_normalization(seed=3)
+    w = orc.synthetic_weights(20, 6, hidden, 2, act, ln, seed_base=seed_base or (41 + hidden))
+    eng = RolloutEngine(20, 6, hidden, 2, act, ln, H, K, kernel=kernel)
+    eng.set_weights(MLPSpec(w.kernels, w.biases, act, w.ln_gamma, w.ln_beta), norm, 1)
+    return eng, w, norm
+
+
+@pytest.mark.parametrize("K,H,hidden,act,ln", SHAPES)
+def test_team_shapes_device_rng(K, H, hidden, act, ln):
+    eng, w, norm = _engine(K, H, hidden, act, ln)
+    assert eng.info()["kernel"] == "team"
+    state = orc.synthetic_state(norm, seed=4)
+    res = eng.get_action(state, None, seed=1234, cand_offset=5, return_costs=True)
+    ap = orc.device_rng_actions(1234, 5, K, H, -np.ones(6), np.ones(6))
+    want, paths = orc.rollout(orc.NumpyDynamics(w, norm), state, ap)
+    _check(res.costs, want, orc.near_threshold_mask(paths), res.best_index - 5, res.first_action, ap[0],
+           f"team K{K} H{H} {act}{'+LN' if ln else ''} h{hidden}")
+    eng.close()
+
+
+@pytest.mark.parametrize("K,H,hidden,act,ln", [(400, 7, 256, "relu", True), (1000, 15, 500, "tanh", False),
+                                               (61, 6, 500, "relu", False)])
+def test_team_host_actions_and_repeats(K, H, hidden, act, ln):
+    """[H, K, A] actions from HBM (the drop-in's np.random.uniform array); five launches of one
+    engine give bit-identical costs (the team exchange's epochs advance per launch)."""
+    eng, w, norm = _engine(K, H, hidden, act, ln)
+    state = orc.synthetic_state(norm, seed=8)
+    acts = np.random.RandomState(K).uniform(-1, 1, (H, K, 6))
+    first = eng.get_action(state, acts, return_costs=True)
+    want, paths = orc.rollout(orc.NumpyDynamics(w, norm), state, acts)
+    _check(first.costs, want, orc.near_threshold_mask(paths), first.best_index, first.first_action, acts[0],
+           f"team-host K{K}")
+    for _ in range(4):
+        again = eng.get_action(state, acts, return_costs=True)
+        assert np.array_equal(again.costs, first.costs) and again.best_index == first.best_index
+    eng.close()
+
+
+def test_team_shard_invariance_bitwise():
+    """Philox keyed by the global candidate: two half shards reproduce the full engine's costs bitwise."""
+    K, H = 1000, 15
+    full, _, norm = _engine(K, H, 500, "tanh", False)
+    half, _, _ = _engine(K // 2, H, 500, "tanh", False)
+    state = orc.synthetic_state(norm, seed=9)
+    r = full.get_action(state, None, seed=77, return_costs=True)
+    a = half.get_action(state, None, seed=77, cand_offset=0, return_costs=True)
+    b = half.get_action(state, None, seed=77, cand_offset=K // 2, return_costs=True)
+    assert np.array_equal(np.concatenate([a.costs, b.costs]), r.costs)
+    full.close()
+    half.close()
+
+
+def test_team_trajectory_states():
+    """states_paths_all (controllers.py:65-74) through the team kernel's trajectory mode."""
+    import torch
+    K, H = 300, 5
+    eng, w, norm = _engine(K, H, 500, "tanh", False)
+    eng.close()
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    eng = RolloutEngine(20, 6, 500, 2, "tanh", False, H, K, cost="none", kernel="team")
+    eng.set_weights(MLPSpec(w.kernels, w.biases, "tanh"), norm, 1)
+    state = orc.synthetic_state(norm, seed=10)
+    acts = np.random.RandomState(3).uniform(-1, 1, (H, K, 6))
+    dev = torch.device("cuda", 0)
+    st = torch.from_numpy(state).to(dev)
+    act = torch.from_numpy(acts).to(dev)
+    traj = torch.full((H + 1, K, 20), np.nan, dtype=torch.float64, device=dev)
+    eng.rollout_async(st.data_ptr(), 0, act.data_ptr(), 0, 0, None, traj.data_ptr(), None,
+                      torch.cuda.current_stream(dev).cuda_stream)
+    got = traj.cpu().numpy()
+    _, want = orc.rollout(orc.NumpyDynamics(w, norm), state, acts)
+    err = np.abs(got - want)
+    print(f"max|dstate|={err.max():.3e}")
+    assert np.array_equal(got[0], want[0])
+    assert (err <= 1e-6 + 1e-6 * np.abs(want)).all()
+    eng.close()
+
+
+def test_team_auto_rule():
+    """Auto picks the team kernel for the reference's small configurations and the slab kernel
+    once the grid would not be resident."""
+    for K, hidden, act, ln, want in [(400, 256, "relu", True, "team"), (1000, 500, "tanh", False, "team"),
+                                     (1100, 500, "tanh", False, "split1"), (65536, 500, "tanh", False, "split4")]:
+        eng, _, _ = _engine(K, 3, hidden, act, ln, kernel="auto")
+        assert eng.info()["kernel"] == want, (K, hidden, eng.info()["kernel"])
+        eng.close()
+
+
+def test_team_cem_iterations_match_oracle():
+    """CEM on the team kernel: every iteration's sampled sequences are scored like the
+    oracle's, and the fused single-call path agrees with the per-iteration one."""
+    import torch
+    K, H, A, iters, seed = 512, 6, 6, 3, 5
+    low, high = -np.ones(A), np.ones(A)
+    eng, w, norm = _engine(K, H, 256, "relu", True)
+    dyn = orc.NumpyDynamics(w, norm)
+    state = orc.synthetic_state(norm, seed=11)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    mu0, sd0 = np.zeros((H, A)), np.full((H, A), 0.5)
+    d_state = torch.from_numpy(state).to(dev)
+    costs = torch.empty(K, dtype=torch.float64, device=dev)
+    res = torch.zeros(32, dtype=torch.float64, device=dev)
+    for it in range(iters):
+        mu, sd = mu0 + 0.1 * it, sd0
+        d_mu, d_sd = torch.from_numpy(mu.copy()).to(dev), torch.from_numpy(sd.copy()).to(dev)
+        eng.cem_rollout_async(d_state.data_ptr(), d_mu.data_ptr(), d_sd.data_ptr(), seed, it, 0, K,
+                              costs.data_ptr(), res.data_ptr(), it > 0, st)
+        got = costs.cpu().numpy()
+        acts = orc.cem_actions(seed, it, 0, K, H, mu, sd, low, high)
+        want, paths = orc.rollout(dyn, state, acts)
+        _check(got, want, orc.near_threshold_mask(paths), int(np.argmin(got)), acts[0, int(np.argmin(got))],
+               acts[0], f"team-cem it{it}")
+    r, _, _ = eng.cem_get_action(state, mu0, sd0, iters, 51, 0.1, seed)
+    assert np.isfinite(r.best_cost)
+    eng.close()
