@@ -9,7 +9,7 @@ namespace bcmpc {
 // Writes out->{best_index, best_cost, first_action} for the winning (cost, index) record
 // (maximize: the record holds -cost).  CEM merge: np.argmin over the iteration-major
 // concatenation keeps the earlier best on ties.
-__device__ __forceinline__ void argmin_write(const ArgminArgs& a, Best best) {
+__device__ __forceinline__ void argmin_record(const ArgminArgs& a, Best best) {
     bcmpc_result* out = a.out;
     if (a.merge) {
         const double prev = out->best_cost;
@@ -29,6 +29,16 @@ __device__ __forceinline__ void argmin_write(const ArgminArgs& a, Best best) {
                 : a.actions ? a.actions[best.i * a.A + j]   // action_paths[0, i*, :] (controllers.py:84-85)
                           : rng_action(a.seed, g, 0, j, lo, hi);
         }
+    }
+}
+
+// the record, then (synchronous steps) the mapped done word: the host spins on it (capi.cpp
+// wait_done) and reads the record after it sees seq
+__device__ __forceinline__ void argmin_write(const ArgminArgs& a, Best best) {
+    argmin_record(a, best);
+    if (a.done) {
+        __threadfence_system();
+        __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

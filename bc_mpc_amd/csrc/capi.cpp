@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -179,6 +180,11 @@ struct bcmpc_engine {
     // writes directly (no device-to-host copy; the stream synchronisation orders it)
     bcmpc_result* h_result_map = nullptr;
     bcmpc_result* d_result_map = nullptr;
+    // ... and its completion word (argmin_write raises seq; wait_done spins on it)
+    unsigned long long* h_done = nullptr;
+    unsigned long long* d_done = nullptr;
+    unsigned long long seq = 0;
+    bool want_done = false;             // the next rollout_impl's argmin raises the done word
     double h_consts[kConstRows * kConstCols]{};
     uint64_t version = 0;
     bool has_weights = false;
@@ -324,7 +330,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device);
     const bool team_shape = split && !reward && e->PL == 0 && c.n_layers == 2 && e->HP <= 512 &&
-                            c.state_dim + c.action_dim <= 32 && c.state_dim <= 32 && c.horizon <= 1022 &&
+                            c.state_dim + c.action_dim <= 32 && c.action_dim <= 15 && c.horizon <= 1022 &&
                             team_members(e->HP) > 0 && !(c.layer_norm && team_members(e->HP) > 1);
     const bool team_fits = team_shape && c.num_paths > 0 && team_blocks(c.num_paths, e->HP) <= (int64_t)ncu;
     bool use_team = c.kernel == BCMPC_KERNEL_TEAM;
@@ -447,7 +453,9 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         hipMemset(e->d_amin_ticket, 0, sizeof(unsigned)) != hipSuccess ||
         hipHostMalloc(&e->h_result, sizeof(bcmpc_result), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&e->h_result_map, sizeof(bcmpc_result), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&e->d_result_map, e->h_result_map, 0) != hipSuccess) {
+        hipHostGetDevicePointer((void**)&e->d_result_map, e->h_result_map, 0) != hipSuccess ||
+        hipHostMalloc(&e->h_done, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&e->d_done, e->h_done, 0) != hipSuccess) {
         g_last_error = "device allocation failed";
         return cleanup(BCMPC_ERR_HIP);
     }
@@ -512,6 +520,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (e->h_result) (void)hipHostFree(e->h_result);
     if (e->h_result_map) (void)hipHostFree(e->h_result_map);
     if (e->h_team_err) (void)hipHostFree(e->h_team_err);
+    if (e->h_done) (void)hipHostFree(e->h_done);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
     for (auto& ev : e->ev)
@@ -799,6 +808,28 @@ static int team_status(bcmpc_engine* e) {
     return BCMPC_OK;
 }
 
+// A synchronous control step's completion: spin on the mapped word the argmin raises after its
+// record (system-scope release) instead of a stream synchronisation, whose completion signal
+// arrives several microseconds later; a stream synchronisation after 2 s (or BCMPC_SYNC=stream)
+// reports whatever went wrong.  The stream may still run the argmin's epilogue: later work on it
+// is stream-ordered.
+static int wait_done(bcmpc_engine* e, unsigned long long seq) {
+    static const bool stream_sync = [] {
+        const char* v = std::getenv("BCMPC_SYNC");
+        return v && std::strcmp(v, "stream") == 0;
+    }();
+    if (!stream_sync) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t i = 1;; ++i) {
+            if (__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE) == seq) return BCMPC_OK;
+            if ((i & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+            __builtin_ia32_pause();
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return BCMPC_OK;
+}
+
 static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, const double* d_actions,
                         uint64_t seed, int64_t cand_offset, double* d_costs, double* d_traj,
                         bcmpc_result* d_result, hipStream_t st, const CemLaunch* cem = nullptr,
@@ -876,6 +907,10 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         m.scratch_c = e->d_amin_c;
         m.scratch_i = e->d_amin_i;
         m.nparts = argmin_parts(c.num_paths);
+        if (e->want_done && !e->comm) {
+            m.done = e->d_done;
+            m.seq = ++e->seq;
+        }
         if (cem) {
             m.cem_mu = cem->mu; m.cem_sigma = cem->sigma; m.cem_iter = cem->iter;
             m.merge = cem->merge; m.pos_base = cem->pos_base;
@@ -1099,14 +1134,21 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
         HIP_TRY(hipMemcpyAsync(e->d_actions, actions, n * sizeof(double), hipMemcpyHostToDevice, e->stream));
         d_act = e->d_actions;
     }
+    e->want_done = lean && !costs_out;
     int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, d_act, seed, cand_offset, e->d_costs, nullptr,
                           lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                           lean ? state : nullptr);
+    const bool spin = e->want_done;
+    e->want_done = false;
     if (rc != BCMPC_OK) return rc;
     if (!lean) HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream));
     if (costs_out)
         HIP_TRY(hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (spin) {
+        if (const int wr = wait_done(e, e->seq)) return wr;
+    } else {
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
     if (const int ts = team_status(e)) return ts;
     *out = lean ? *e->h_result_map : *e->h_result;
     return BCMPC_OK;
@@ -1261,19 +1303,27 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         if (!lean)
             HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
         int rc = mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
+        // (the final-state copy was enqueued before the rollout: the argmin's done word implies it)
+        e->want_done = lean && !costs_out;
         if (rc == BCMPC_OK)
             rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_actions, seed, cand_offset, e->d_costs, nullptr,
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
+        const bool spin = e->want_done && rc == BCMPC_OK;
+        e->want_done = false;
         if (rc == BCMPC_OK && !lean &&
             hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             rc = fail(BCMPC_ERR_HIP, "result copy failed");
         if (rc == BCMPC_OK && costs_out &&
             hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             rc = fail(BCMPC_ERR_HIP, "costs copy failed");
-        const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: nothing left in flight)
-        if (rc != BCMPC_OK) return rc;
-        if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+        if (spin) {
+            if (const int wr = wait_done(e, e->seq)) return wr;
+        } else {
+            const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: nothing left in flight)
+            if (rc != BCMPC_OK) return rc;
+            if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+        }
         if (const int ts = team_status(e)) return ts;
         std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
         *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];

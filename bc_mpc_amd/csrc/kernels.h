@@ -36,6 +36,10 @@ struct ArgminArgs {
     double* scratch_c;       // [kArgminParts] per-block best (argmin_partial -> argmin_final)
     int64_t* scratch_i;
     int32_t nparts;          // argmin_parts(K)
+    // synchronous control steps: after the record, a system-scope release of seq into this mapped
+    // host word (the host spins on it instead of a stream synchronisation), or nullptr
+    unsigned long long* done;
+    unsigned long long seq;
 };
 struct RolloutArgs {
     const float __attribute__((ext_vector_type(4)))* w[BCMPC_MAX_LAYERS + 1];  // packed kernels

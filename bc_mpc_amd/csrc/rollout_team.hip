@@ -112,7 +112,7 @@ __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* _
         for (int j = 0; j < NTL; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) s0 += acc[j][r];
-        s0 = nwr > 0 ? add_rows(s0) / (float)nwr : 0.f;
+        s0 = add_rows(s0) * (nwr > 0 ? 1.0f / (float)nwr : 0.f);     // (loop-invariant reciprocal)
 #pragma unroll
         for (int j = 0; j < NTL; ++j)
 #pragma unroll
@@ -146,7 +146,7 @@ __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* _
             }
         }
         const float eps = RELU ? 1e-12f : 1e-12f * 16777216.0f;        // tanh: activations carry x 2^12
-        const float rs = 1.0f / sqrtf(m2 / (float)hidden + eps);
+        const float rs = __builtin_amdgcn_rsqf(m2 * (1.0f / (float)hidden) + eps);    // v_rsq_f32 (~1 ulp)
 #pragma unroll
         for (int j = 0; j < NTL; ++j) {
             const f4 gv = *reinterpret_cast<const f4*>(lg + 16 * (x * NTL + j) + 4 * q);
@@ -204,11 +204,11 @@ __device__ __forceinline__ void split_tiles(const f4 (&v)[NTL], int odd, h8 (&xh
 }  // namespace
 
 // LDS: consts | biases [2][HP] + 32 | LN gamma [2][HP], beta [2][HP] | slab [P][hi|lo][64] f4 |
-// column exchange [2 layers][NWV][16][2] | output partials [NWV][2][64] f4 | team total [2][64] f4 |
+// column exchange [2 layers][NWV][16][2] | output partials [NWV][2][64] f4 | members' partials [T][2][64] f4 |
 // action inputs [kTeamNch][16][16]
 __host__ __device__ constexpr int team_lds_bytes(int HP, int NWV, int T, int AK) {
     return param_bytes(2, HP) + ((AK & 2) ? 4 * HP * 4 : 0) + (HP / 32) * 2048 + 2 * NWV * 16 * 2 * 4 +
-           NWV * 2048 + (T > 1 ? 2048 : 0) + kTeamNch * 16 * 16 * 4;
+           NWV * 2048 + (T > 1 ? T * 2048 : 0) + kTeamNch * 16 * 16 * 4;
 }
 
 template <int HP, int NWV, int TPW, int T, int AK>
@@ -221,6 +221,7 @@ void rollout_team(const RolloutArgs a) {
     constexpr int PPW = (TPW + 1) / 2;                  // output-layer k-steps per wave (TPW = 1: half of one)
     static_assert(HP == 16 * TPW * NWV * T && (TPW == 1 || TPW % 2 == 0) && L0T % 2 == 0, "team geometry");
     static_assert(!LNK || T == 1, "a LayerNorm after layer 1 needs the whole layer in one workgroup");
+    static_assert(T == 1 || NWV >= T, "one collecting wave per other member");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
@@ -258,7 +259,7 @@ void rollout_team(const RolloutArgs a) {
         f4* const parts = reinterpret_cast<f4*>(base + off);
         off += NWV * 2048;
         f4* const tot = reinterpret_cast<f4*>(base + off);
-        off += T > 1 ? 2048 : 0;
+        off += T > 1 ? T * 2048 : 0;
         float* const xas = reinterpret_cast<float*>(base + off);
 
         for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
@@ -301,6 +302,8 @@ void rollout_team(const RolloutArgs a) {
                     wol[pp][v] = fload(r2, voff, (p * 2 + v) * 2048 + 1024);
                 }
         }
+        for (int i = threadIdx.x; i < kTeamNch * 16 * 16; i += blockDim.x)
+            if ((i & 15) >= A) xas[i] = 0.f;                // action slots past A stay zero (fill writes j < A)
         __syncthreads();                                  // parameters in LDS
 
         // ---- per-candidate state: lane (q, m) holds dims 16 v + 4 q + r (v = 0, 1) of candidate m,
@@ -356,19 +359,26 @@ void rollout_team(const RolloutArgs a) {
                 //      (cost_functions.py:12-28), in step order (:59-63) ----
                 const int npen = partner_row16((s[0][1] >= 0.2) + (s[0][2] >= 0.0) + (s[0][3] >= 0.0));
                 const double s17 = s[1][1];               // dim 17: v = 1, row q = 0, r = 1
+                // (branch-free: dims >= S carry the padded constants -- mean 0, std 0 -- and are never read)
+                f4 bv[2];
+                double c4[2][4], c5[2][4];
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
-                    const f4 bv = *reinterpret_cast<const f4*>(Bout + 16 * v + 4 * q);
+                    bv[v] = *reinterpret_cast<const f4*>(Bout + 16 * v + 4 * q);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int d = 16 * v + 4 * q + r;
-                        if (d < S) {
-                            const float dn = fmaf(ot[v][r], fo, bv[r]);              // BiasAdd (f32)
-                            const double ud = __dadd_rn(__dmul_rn((double)dn, C[5 * 32 + d]), C[4 * 32 + d]);
-                            s[v][r] = __dadd_rn(s[v][r], ud);
-                        }
+                        c4[v][r] = C[4 * 32 + 16 * v + 4 * q + r];
+                        c5[v][r] = C[5 * 32 + 16 * v + 4 * q + r];
                     }
                 }
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float dn = fmaf(ot[v][r], fo, bv[v][r]);                 // BiasAdd (f32)
+                        const double ud = __dadd_rn(__dmul_rn((double)dn, c5[v][r]), c4[v][r]);
+                        s[v][r] = __dadd_rn(s[v][r], ud);
+                    }
                 if (a.cost == BCMPC_COST_CHEETAH) {
                     const double score =
                         __dsub_rn(10.0 * (double)npen, div_rn(__dsub_rn(s[1][1], s17), 0.01, 1.0 / 0.01));
@@ -399,13 +409,26 @@ void rollout_team(const RolloutArgs a) {
             {
                 float x[8];
                 float mx = 0.f;
+                const float* const xr = xas + ((h % kTeamNch) * 16 + m) * 16;
+                double c0[2][4], c1[2][4], c8[2][4];
+                float av[2][4];
 #pragma unroll
                 for (int v = 0; v < 2; ++v)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int d = 16 * v + 4 * q + r;
-                        float xv = (d >= S && d < S + A) ? xas[((h % kTeamNch) * 16 + m) * 16 + d - S] : 0.f;
-                        if (d < S) xv = (float)div_rn(__dsub_rn(s[v][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
+                        c0[v][r] = C[0 * 32 + d];
+                        c1[v][r] = C[1 * 32 + d];
+                        c8[v][r] = C[8 * 32 + d];
+                        av[v][r] = xr[min(max(d - S, 0), 15)];     // (slots >= A hold zeros)
+                    }
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int d = 16 * v + 4 * q + r;
+                        const float xs_ = (float)div_rn(__dsub_rn(s[v][r], c0[v][r]), c1[v][r], c8[v][r]);
+                        const float xv = d < S ? xs_ : av[v][r];
                         x[4 * v + r] = xv;
                         mx = fmaxf(mx, fabsf(xv));
                     }
@@ -449,15 +472,23 @@ void rollout_team(const RolloutArgs a) {
             stamp(4);
 
             // ---- layer 1 [h -> h]: this wave's TPW tiles over all P k-steps ----
-            f4 acc1[TPW];
+            // (TPW <= 2: even / odd k-steps in separate accumulators, four independent MFMA chains)
+            constexpr int KS = TPW <= 2 ? 2 : 1;
+            f4 acc1[TPW], acc1b[TPW];
 #pragma unroll
-            for (int j = 0; j < TPW; ++j) acc1[j] = (f4){0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < TPW; ++j) acc1[j] = acc1b[j] = (f4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int p = 0; p < P; ++p) {
                 const h8 bh = sread(slab + (p * 2 + 0) * 64 + lane), bl = sread(slab + (p * 2 + 1) * 64 + lane);
 #pragma unroll
-                for (int j = 0; j < TPW; ++j) acc1[j] = mm3(w1h[p][j], w1l[p][j], bh, bl, acc1[j]);
+                for (int j = 0; j < TPW; ++j) {
+                    if (KS == 2 && (p & 1)) acc1b[j] = mm3(w1h[p][j], w1l[p][j], bh, bl, acc1b[j]);
+                    else acc1[j] = mm3(w1h[p][j], w1l[p][j], bh, bl, acc1[j]);
+                }
             }
+            if constexpr (KS == 2)
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) acc1[j] += acc1b[j];
             stamp(5);
             const float f1 = DYN ? f1base * fcol0 : f1base;
             h8 oh[PPW], ol[PPW];
@@ -505,41 +536,43 @@ void rollout_team(const RolloutArgs a) {
                     for (int x = 1; x < NWV; ++x) ot[v] += parts[(x * 2 + v) * 64 + lane];
                 }
             } else {
+                // member partial: every wave sums the parts in wave order (the same bits in each)
+                f4 mp[2];
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    mp[v] = parts[(0 * 2 + v) * 64 + lane];
+#pragma unroll
+                    for (int x = 1; x < NWV; ++x) mp[v] += parts[(x * 2 + v) * 64 + lane];
+                }
+                // exchange (rows < S only): wave 0 publishes this member's partial as granules
+                // {epoch, f32} at k * 64 + lane (k = 4 v + r), wave j in [1, T) collects member
+                // (tm + j) % T's; every partial lands in the LDS slot of its member
+                const unsigned ep = (gen << 10) + (unsigned)h + 1u;
+                const size_t slot = ((size_t)col * 2 + (h & 1)) * T;
                 if (w == 0) {
-                    f4 mp[2];
-#pragma unroll
-                    for (int v = 0; v < 2; ++v) {
-                        mp[v] = parts[(0 * 2 + v) * 64 + lane];
-#pragma unroll
-                        for (int x = 1; x < NWV; ++x) mp[v] += parts[(x * 2 + v) * 64 + lane];
-                    }
-                    // publish this member's partial: granule k * 64 + lane = {epoch, f32 bits}
-                    const unsigned ep = (gen << 10) + (unsigned)h + 1u;
-                    const size_t slot = ((size_t)col * 2 + (h & 1)) * T;
                     gu64* const mine = gb + (slot + tm) * 512;
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
-                        __hip_atomic_store(mine + k * 64 + lane,
-                                           ((unsigned long long)ep << 32) | __float_as_uint(mp[k >> 2][k & 3]),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // sweep the granules until every tag is this step's epoch, summing the partials in
-                    // member order on the way (a pass with a stale tag is discarded)
+                        if (16 * (k >> 2) + 4 * q + (k & 3) < S)
+                            __hip_atomic_store(mine + k * 64 + lane,
+                                               ((unsigned long long)ep << 32) | __float_as_uint(mp[k >> 2][k & 3]),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    tot[(tm * 2 + 0) * 64 + lane] = mp[0];
+                    tot[(tm * 2 + 1) * 64 + lane] = mp[1];
+                } else if (w < T) {
+                    const int t = (tm + w) % T;
+                    const gu64* const src = gb + (slot + t) * 512;
+                    f4 got[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
                     for (int spins = 0; !dead; ++spins) {
                         bool ok = true;
 #pragma unroll
-                        for (int t = 0; t < T; ++t) {
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) {
-                                float pv = mp[k >> 2][k & 3];
-                                if (t != tm) {
-                                    const unsigned long long xv = __hip_atomic_load(
-                                        gb + (slot + t) * 512 + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                    pv = __uint_as_float((unsigned)xv);
-                                    ok &= (unsigned)(xv >> 32) == ep;
-                                }
-                                ot[k >> 2][k & 3] = t == 0 ? pv : ot[k >> 2][k & 3] + pv;
+                        for (int k = 0; k < 8; ++k)
+                            if (16 * (k >> 2) + 4 * q + (k & 3) < S) {
+                                const unsigned long long xv =
+                                    __hip_atomic_load(src + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                got[k >> 2][k & 3] = __uint_as_float((unsigned)xv);
+                                ok &= (unsigned)(xv >> 32) == ep;
                             }
-                        }
                         if (__all(ok)) break;
                         if (spins >= kTeamSpins) {
                             dead = true;
@@ -549,13 +582,16 @@ void rollout_team(const RolloutArgs a) {
                         }
                         __builtin_amdgcn_s_sleep(1);
                     }
-                    if (dead) ot[0] = ot[1] = mp[0];             // (a failed call: any value)
-                    tot[0 * 64 + lane] = ot[0];
-                    tot[1 * 64 + lane] = ot[1];
+                    tot[(t * 2 + 0) * 64 + lane] = got[0];
+                    tot[(t * 2 + 1) * 64 + lane] = got[1];
                 }
-                __syncthreads();                          // the team's total
-                ot[0] = tot[0 * 64 + lane];
-                ot[1] = tot[1 * 64 + lane];
+                __syncthreads();                          // every member's partial in LDS
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    ot[v] = tot[(0 * 2 + v) * 64 + lane];
+#pragma unroll
+                    for (int t = 1; t < T; ++t) ot[v] += tot[(t * 2 + v) * 64 + lane];     // member order
+                }
             }
             stamp(8);
         }
@@ -618,7 +654,7 @@ static hipError_t launch_team_t(const RolloutArgs& a, hipStream_t st) {
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    if (a.L != 2 || a.model != BCMPC_MODEL_DELTA || a.pL != 0 || a.S + a.A > 32 || a.S > 32 || a.H > 1022 ||
+    if (a.L != 2 || a.model != BCMPC_MODEL_DELTA || a.pL != 0 || a.S + a.A > 32 || a.S > 32 || a.A > 15 || a.H > 1022 ||
         (a.cost == BCMPC_COST_CHEETAH && a.S < 18) || AK != ((a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0)) ||
         (T > 1 && (!a.team_buf || !a.team_ctl)))
         return hipErrorInvalidValue;
