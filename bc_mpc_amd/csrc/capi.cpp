@@ -172,6 +172,7 @@ struct bcmpc_engine {
     unsigned* d_amin_ticket = nullptr;  // fused argmin (split kernel): last-workgroup ticket
     // team kernel (rollout_team.hip): exchange granules, {ticket, generation}, mapped timeout flag
     unsigned long long* d_team = nullptr;
+    int team_kind = 0;                  // 0 plain delta net, 1 + policy, 2 reward net (+ policy)
     unsigned* d_team_ctl = nullptr;
     unsigned* h_team_err = nullptr;
     unsigned* d_team_err = nullptr;
@@ -324,21 +325,25 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         const char* ev = std::getenv("BCMPC_SPLITR");
         use_rr = ev && *ev && ev[0] == '1';
     }
-    // small-K team kernel (rollout_team.hip): the 2-layer delta net without policy / reward at hidden
-    // <= 512 (LayerNorm: <= 256), when the whole grid fits one workgroup per CU (the team members of a
-    // column wait for each other).  Auto: whenever it fits, unless BCMPC_TEAM=0
+    // small-K team kernel (rollout_team.hip): the 2-layer delta net at hidden <= 512 (LayerNorm: <=
+    // 256), or at hidden 512 (tanh) with a fused policy of <= 2 layers and / or the reward net (the
+    // run.sh recipe), when the whole grid fits one workgroup per CU (the team members of a column wait
+    // for each other).  Auto: whenever it fits, unless BCMPC_TEAM=0
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device);
-    const bool team_shape = split && !reward && e->PL == 0 && c.n_layers == 2 && e->HP <= 512 &&
-                            c.state_dim + c.action_dim <= 32 && c.action_dim <= 15 && c.horizon <= 1022 &&
-                            team_members(e->HP) > 0 && !(c.layer_norm && team_members(e->HP) > 1);
-    const bool team_fits = team_shape && c.num_paths > 0 && team_blocks(c.num_paths, e->HP) <= (int64_t)ncu;
+    const int tkind = reward ? 2 : e->PL > 0 ? 1 : 0;
+    const int tmem = team_members(e->HP, tkind);
+    const bool team_shape = split && c.n_layers == 2 && e->HP <= 512 && c.state_dim + c.action_dim <= 32 &&
+                            c.action_dim <= 15 && c.horizon <= 1022 && tmem > 0 && !(c.layer_norm && tmem > 1) &&
+                            (tkind == 0 || (c.activation == BCMPC_ACT_TANH && !c.layer_norm && c.state_dim >= 16 &&
+                                            e->PL <= 2));
+    const bool team_fits = team_shape && c.num_paths > 0 && team_blocks(c.num_paths, e->HP, tkind) <= (int64_t)ncu;
     bool use_team = c.kernel == BCMPC_KERNEL_TEAM;
     if (use_team && !team_fits) {
         delete e;
-        return fail(BCMPC_ERR_UNSUPPORTED, "team kernel: 2-layer delta net without policy / reward net, hidden <= "
-                                           "512 (LayerNorm: <= 256), S + A <= 32, ceil(K / 128) * 8 * members "
-                                           "workgroups <= the device's CUs");
+        return fail(BCMPC_ERR_UNSUPPORTED, "team kernel: 2-layer net, hidden <= 512 (LayerNorm: <= 256; with a "
+                                           "policy or the reward net: 512, tanh, no LayerNorm), S + A <= 32, "
+                                           "ceil(K / 128) * 8 * members workgroups <= the device's CUs");
     }
     if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr) {
         const char* ev = std::getenv("BCMPC_TEAM");
@@ -348,7 +353,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->split = true;
         e->nc = 1;
         e->kernel = BCMPC_KERNEL_TEAM;
-        e->nw = e->HP / 16 / team_layer0_tiles(e->HP);
+        e->nw = e->HP / 16 / team_layer0_tiles(e->HP, tkind);
+        e->team_kind = tkind;
         kern = e->kernel;
     } else if (use_rr) {
         e->split = true;
@@ -462,7 +468,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     for (int i = 0; i < 3; ++i)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { g_last_error = "event create failed"; return cleanup(BCMPC_ERR_HIP); }
     if (e->kernel == BCMPC_KERNEL_TEAM) {
-        const size_t tb = team_buf_bytes(c.num_paths, e->HP);
+        const size_t tb = team_buf_bytes(c.num_paths, e->HP, e->team_kind);
         if ((tb && hipMalloc(&e->d_team, tb) != hipSuccess) ||
             (tb && hipMemset(e->d_team, 0, tb) != hipSuccess) ||
             hipMalloc(&e->d_team_ctl, 4 * sizeof(unsigned)) != hipSuccess ||
@@ -560,8 +566,9 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         pack_x3_layer(w->kernels[0], S + A, h, 1, T, tb, s0, hh + 2 * e->w_off[0]);
         e->winv[0] = 1.0f / s0;
         const float sd = x3_scale(w->kernels[1], (size_t)h * h), sr = x3_scale(w->kernels[3], (size_t)h * h);
-        pack_x3_layer(w->kernels[1], h, h, P, T, tb, sd, hh + 2 * e->w_off[1]);
-        pack_x3_layer(w->kernels[3], h, h, P, T, tb, sr, hh + 2 * e->w_off[3]);
+        const int tbh = e->kernel == BCMPC_KERNEL_TEAM ? team_layer1_tiles(HP, e->team_kind) : tb;   // (team: head tiles per wave)
+        pack_x3_layer(w->kernels[1], h, h, P, T, tbh, sd, hh + 2 * e->w_off[1]);
+        pack_x3_layer(w->kernels[3], h, h, P, T, tbh, sr, hh + 2 * e->w_off[3]);
         e->winv[1] = (1.0f / sd) / 4096.0f;
         e->winv[3] = (1.0f / sr) / 4096.0f;
         // both output kernels feed one accumulator: one scale (the smaller of the two)
@@ -602,7 +609,7 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
             const int in = l == 0 ? S + A : h, out = l == L ? S : h;
             const float sw = x3_scale(w->kernels[l], (size_t)in * out);
             // (team kernel: layer 0 in tb = team_layer0_tiles per wave, hidden layers in team_layer1_tiles)
-            const int tbh = e->kernel == BCMPC_KERNEL_TEAM ? team_layer1_tiles(HP) : tb;
+            const int tbh = e->kernel == BCMPC_KERNEL_TEAM ? team_layer1_tiles(HP, e->team_kind) : tb;
             if (l == 0) pack_x3_layer(w->kernels[0], in, out, 1, T, tb, sw, hh + 2 * e->w_off[0]);
             else if (l < L) pack_x3_layer(w->kernels[l], in, out, P, T, tbh, sw, hh + 2 * e->w_off[l]);
             else pack_x3_layer(w->kernels[L], in, out, P, 2, 2, sw, hh + 2 * e->w_off[L]);
@@ -936,8 +943,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         static uint64_t* d_tst = nullptr;
         static size_t tst_n = 0;
         const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
-        const size_t nwv = (size_t)(e->HP / 16 / team_layer0_tiles(e->HP));
-        const size_t blocks = (size_t)team_blocks(c.num_paths, e->HP);
+        const size_t nwv = (size_t)(e->HP / 16 / team_layer0_tiles(e->HP, e->team_kind));
+        const size_t blocks = (size_t)team_blocks(c.num_paths, e->HP, e->team_kind);
         if (stamps) {
             if (tst_n < blocks * nwv * 10) {
                 if (d_tst) (void)hipFree(d_tst);

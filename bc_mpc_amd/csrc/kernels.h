@@ -171,11 +171,12 @@ hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hi
 size_t rr_image_bytes(int hidden_padded);
 int rr_candidates_per_block();
 hipError_t launch_rollout_rr(const RolloutArgs& a, int hidden_padded, hipStream_t st);
-int team_members(int hidden_padded);          // rollout_team.hip: workgroups per candidate column
-int team_layer0_tiles(int hidden_padded);     // layer-0 tiles per wave (weight packing)
-int team_layer1_tiles(int hidden_padded);     // layer-1 tiles per wave
-int64_t team_blocks(int64_t K, int hidden_padded);
-size_t team_buf_bytes(int64_t K, int hidden_padded);
+// rollout_team.hip; kind: 0 the plain delta net, 1 + fused policy, 2 the reward net (+ policy)
+int team_members(int hidden_padded, int kind);          // workgroups per candidate column (0: unsupported)
+int team_layer0_tiles(int hidden_padded, int kind);     // layer-0 tiles per wave (weight packing)
+int team_layer1_tiles(int hidden_padded, int kind);     // hidden-layer (head) tiles per wave
+int64_t team_blocks(int64_t K, int hidden_padded, int kind);
+size_t team_buf_bytes(int64_t K, int hidden_padded, int kind);
 hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 hipError_t launch_select(const SelectArgs& a, hipStream_t st);

@@ -83,6 +83,12 @@ __device__ __forceinline__ float tanh4096(float z) {     // tanh(y) * 2^12 from 
 
 __host__ __device__ constexpr int team_wpe(int NWV) { return NWV >= 8 ? 2 : 1; }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads (a __syncthreads() fence drains vmcnt too, which would hold every barrier of the
+// first step behind the weight prologue's ~80 loads per wave).  Every hand-off between waves in
+// this kernel goes through LDS; cross-workgroup data travels in atomic granules.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // relu / LayerNorm epilogue of one wave's NTL tiles (tile x * NTL + j of the layer), one candidate
 // column per lane column m: BiasAdd + activation in f32, then
 //   XCH (LN, or relu's column max across the member): one exchange of per-column statistics
@@ -130,7 +136,7 @@ __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* _
     }
     if constexpr (XCH) {
         if (q == 0) *reinterpret_cast<f2*>(xch + (w * 16 + m) * 2) = (f2){s0, s1};
-        __syncthreads();                                                 // every wave's statistics published
+        lds_barrier();                                                      // every wave's statistics published
     }
     if constexpr (LNK) {
         float n = 0.f, mean = 0.f, m2 = 0.f;
@@ -203,15 +209,18 @@ __device__ __forceinline__ void split_tiles(const f4 (&v)[NTL], int odd, h8 (&xh
 
 }  // namespace
 
-// LDS: consts | biases [2][HP] + 32 | LN gamma [2][HP], beta [2][HP] | slab [P][hi|lo][64] f4 |
+// LDS: consts | biases [2 or 3][HP] + 32 | LN gamma [2][HP], beta [2][HP] | slab [P][hi|lo][64] f4 |
 // column exchange [2 layers][NWV][16][2] | output partials [NWV][2][64] f4 | members' partials [T][2][64] f4 |
-// action inputs [kTeamNch][16][16]
-__host__ __device__ constexpr int team_lds_bytes(int HP, int NWV, int T, int AK) {
-    return param_bytes(2, HP) + ((AK & 2) ? 4 * HP * 4 : 0) + (HP / 32) * 2048 + 2 * NWV * 16 * 2 * 4 +
-           NWV * 2048 + (T > 1 ? T * 2048 : 0) + kTeamNch * 16 * 16 * 4;
+// action inputs [kTeamNch][16][16] (no policy) | policy biases + params, policy hidden->hidden weights
+// (PHP > 0; its first and output layers live in registers)
+__host__ __device__ constexpr int team_lds_bytes(int HP, int NWV, int T, int AK, bool RW = false, int PHP = 0,
+                                                 int PL = 0, int pw_bytes = 0) {
+    return param_bytes(RW ? 3 : 2, HP) + ((AK & 2) ? 4 * HP * 4 : 0) + (HP / 32) * 2048 + (AK ? 2 * NWV * 16 * 2 * 4 : 0) +
+           NWV * 2048 + (T > 1 ? T * 2048 : 0) + (PHP > 0 ? pol_param_bytes(PL, PHP) + pw_bytes
+                                                          : kTeamNch * 16 * 16 * 4);
 }
 
-template <int HP, int NWV, int TPW, int T, int AK>
+template <int HP, int NWV, int TPW, int T, int AK, int PHP = 0, bool RW = false>
 __global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(team_wpe(NWV), team_wpe(NWV))))
 void rollout_team(const RolloutArgs a) {
     constexpr bool RELU = (AK & 1) != 0, LNK = (AK & 2) != 0, DYN = RELU && !LNK;
@@ -219,9 +228,18 @@ void rollout_team(const RolloutArgs a) {
     constexpr int NT = HP / 16, P = HP / 32;
     constexpr int L0T = NT / NWV, L0P = L0T / 2;        // layer-0 tiles / k-steps per wave (whole layer per member)
     constexpr int PPW = (TPW + 1) / 2;                  // output-layer k-steps per wave (TPW = 1: half of one)
-    static_assert(HP == 16 * TPW * NWV * T && (TPW == 1 || TPW % 2 == 0) && L0T % 2 == 0, "team geometry");
     static_assert(!LNK || T == 1, "a LayerNorm after layer 1 needs the whole layer in one workgroup");
-    static_assert(T == 1 || NWV >= T, "one collecting wave per other member");
+    // fused policy (MPCcontrollerPolicyNet, ppo_bc_policy.py:54-88): each wave owns one policy tile
+    // pair; it shares the dynamics slab and the partials buffer (both free during the policy phase
+    // only when a team barrier ends the step, T > 1).  Reward net (NNDynamicsRewardModel): no LN.
+    // Reward net (NNDynamicsRewardModel): waves [0, NWV/2) hold delta-head tiles, waves [NWV/2, NWV)
+    // reward-head tiles (TPW each), so every wave keeps one head's weights: NH waves per head.
+    constexpr int PTW = PHP / 16 / NWV;                 // policy tiles per wave (1: half a k-step, 2: one)
+    static_assert(PHP == 0 || ((PTW == 1 || PTW == 2) && T > 1 && AK == 0), "policy geometry");
+    static_assert(!RW || (AK == 0 && TPW == 1 && NWV % 2 == 0), "reward net: tanh, no LayerNorm, one tile per wave");
+    constexpr int NB = RW ? 3 : 2;                      // hidden bias arrays (trunk, delta head, reward head)
+    constexpr int NH = RW ? NWV / 2 : NWV;              // waves per head
+    static_assert(HP == 16 * TPW * NH * T && (TPW == 1 || TPW % 2 == 0) && L0T % 2 == 0, "team geometry");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
@@ -231,7 +249,8 @@ void rollout_team(const RolloutArgs a) {
     const int bx = blockIdx.x;
     const int col = ((bx >> 3) / T) * 8 + (bx & 7);     // members of a column: blocks b, b + 8, ...
     const int tm = (bx >> 3) % T;                       // member
-    const int g = tm * NWV + w;                         // team wave: layer-1 tiles [TPW g, TPW (g + 1))
+    const bool rw_wave = RW && w >= NH;                 // (reward net) this wave holds reward-head tiles
+    const int g = tm * NH + (RW ? w % NH : w);          // team wave of its head: tiles [TPW g, TPW (g + 1))
     const int64_t ncol = (a.K + 15) / 16;
     uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp_ = TEAM_STAMP ? __builtin_amdgcn_s_memtime() : 0;
@@ -249,23 +268,35 @@ void rollout_team(const RolloutArgs a) {
         char* const base = reinterpret_cast<char*>(lds);
         double* C = reinterpret_cast<double*>(base);
         float* Bl = reinterpret_cast<float*>(base + kConstRows * kConstCols * 8);
-        int off = param_bytes(2, HP);
+        int off = param_bytes(NB, HP);
         float* const lnp = reinterpret_cast<float*>(base + off);
         off += LNK ? 4 * HP * 4 : 0;
         f4* const slab = reinterpret_cast<f4*>(base + off);
         off += P * 2048;
         float* const xch = reinterpret_cast<float*>(base + off);
-        off += 2 * NWV * 16 * 2 * 4;
+        off += AK ? 2 * NWV * 16 * 2 * 4 : 0;                              // (as team_lds_bytes)
         f4* const parts = reinterpret_cast<f4*>(base + off);
         off += NWV * 2048;
         f4* const tot = reinterpret_cast<f4*>(base + off);
         off += T > 1 ? T * 2048 : 0;
-        float* const xas = reinterpret_cast<float*>(base + off);
+        float* const xas = reinterpret_cast<float*>(base + off);          // (no policy)
+        float* const Pb = reinterpret_cast<float*>(base + off);           // (policy) biases [pL][PHP] + params
+        const char* const plw = base + off + (PHP > 0 ? pol_param_bytes(a.pL, PHP) : 0);   // policy weights
 
         for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
-        for (int l = 0; l < 2; ++l)
+        for (int l = 0; l < NB; ++l)
             for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kAct;
-        for (int i = threadIdx.x; i < 32; i += blockDim.x) Bl[2 * HP + i] = a.b[2][i];
+        for (int i = threadIdx.x; i < 32; i += blockDim.x) Bl[NB * HP + i] = a.b[NB][i];
+        int pw_total = 0;                                 // policy: every layer's packed bytes, copied once
+        if constexpr (PHP > 0) {
+            for (int l = 1; l < a.pL; ++l) pw_total += a.pwbytes[l];
+            for (int l = 0; l < a.pL; ++l)
+                for (int i = threadIdx.x; i < PHP; i += blockDim.x) Pb[l * PHP + i] = a.pb[l][i] * kTanhK;
+            for (int i = threadIdx.x; i < kPolParams; i += blockDim.x) Pb[a.pL * PHP + i] = a.pparams[i];
+            const f4* src = a.pw[1];                      // hidden layers 1..pL-1 (contiguous, capi.cpp pw_off)
+            for (int i = threadIdx.x; i < pw_total / 16; i += blockDim.x)
+                reinterpret_cast<f4*>(const_cast<char*>(plw))[i] = src[i];
+        }
         if constexpr (LNK)
             for (int l = 0; l < 2; ++l)
                 for (int i = threadIdx.x; i < HP; i += blockDim.x) {
@@ -273,60 +304,16 @@ void rollout_team(const RolloutArgs a) {
                     lnp[(2 + l) * HP + i] = a.lnb[l][i];
                 }
 
-        // ---- every weight fragment this wave uses, once (capi.cpp: layer 0 packed with TWp = L0T,
-        //      layer 1 with TWp = TPW, the output layer [0][k-step][tile]) ----
-        const int voff = lane * 16;
-        h8 w0h[L0T], w0l[L0T], w1h[P][TPW], w1l[P][TPW], woh[PPW][2], wol[PPW][2];
-        {
-            const __amdgpu_buffer_rsrc_t r0 = layer_rsrc(a.w[0], a.wbytes[0]);
-#pragma unroll
-            for (int j = 0; j < L0T; ++j) {
-                w0h[j] = fload(r0, voff, (w * L0T + j) * 2048);
-                w0l[j] = fload(r0, voff, (w * L0T + j) * 2048 + 1024);
-            }
-            const __amdgpu_buffer_rsrc_t r1 = layer_rsrc(a.w[1], a.wbytes[1]);
-#pragma unroll
-            for (int p = 0; p < P; ++p)
-#pragma unroll
-                for (int j = 0; j < TPW; ++j) {
-                    w1h[p][j] = fload(r1, voff, ((g * P + p) * TPW + j) * 2048);
-                    w1l[p][j] = fload(r1, voff, ((g * P + p) * TPW + j) * 2048 + 1024);
-                }
-            const __amdgpu_buffer_rsrc_t r2 = layer_rsrc(a.w[2], a.wbytes[2]);
-#pragma unroll
-            for (int pp = 0; pp < PPW; ++pp)
-#pragma unroll
-                for (int v = 0; v < 2; ++v) {
-                    const int p = TPW == 1 ? g >> 1 : g * PPW + pp;
-                    woh[pp][v] = fload(r2, voff, (p * 2 + v) * 2048);
-                    wol[pp][v] = fload(r2, voff, (p * 2 + v) * 2048 + 1024);
-                }
-        }
-        for (int i = threadIdx.x; i < kTeamNch * 16 * 16; i += blockDim.x)
-            if ((i & 15) >= A) xas[i] = 0.f;                // action slots past A stay zero (fill writes j < A)
+        if constexpr (PHP == 0)
+            for (int i = threadIdx.x; i < kTeamNch * 16 * 16; i += blockDim.x)
+                if ((i & 15) >= A) xas[i] = 0.f;            // action slots past A stay zero (fill writes j < A)
         __syncthreads();                                  // parameters in LDS
-
-        // ---- per-candidate state: lane (q, m) holds dims 16 v + 4 q + r (v = 0, 1) of candidate m,
-        //      in every wave of every member ----
-        const int64_t cand = (int64_t)col * 16 + m;
-        const bool valid = cand < a.K;
-        const bool writer = tm == 0 && w == 0;            // costs / trajectories: member 0, wave 0
-        double s[2][4];
-        double cost = 0.0;                                // trajectory_cost = 0 (cost_functions.py:60)
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int d = 16 * v + 4 * q + r;
-                s[v][r] = (valid && d < S) ? (a.state_inline ? a.state_v[d] : a.state[cand * a.state_stride + d]) : 0.0;
-                if (writer && a.traj && valid && d < S) a.traj[cand * S + d] = s[v][r];
-            }
-
         // ---- actions, normalised (dynamics.py:110) and cast to f32 (the TF feed), staged in LDS for
         //      kTeamNch steps at a time by the whole workgroup (one action per thread and pass, not per
         //      lane in the step loop): the caller's [H,K,A] array (np.random.uniform,
         //      controllers.py:53), Philox (rng_action), or the CEM sampler ----
         auto fill_actions = [&](int h0) {
+            if constexpr (PHP > 0) return;                // (the policy makes the actions)
             const int nh = min(kTeamNch, a.H - h0), n = nh * 16 * A;
             for (int i = threadIdx.x; i < n; i += blockDim.x) {
                 const int hh = i / (16 * A), rem = i - hh * 16 * A, mm = rem / A, j = rem - mm * A;
@@ -345,15 +332,99 @@ void rollout_team(const RolloutArgs a) {
             }
         };
 
+        fill_actions(0);                                  // (before the weight loads: its global loads
+        lds_barrier();                                    //  would otherwise wait behind them)
+        // ---- every weight fragment this wave uses, once (issued after the parameter barrier so the
+        //      loads stay in flight through the first step's LDS barriers) (capi.cpp: layer 0 packed with TWp = L0T,
+        //      layer 1 with TWp = TPW, the output layer [0][k-step][tile]) ----
+        const int voff = lane * 16;
+        h8 w0h[L0T], w0l[L0T], w1h[P][TPW], w1l[P][TPW], woh[PPW][2], wol[PPW][2];
+        // fused policy: its first layer's tiles and its output layer's k-step stay in registers
+        constexpr int PA = PHP > 0 ? PTW : 1;
+        h8 p0h[PA], p0l[PA], pwoh, pwol;
+        if constexpr (PHP > 0) {
+            const __amdgpu_buffer_rsrc_t q0 = layer_rsrc(a.pw[0], a.pwbytes[0]);
+#pragma unroll
+            for (int j = 0; j < PTW; ++j) {
+                p0h[j] = fload(q0, voff, (w * PTW + j) * 2048);
+                p0l[j] = fload(q0, voff, (w * PTW + j) * 2048 + 1024);
+            }
+            const __amdgpu_buffer_rsrc_t qo = layer_rsrc(a.pw[a.pL], a.pwbytes[a.pL]);
+            const int kp = PTW == 2 ? w : w >> 1;         // this wave's k-step of the output layer
+            pwoh = fload(qo, voff, kp * 2048);
+            pwol = fload(qo, voff, kp * 2048 + 1024);
+        }
+        {
+            if constexpr (!RW) {                          // (reward net: streamed per step, below)
+                const __amdgpu_buffer_rsrc_t r0 = layer_rsrc(a.w[0], a.wbytes[0]);
+#pragma unroll
+                for (int j = 0; j < L0T; ++j) {
+                    w0h[j] = fload(r0, voff, (w * L0T + j) * 2048);
+                    w0l[j] = fload(r0, voff, (w * L0T + j) * 2048 + 1024);
+                }
+            }
+            const int lh = rw_wave ? 3 : 1;               // this wave's head (dense_1 or dense_3)
+            const __amdgpu_buffer_rsrc_t r1 = layer_rsrc(a.w[lh], a.wbytes[lh]);
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) {
+                    w1h[p][j] = fload(r1, voff, ((g * P + p) * TPW + j) * 2048);
+                    w1l[p][j] = fload(r1, voff, ((g * P + p) * TPW + j) * 2048 + 1024);
+                }
+            // (reward-head waves: tile 0 zero, tile 1 = dense_4 packed as one 16-row tile whose row S-16
+            //  feeds output row S -- capi.cpp split reward layout; the delta output weights there are 0)
+            const __amdgpu_buffer_rsrc_t r2 = layer_rsrc(a.w[rw_wave ? 4 : 2], a.wbytes[rw_wave ? 4 : 2]);
+#pragma unroll
+            for (int pp = 0; pp < PPW; ++pp)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const int p = TPW == 1 ? g >> 1 : g * PPW + pp;
+                    const int o = rw_wave ? (v == 0 ? 0x7FFFF000 : p * 2048) : (p * 2 + v) * 2048;  // (beyond range: 0)
+                    woh[pp][v] = fload(r2, voff, o);
+                    wol[pp][v] = fload(r2, voff, o + 1024);
+                }
+        }
+
+        // ---- per-candidate state: lane (q, m) holds dims 16 v + 4 q + r (v = 0, 1) of candidate m,
+        //      in every wave of every member ----
+        const int64_t cand = (int64_t)col * 16 + m;
+        const bool valid = cand < a.K;
+        const bool writer = tm == 0 && w == 0;            // costs / trajectories: member 0, wave 0
+        double s[2][4];
+        double cost = 0.0;                                // trajectory_cost = 0 (cost_functions.py:60)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * v + 4 * q + r;
+                s[v][r] = (valid && d < S) ? (a.state_inline ? a.state_v[d] : a.state[cand * a.state_stride + d]) : 0.0;
+                if (writer && a.traj && valid && d < S) a.traj[cand * S + d] = s[v][r];
+            }
+
         const float f1base = a.winv[1] * kAct;
         const float fo = a.winv[2];
-        float* const Bout = Bl + 2 * HP;
+        float* const Bout = Bl + NB * HP;
+        const int qc = RW ? (S - 16) >> 2 : 0;           // lane row holding the cost: dim 17 / reward row S
         gu64* const gb = (gu64*)a.team_buf;           // (global address space: never flat)
         bool dead = false;                                // a team exchange timed out: finish without waiting
         f4 ot[2];                                         // the step's summed output layer (rows 16 v + 4 q + r)
 
         stamp(9);
         for (int h = 0;; ++h) {
+            if constexpr (RW) {
+                // reward net: the registers hold both heads' tiles, so the trunk's fragments (8 KB per
+                // wave) are re-read from L2 every step, requested here -- their latency passes under the
+                // tail, the policy and the layer-0 input (an opaque offset keeps them in the loop)
+                int vo = voff;
+                asm volatile("" : "+v"(vo));
+                const __amdgpu_buffer_rsrc_t r0 = layer_rsrc(a.w[0], a.wbytes[0]);
+#pragma unroll
+                for (int j = 0; j < L0T; ++j) {
+                    w0h[j] = fload(r0, vo, (w * L0T + j) * 2048);
+                    w0l[j] = fload(r0, vo, (w * L0T + j) * 2048 + 1024);
+                }
+            }
             if (h > 0) {
                 // ---- de-normalise + residual (dynamics.py:113,116; f64, no FMA), cheetah cost
                 //      (cost_functions.py:12-28), in step order (:59-63) ----
@@ -362,13 +433,17 @@ void rollout_team(const RolloutArgs a) {
                 // (branch-free: dims >= S carry the padded constants -- mean 0, std 0 -- and are never read)
                 f4 bv[2];
                 double c4[2][4], c5[2][4];
+                // (the constants are re-read from LDS every step: an opaque base keeps the compiler from
+                //  hoisting 40 doubles per lane out of the step loop, registers the resident weights need)
+                const double* Cs = C;
+                asm volatile("" : "+v"(Cs));
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
                     bv[v] = *reinterpret_cast<const f4*>(Bout + 16 * v + 4 * q);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        c4[v][r] = C[4 * 32 + 16 * v + 4 * q + r];
-                        c5[v][r] = C[5 * 32 + 16 * v + 4 * q + r];
+                        c4[v][r] = Cs[4 * 32 + 16 * v + 4 * q + r];
+                        c5[v][r] = Cs[5 * 32 + 16 * v + 4 * q + r];
                     }
                 }
 #pragma unroll
@@ -379,6 +454,19 @@ void rollout_team(const RolloutArgs a) {
                         const double ud = __dadd_rn(__dmul_rn((double)dn, c5[v][r]), c4[v][r]);
                         s[v][r] = __dadd_rn(s[v][r], ud);
                     }
+                if constexpr (RW) {
+                    // learned reward (dynamics.py:236) x gamma**h, running sum (controllers.py:139,150):
+                    // output row S = tile 1, lane row (S - 16) >> 2, register (S - 16) & 3
+                    if (q == qc) {
+                        float o_s = 0.f;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (r == ((S - 16) & 3)) o_s = ot[1][r];
+                        const float nr = fmaf(o_s, fo, Bout[S]);                      // BiasAdd (f32)
+                        const double rw = __dadd_rn(__dmul_rn((double)nr, a.std_reward), a.mean_reward);
+                        cost = __dadd_rn(cost, __dmul_rn(rw, a.gpow[h - 1]));
+                    }
+                }
                 if (a.cost == BCMPC_COST_CHEETAH) {
                     const double score =
                         __dsub_rn(10.0 * (double)npen, div_rn(__dsub_rn(s[1][1], s17), 0.01, 1.0 / 0.01));
@@ -396,11 +484,115 @@ void rollout_team(const RolloutArgs a) {
             }
             stamp(0);
             if (h == a.H) break;
-            if (h % kTeamNch == 0) {
+            if (h > 0 && h % kTeamNch == 0) {
                 fill_actions(h);
-                __syncthreads();                          // the chunk's action inputs (the previous chunk's
+                lds_barrier();                               // the chunk's action inputs (the previous chunk's
             }                                             // last reads were before the partials barrier)
             stamp(1);
+
+            // ---- fused policy (MlpPolicy.act, ppo_bc_policy.py:54-88; mixing controllers.py:196-206),
+            //      computed by every member (the same bits everywhere): obz = clip((f32(ob) - mean) / std,
+            //      -5, 5) x 2^11 in this lane's dims (one k-step B fragment, no exchange), tanh hidden
+            //      layers x 2^12 (wave w: tile pair = k-step w of the next layer, through the slab), the
+            //      output tile (action j at row S - 16 + j) K-split over the waves, partials summed in
+            //      wave order in every wave; pact = the actions of this lane's v = 1 dims ----
+            double pact[4] = {0.0, 0.0, 0.0, 0.0};
+            if constexpr (PHP > 0) {
+                constexpr int PPn = PHP / 32;
+                const float* const pm = Pb + a.pL * PHP;   // [obmean 32][obstd 32][logstd 16][out bias 16]
+                h8 zh, zl;
+                {
+                    float z[8];
+#pragma unroll
+                    for (int v = 0; v < 2; ++v)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int d = 16 * v + 4 * q + r;
+                            float vv = ((float)s[v][r] - pm[d]) / pm[32 + d];
+                            vv = fminf(fmaxf(vv, -5.0f), 5.0f);
+                            z[4 * v + r] = d < S ? vv * 2048.0f : 0.f;
+                        }
+                    split8(z, zh, zl);
+                }
+                auto lread = [&](int byte_off) __attribute__((always_inline)) {
+                    return *reinterpret_cast<const h8*>(plw + byte_off + lane * 16);
+                };
+                typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                // this wave's policy tiles [PTW w, PTW (w + 1)) of every hidden layer; their epilogue
+                // is the B fragment of k-step w (PTW = 2) or half w & 1 of k-step w >> 1 (PTW = 1)
+                f4 pa[PTW];
+                h8 xh, xl;
+                auto pepi = [&](float f, const float* bias) __attribute__((always_inline)) {
+                    if constexpr (PTW == 2) {
+                        epi_pair_tanh(pa[0], pa[1], f, bias, 2 * w, q, xh, xl);
+                    } else {
+                        const f4 b = *reinterpret_cast<const f4*>(bias + 16 * w + 4 * q);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) pa[0][r] = tanh4096(fmaf(pa[0][r], f, b[r]));
+                        split_tiles<1>(pa, w & 1, *reinterpret_cast<h8(*)[1]>(&xh), *reinterpret_cast<h8(*)[1]>(&xl));
+                    }
+                };
+#pragma unroll
+                for (int j = 0; j < PTW; ++j) pa[j] = mm3(p0h[j], p0l[j], zh, zl, (f4){0.f, 0.f, 0.f, 0.f});
+                pepi(a.pwinv[0] * kTanhK, Pb);
+                int lbase = 0, buf = 0;                   // (LDS: hidden layers 1..pL-1 only)
+                for (int l = 1; l < a.pL; ++l) {
+                    if constexpr (PTW == 2) {
+                        swrite(slab + ((buf * PPn + w) * 2 + 0) * 64 + lane, xh);
+                        swrite(slab + ((buf * PPn + w) * 2 + 1) * 64 + lane, xl);
+                    } else {
+                        const h4 hh4 = {xh[4 * (w & 1)], xh[4 * (w & 1) + 1], xh[4 * (w & 1) + 2], xh[4 * (w & 1) + 3]};
+                        const h4 ll4 = {xl[4 * (w & 1)], xl[4 * (w & 1) + 1], xl[4 * (w & 1) + 2], xl[4 * (w & 1) + 3]};
+                        reinterpret_cast<h4*>(slab + ((buf * PPn + (w >> 1)) * 2 + 0) * 64 + lane)[w & 1] = hh4;
+                        reinterpret_cast<h4*>(slab + ((buf * PPn + (w >> 1)) * 2 + 1) * 64 + lane)[w & 1] = ll4;
+                    }
+                    lds_barrier();                        // the layer's input complete
+#pragma unroll
+                    for (int j = 0; j < PTW; ++j) pa[j] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int pq = 0; pq < PPn; ++pq) {
+                        const h8 bh = sread(slab + ((buf * PPn + pq) * 2 + 0) * 64 + lane);
+                        const h8 bl = sread(slab + ((buf * PPn + pq) * 2 + 1) * 64 + lane);
+#pragma unroll
+                        for (int j = 0; j < PTW; ++j) {
+                            const int o = lbase + ((PTW * w + j) * PPn + pq) * 2048;     // [tile][k-step][hi|lo]
+                            pa[j] = mm3(lread(o), lread(o + 1024), bh, bl, pa[j]);
+                        }
+                    }
+                    pepi(a.pwinv[l] * kTanhK, Pb + l * PHP);
+                    lbase += a.pwbytes[l];
+                    buf ^= 1;                             // (double-buffered: no barrier before the writes)
+                }
+                // output layer [PHP -> one 16-row tile], K-split: this wave's (half) k-step, from registers
+                const f4 po_ = mm3(pwoh, pwol, xh, xl, (f4){0.f, 0.f, 0.f, 0.f});
+                parts[w * 64 + lane] = po_;
+                lds_barrier();                            // the output layer's partials
+                f4 o = parts[0 * 64 + lane];
+#pragma unroll
+                for (int x = 1; x < NWV; ++x) o += parts[x * 64 + lane];    // fixed summation order
+                const float fo_p = a.pwinv[a.pL];
+                const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 + 4 * q + r - S;
+                    if (j < 0 || j >= A) continue;
+                    const float mean = o[r] * fo_p + pm[80 + 4 * q + r];       // dense bias (f32)
+                    if (a.pol_mode == BCMPC_POLICY_STOCHASTIC) {
+                        const float sd = expf(pm[64 + j]);
+                        pact[r] = (double)(mean + sd * rng_normal(a.seed ^ 0x9E3779B97F4A7C15ull, gcand, h, j));
+                    } else {
+                        // (1 - explore) * mean in f32 (NumPy keeps the f32 dtype), + explore * U in f64
+                        const double uu = !valid ? 0.0
+                                          : a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
+                                                      : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
+                        const float t1 = (float)(1.0 - a.explore) * mean;
+                        pact[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, uu));
+                    }
+                    if (writer && a.act_out && h < a.act_out_steps && valid)   // action_paths (controllers.py:213)
+                        __hip_atomic_store(&a.act_out[((int64_t)h * a.K + cand) * A + j], pact[r], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
 
             // ---- layer-0 input: normalised state (dynamics.py:109) and action, cast to f32, scaled by
             //      the power of two that puts the column's max |x| in [2^11, 2^12) ----
@@ -412,15 +604,24 @@ void rollout_team(const RolloutArgs a) {
                 const float* const xr = xas + ((h % kTeamNch) * 16 + m) * 16;
                 double c0[2][4], c1[2][4], c8[2][4];
                 float av[2][4];
+                const double* Cs = C;
+                asm volatile("" : "+v"(Cs));
 #pragma unroll
                 for (int v = 0; v < 2; ++v)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int d = 16 * v + 4 * q + r;
-                        c0[v][r] = C[0 * 32 + d];
-                        c1[v][r] = C[1 * 32 + d];
-                        c8[v][r] = C[8 * 32 + d];
-                        av[v][r] = xr[min(max(d - S, 0), 15)];     // (slots >= A hold zeros)
+                        c0[v][r] = Cs[0 * 32 + d];
+                        c1[v][r] = Cs[1 * 32 + d];
+                        c8[v][r] = Cs[8 * 32 + d];
+                        if constexpr (PHP > 0) {              // the policy's action (dynamics.py:110)
+                            const int j = min(max(d - S, 0), A - 1);
+                            av[v][r] = v == 1 && d >= S && d < S + A
+                                           ? (float)div_rn(__dsub_rn(pact[r], C[2 * 32 + j]), C[3 * 32 + j], C[9 * 32 + j])
+                                           : 0.f;
+                        } else {
+                            av[v][r] = xr[min(max(d - S, 0), 15)];     // (slots >= A hold zeros)
+                        }
                     }
 #pragma unroll
                 for (int v = 0; v < 2; ++v)
@@ -468,7 +669,7 @@ void rollout_team(const RolloutArgs a) {
                 }
             }
             stamp(3);
-            __syncthreads();                              // layer-1 input complete
+            lds_barrier();                                   // layer-1 input complete
             stamp(4);
 
             // ---- layer 1 [h -> h]: this wave's TPW tiles over all P k-steps ----
@@ -490,16 +691,18 @@ void rollout_team(const RolloutArgs a) {
 #pragma unroll
                 for (int j = 0; j < TPW; ++j) acc1[j] += acc1b[j];
             stamp(5);
-            const float f1 = DYN ? f1base * fcol0 : f1base;
+            // (reward-head waves: dense_3's scale and biases)
+            const float f1 = rw_wave ? a.winv[3] * kTanhK : DYN ? f1base * fcol0 : f1base;
+            const float* const Bh = Bl + (rw_wave ? 2 : 1) * HP;
             h8 oh[PPW], ol[PPW];
             float fcol1 = 1.f;
             if constexpr (AK == 0 && TPW >= 2) {
 #pragma unroll
                 for (int pp = 0; pp < PPW; ++pp)
-                    epi_pair_tanh(acc1[2 * pp], acc1[2 * pp + 1], f1, Bl + HP, TPW * g + 2 * pp, q, oh[pp], ol[pp]);
+                    epi_pair_tanh(acc1[2 * pp], acc1[2 * pp + 1], f1, Bh, TPW * g + 2 * pp, q, oh[pp], ol[pp]);
             } else {
                 if constexpr (AK == 0) {
-                    const f4 b = *reinterpret_cast<const f4*>(Bl + HP + 16 * g + 4 * q);
+                    const f4 b = *reinterpret_cast<const f4*>(Bh + 16 * g + 4 * q);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc1[0][r] = tanh4096(fmaf(acc1[0][r], f1, b[r]));
                 } else if constexpr (DYN) {
@@ -526,7 +729,7 @@ void rollout_team(const RolloutArgs a) {
             }
             parts[(w * 2 + 0) * 64 + lane] = po[0];
             parts[(w * 2 + 1) * 64 + lane] = po[1];
-            __syncthreads();                              // partials complete; every wave is done with the slab
+            lds_barrier();                                   // partials complete; every wave is done with the slab
             stamp(7);
             if constexpr (T == 1) {
 #pragma unroll
@@ -544,30 +747,35 @@ void rollout_team(const RolloutArgs a) {
 #pragma unroll
                     for (int x = 1; x < NWV; ++x) mp[v] += parts[(x * 2 + v) * 64 + lane];
                 }
-                // exchange (rows < S only): wave 0 publishes this member's partial as granules
-                // {epoch, f32} at k * 64 + lane (k = 4 v + r), wave j in [1, T) collects member
-                // (tm + j) % T's; every partial lands in the LDS slot of its member
+                // exchange (rows < S, + row S for the reward net): wave 0 publishes this member's partial
+                // as granules {epoch, f32} at k * 64 + lane (k = 4 v + r); member (tm + o) % T's are
+                // collected by wave o % NWV; every partial lands in the LDS slot of its member
                 const unsigned ep = (gen << 10) + (unsigned)h + 1u;
                 const size_t slot = ((size_t)col * 2 + (h & 1)) * T;
+                const int R = S + (RW ? 1 : 0);           // rows exchanged: delta rows (+ the reward row)
                 if (w == 0) {
                     gu64* const mine = gb + (slot + tm) * 512;
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
-                        if (16 * (k >> 2) + 4 * q + (k & 3) < S)
+                        if (16 * (k >> 2) + 4 * q + (k & 3) < R)
                             __hip_atomic_store(mine + k * 64 + lane,
                                                ((unsigned long long)ep << 32) | __float_as_uint(mp[k >> 2][k & 3]),
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     tot[(tm * 2 + 0) * 64 + lane] = mp[0];
                     tot[(tm * 2 + 1) * 64 + lane] = mp[1];
-                } else if (w < T) {
-                    const int t = (tm + w) % T;
+                }
+                // member (tm + o) % T is collected by wave o % NWV
+#pragma unroll
+                for (int o = 1; o < T; ++o) {
+                    if (o % NWV != w) continue;
+                    const int t = (tm + o) % T;
                     const gu64* const src = gb + (slot + t) * 512;
                     f4 got[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
                     for (int spins = 0; !dead; ++spins) {
                         bool ok = true;
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
-                            if (16 * (k >> 2) + 4 * q + (k & 3) < S) {
+                            if (16 * (k >> 2) + 4 * q + (k & 3) < R) {
                                 const unsigned long long xv =
                                     __hip_atomic_load(src + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 got[k >> 2][k & 3] = __uint_as_float((unsigned)xv);
@@ -585,7 +793,7 @@ void rollout_team(const RolloutArgs a) {
                     tot[(t * 2 + 0) * 64 + lane] = got[0];
                     tot[(t * 2 + 1) * 64 + lane] = got[1];
                 }
-                __syncthreads();                          // every member's partial in LDS
+                lds_barrier();                               // every member's partial in LDS
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
                     ot[v] = tot[(0 * 2 + v) * 64 + lane];
@@ -595,7 +803,7 @@ void rollout_team(const RolloutArgs a) {
             }
             stamp(8);
         }
-        if (writer && a.costs && valid && q == 0) a.costs[cand] = cost;
+        if (writer && a.costs && valid && q == qc) a.costs[cand] = cost;
         if constexpr (TEAM_STAMP) {
             if (a.stamps && lane == 0)
                 for (int k = 0; k < 10; ++k) a.stamps[((size_t)blockIdx.x * NWV + w) * 10 + k] = ph_[k];
@@ -614,52 +822,64 @@ void rollout_team(const RolloutArgs a) {
     }
 }
 
-// geometry per padded hidden width: waves per member, layer-1 tiles per wave, members per team
+// geometry per padded hidden width and model kind (0 plain delta net, 1 + fused policy, 2 reward net
+// with or without the policy): waves per member, layer-1 (head) tiles per wave, members per team
 struct TeamShape {
     int nwv, tpw, members;
 };
-static TeamShape team_shape_of(int hidden_padded) {
-    switch (hidden_padded) {
-        case 64: return {2, 2, 1};
-        case 128: return {4, 2, 1};
-        case 256: return {4, 4, 1};
-        case 512: return {4, 2, 4};
-        default: return {0, 0, 0};
+static TeamShape team_shape_of(int hidden_padded, int kind) {
+    if (kind == 0) {
+        switch (hidden_padded) {
+            case 64: return {2, 2, 1};
+            case 128: return {4, 2, 1};
+            case 256: return {4, 4, 1};
+            case 512: return {4, 2, 4};
+            default: return {0, 0, 0};
+        }
     }
+    if (hidden_padded != 512) return {0, 0, 0};
+    return kind == 1 ? TeamShape{4, 2, 4} : TeamShape{8, 1, 8};   // reward: one head tile per wave
 }
 
-int team_members(int hidden_padded) { return team_shape_of(hidden_padded).members; }
-int team_layer0_tiles(int hidden_padded) {
-    const TeamShape t = team_shape_of(hidden_padded);
+int team_members(int hidden_padded, int kind) { return team_shape_of(hidden_padded, kind).members; }
+int team_layer0_tiles(int hidden_padded, int kind) {
+    const TeamShape t = team_shape_of(hidden_padded, kind);
     return t.nwv ? hidden_padded / 16 / t.nwv : 0;
 }
-int team_layer1_tiles(int hidden_padded) { return team_shape_of(hidden_padded).tpw; }
-int64_t team_blocks(int64_t K, int hidden_padded) {
+int team_layer1_tiles(int hidden_padded, int kind) { return team_shape_of(hidden_padded, kind).tpw; }
+int64_t team_blocks(int64_t K, int hidden_padded, int kind) {
     const int64_t ncol = (K + 15) / 16;
-    return ((ncol + 7) / 8) * 8 * team_members(hidden_padded);
+    return ((ncol + 7) / 8) * 8 * team_members(hidden_padded, kind);
 }
-size_t team_buf_bytes(int64_t K, int hidden_padded) {
-    const int T = team_members(hidden_padded);
+size_t team_buf_bytes(int64_t K, int hidden_padded, int kind) {
+    const int T = team_members(hidden_padded, kind);
     return T > 1 ? (size_t)((K + 15) / 16 + 8) * 2 * T * 512 * sizeof(unsigned long long) : 0;
 }
+static int team_kind(const RolloutArgs& a) { return a.model == BCMPC_MODEL_REWARD ? 2 : a.pL > 0 ? 1 : 0; }
 
-template <int HP, int NWV, int TPW, int T, int AK>
+template <int HP, int NWV, int TPW, int T, int AK, int PHP = 0, bool RW = false>
 static hipError_t launch_team_t(const RolloutArgs& a, hipStream_t st) {
-    constexpr int lds = team_lds_bytes(HP, NWV, T, AK);
-    static_assert(lds <= 160 * 1024, "LDS");
+    int pw_bytes = 0;
+    if constexpr (PHP > 0) {
+        if (a.pL < 1 || a.pL > BCMPC_MAX_LAYERS || a.phidden_padded != PHP) return hipErrorInvalidValue;
+        for (int l = 1; l < a.pL; ++l) pw_bytes += a.pwbytes[l];      // (LDS: the hidden->hidden layers)
+    }
+    const int lds = team_lds_bytes(HP, NWV, T, AK, RW, PHP, PHP > 0 ? a.pL : 0, pw_bytes);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)rollout_team<HP, NWV, TPW, T, AK>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        hipError_t e = hipFuncSetAttribute((const void*)rollout_team<HP, NWV, TPW, T, AK, PHP, RW>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    if (a.L != 2 || a.model != BCMPC_MODEL_DELTA || a.pL != 0 || a.S + a.A > 32 || a.S > 32 || a.A > 15 || a.H > 1022 ||
+    if (a.L != 2 || (a.model == BCMPC_MODEL_REWARD) != RW || (a.pL > 0) != (PHP > 0) || a.S + a.A > 32 ||
+        a.S > 32 || a.A > 15 || a.H > 1022 || ((RW || PHP > 0) && a.S < 16) ||
         (a.cost == BCMPC_COST_CHEETAH && a.S < 18) || AK != ((a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0)) ||
         (T > 1 && (!a.team_buf || !a.team_ctl)))
         return hipErrorInvalidValue;
-    const int64_t blocks = team_blocks(a.K, HP);
-    hipLaunchKernelGGL((rollout_team<HP, NWV, TPW, T, AK>), dim3((unsigned)blocks), dim3(64 * NWV), lds, st, a);
+    const int64_t blocks = team_blocks(a.K, HP, team_kind(a));
+    hipLaunchKernelGGL((rollout_team<HP, NWV, TPW, T, AK, PHP, RW>), dim3((unsigned)blocks), dim3(64 * NWV), lds, st, a);
     return hipGetLastError();
 }
 
@@ -680,6 +900,14 @@ static hipError_t launch_team_ak(const RolloutArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+    const int kind = team_kind(a);
+    if (kind > 0) {
+        // the policy / reward variants: hidden 512, tanh, no LayerNorm (the run.sh recipe's nets)
+        if (hidden_padded != 512 || a.act != BCMPC_ACT_TANH || a.ln) return hipErrorInvalidValue;
+        if (kind == 1) return launch_team_t<512, 4, 2, 4, 0, 128, false>(a, st);
+        if (a.pL > 0) return launch_team_t<512, 8, 1, 8, 0, 128, true>(a, st);
+        return launch_team_t<512, 8, 1, 8, 0, 0, true>(a, st);
+    }
     switch (hidden_padded) {
         case 64: return launch_team_ak<64, 2, 2, 1>(a, st);
         case 128: return launch_team_ak<128, 4, 2, 1>(a, st);

@@ -315,7 +315,7 @@ def _split_policy_ok(hidden, act, ln):
     return act == "tanh" and not ln and 448 < hidden <= 1024
 
 
-@pytest.mark.parametrize("kernel", ["fp32", "split1", "split2", "split4"])
+@pytest.mark.parametrize("kernel", ["fp32", "split1", "split2", "split4", "team"])
 @pytest.mark.parametrize("name", golden_names("policy"))
 def test_policy_engine_matches_reference_fixture(name, kernel):
     """MPCcontrollerPolicyNet (self_exp=False) fused into the group kernel (fp32) or the split
@@ -325,6 +325,8 @@ def test_policy_engine_matches_reference_fixture(name, kernel):
     w, p = g.weights, g.policy
     if kernel != "fp32" and not _split_policy_ok(w.hidden, w.activation, w.layer_norm):
         pytest.skip("split kernel with a policy: tanh dynamics without LayerNorm, hidden 449..1024")
+    if kernel == "team" and not (w.hidden <= 512 and p.hidden <= 128 and p.n_layers <= 2 and g.K <= 2048):
+        pytest.skip("team kernel with a policy: hidden 449..512, policy <= 2 x 128, small K")
     kw = dict(precision="fp32") if kernel == "fp32" else dict(kernel=kernel)
     eng = RolloutEngine(g.S, g.A, w.hidden, w.n_layers, w.activation, w.layer_norm, g.H, g.K,
                         policy_hidden=p.hidden, policy_layers=p.n_layers, policy_mode="explore", **kw)
@@ -361,7 +363,7 @@ def test_policy_controller_dropin(name):
     assert np.random.random() == float(g.z["next_draw"])        # same RNG side effect as the reference
 
 
-@pytest.mark.parametrize("kernel", ["fp32", "split2"])
+@pytest.mark.parametrize("kernel", ["fp32", "split2", "team"])
 def test_policy_stochastic_mode_pinned_every_step(kernel):
     """self_exp=True (run.sh's recipe, controllers.py:202-203): at EVERY horizon step the action the
     kernel rolled out equals mean(s_h) + exp(logstd) * z_h, where s_h is the GPU's own trajectory
@@ -379,7 +381,7 @@ def test_policy_stochastic_mode_pinned_every_step(kernel):
         kw = dict(precision="fp32")
     else:
         w = orc.synthetic_weights(S, A, 500, 2, "tanh", False)
-        kw = dict(kernel="split2")
+        kw = dict(kernel=kernel)
     p = orc.synthetic_policy(S, A, 128, 2)
     norm = orc.synthetic_normalization()
     state = orc.synthetic_state(norm)

@@ -81,12 +81,14 @@ def _skip_split(g, kernel):
             pytest.skip("split4 needs >= 4 waves (hidden > 64)")
 
 
-@pytest.mark.parametrize("kernel", ["group4", "group8", "split1", "split2", "split4"])
+@pytest.mark.parametrize("kernel", ["group4", "group8", "split1", "split2", "split4", "team"])
 @pytest.mark.parametrize("name", REWARD)
 def test_reward_engine_matches_reference_fixture(name, kernel):
     from bc_mpc_amd.engine import RolloutEngine
     g = RewardGolden(name)
     _skip_split(g, kernel)
+    if kernel == "team" and not (448 < g.weights.hidden <= 512 and not g.weights.layer_norm and 0 < g.K <= 1024):
+        pytest.skip("team kernel, reward net: hidden 449..512, no LayerNorm, K <= 1024")
     eng = RolloutEngine(g.S, g.A, g.weights.hidden, 2, "tanh", g.weights.layer_norm, g.H, g.K, device=0,
                         cost="reward", model="reward", kernel=kernel)
     assert eng.info()["kernel"] == kernel
@@ -128,12 +130,15 @@ def test_reward_controller_dropin(name):
     assert np.array_equal(env.action_space.np_random.uniform(-1, 1, size=g.A), want_next)
 
 
-@pytest.mark.parametrize("kernel", ["group4", "group8"])
+@pytest.mark.parametrize("kernel", ["group4", "group8", "team"])
 @pytest.mark.parametrize("name", POLREW)
 def test_policy_reward_engine_matches_reference_fixture(name, kernel):
     from bc_mpc_amd.engine import PolicySpec, RolloutEngine
     g = RewardGolden(name)
     p = g.policy
+    if kernel == "team" and not (448 < g.weights.hidden <= 512 and not g.weights.layer_norm and 0 < g.K <= 1024
+                                 and p.hidden <= 128 and p.n_layers <= 2):
+        pytest.skip("team kernel, reward net + policy: hidden 449..512, no LayerNorm, policy <= 2 x 128")
     eng = RolloutEngine(g.S, g.A, g.weights.hidden, 2, "tanh", g.weights.layer_norm, g.H, g.K, device=0,
                         cost="reward", model="reward", kernel=kernel, policy_hidden=p.hidden,
                         policy_layers=p.n_layers, policy_mode="explore")
@@ -277,3 +282,42 @@ def test_split_policy_reward_matches_fp32_engine(mode):
     assert (err <= 2e-6).all()
     assert_rewards_close(rsp.costs, r32.costs, f"split polrew {mode}")
     assert rsp.best_index == int(np.argmax(rsp.costs))
+
+
+@pytest.mark.parametrize("mode", ["explore", "stochastic", "none"])
+def test_team_policy_reward_matches_fp32_engine(mode):
+    """The run.sh recipe's shape on the small-K team kernel (rollout_team.hip: reward-head and
+    delta-head waves, fused policy, 8 workgroups per 16-candidate column, one exchange per step)
+    against the fp32 group kernel on the same draws: K = 400 (train_mpc_ppo.py:71), hidden 500."""
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    S, A, K, H, h = 20, 6, 400, 12, 500
+    norm = orc.synthetic_normalization(S, A, seed=5, reward=True)
+    w = orc.synthetic_reward_weights(S, A, h, False, seed_base=123)
+    p = orc.synthetic_policy(S, A, 128, 2, seed=9)
+    state = orc.synthetic_state(norm, seed=6)
+    expl = np.random.RandomState(4).uniform(-1, 1, (H, K, A))
+    out = {}
+    for kern in ("fp32", "team"):
+        kw = dict(precision="fp32") if kern == "fp32" else dict(kernel="team")
+        pol = dict(policy_hidden=128, policy_layers=2, policy_mode=mode) if mode != "none" else {}
+        e = RolloutEngine(S, A, h, 2, "tanh", False, H, K, cost="reward", model="reward", **pol, **kw)
+        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh", model="reward"), norm, 1)
+        e.set_discount(0.99)
+        if mode != "none":
+            e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.5, 1)
+        if kern == "team":
+            assert e.info()["kernel"] == "team"
+        rs = [e.get_action(state, expl if mode != "stochastic" else None, seed=13, return_costs=True)
+              for _ in range(3)]
+        for r in rs[1:]:                                   # repeated launches: bit-identical
+            assert np.array_equal(r.costs, rs[0].costs)
+        out[kern] = (rs[0], e.first_actions() if mode != "none" else None)
+        e.close()
+    (r32, a32), (rt, at) = out["fp32"], out["team"]
+    if mode != "none":
+        err = np.abs(at - a32)
+        print(f"[team polrew {mode}] max|dfirst|={err.max():.3e}")
+        assert (err <= 2e-6).all()
+    assert_rewards_close(rt.costs, r32.costs, f"team polrew {mode}")
+    assert rt.best_index == int(np.argmax(rt.costs))
