@@ -66,6 +66,14 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 constexpr int kTeamSpins = 1 << 20;      // exchange polls before a team gives up (~1 s)
 constexpr int kTeamNch = 16;             // steps of action inputs staged in LDS per fill
+constexpr int kPolNch = 8;               // steps of the policy's draws (f64) staged per fill
+
+// reward-net layout: TEAM_RW_NWV waves per member (4: one 512-register wave per SIMD, two head tiles
+// per wave; 8: two 256-register waves per SIMD, one head tile each -- 68 spilled registers with the
+// policy, measured slower)
+#ifndef TEAM_RW_NWV
+#define TEAM_RW_NWV 4
+#endif
 
 __device__ __forceinline__ f4 mm(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
 
@@ -216,7 +224,7 @@ __device__ __forceinline__ void split_tiles(const f4 (&v)[NTL], int odd, h8 (&xh
 __host__ __device__ constexpr int team_lds_bytes(int HP, int NWV, int T, int AK, bool RW = false, int PHP = 0,
                                                  int PL = 0, int pw_bytes = 0) {
     return param_bytes(RW ? 3 : 2, HP) + ((AK & 2) ? 4 * HP * 4 : 0) + (HP / 32) * 2048 + (AK ? 2 * NWV * 16 * 2 * 4 : 0) +
-           NWV * 2048 + (T > 1 ? T * 2048 : 0) + (PHP > 0 ? pol_param_bytes(PL, PHP) + pw_bytes
+           NWV * 2048 + (T > 1 ? T * 2048 : 0) + (PHP > 0 ? pol_param_bytes(PL, PHP) + pw_bytes + kPolNch * 16 * 16 * 8
                                                           : kTeamNch * 16 * 16 * 4);
 }
 
@@ -236,7 +244,7 @@ void rollout_team(const RolloutArgs a) {
     // reward-head tiles (TPW each), so every wave keeps one head's weights: NH waves per head.
     constexpr int PTW = PHP / 16 / NWV;                 // policy tiles per wave (1: half a k-step, 2: one)
     static_assert(PHP == 0 || ((PTW == 1 || PTW == 2) && T > 1 && AK == 0), "policy geometry");
-    static_assert(!RW || (AK == 0 && TPW == 1 && NWV % 2 == 0), "reward net: tanh, no LayerNorm, one tile per wave");
+    static_assert(!RW || (AK == 0 && NWV % 2 == 0), "reward net: tanh, no LayerNorm, delta / reward waves");
     constexpr int NB = RW ? 3 : 2;                      // hidden bias arrays (trunk, delta head, reward head)
     constexpr int NH = RW ? NWV / 2 : NWV;              // waves per head
     static_assert(HP == 16 * TPW * NH * T && (TPW == 1 || TPW % 2 == 0) && L0T % 2 == 0, "team geometry");
@@ -282,6 +290,7 @@ void rollout_team(const RolloutArgs a) {
         float* const xas = reinterpret_cast<float*>(base + off);          // (no policy)
         float* const Pb = reinterpret_cast<float*>(base + off);           // (policy) biases [pL][PHP] + params
         const char* const plw = base + off + (PHP > 0 ? pol_param_bytes(a.pL, PHP) : 0);   // policy weights
+        double* const pdraw = reinterpret_cast<double*>(const_cast<char*>(plw));  // (offset by pw_total below)
 
         for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
         for (int l = 0; l < NB; ++l)
@@ -312,8 +321,32 @@ void rollout_team(const RolloutArgs a) {
         //      kTeamNch steps at a time by the whole workgroup (one action per thread and pass, not per
         //      lane in the step loop): the caller's [H,K,A] array (np.random.uniform,
         //      controllers.py:53), Philox (rng_action), or the CEM sampler ----
+        // the policy's draws for kPolNch steps, by the whole workgroup: N(0,1) of the stochastic policy
+        // (rng_normal, f32, exact in the f64 slot) or the explore uniforms U (the caller's array,
+        // controllers.py:191, or Philox) -- none depends on the state, so no step waits for them
+        double* const pdr = pdraw + (PHP > 0 ? pw_total / 8 : 0);
+        auto fill_draws = [&](int h0) {
+            const int nh = min(kPolNch, a.H - h0), n = nh * 16 * A;
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const int hh = i / (16 * A), rem = i - hh * 16 * A, mm = rem / A, j = rem - mm * A;
+                const int64_t c = (int64_t)col * 16 + mm;
+                double v = 0.0;
+                if (c < a.K) {
+                    const int h = h0 + hh;
+                    const uint64_t gc = (uint64_t)(a.cand_offset + c);
+                    v = a.pol_mode == BCMPC_POLICY_STOCHASTIC
+                            ? (double)rng_normal(a.seed ^ 0x9E3779B97F4A7C15ull, gc, h, j)
+                        : a.actions ? a.actions[((int64_t)h * a.K + c) * A + j]
+                                    : rng_action(a.seed, gc, h, j, C[6 * 32 + j], C[7 * 32 + j]);
+                }
+                pdr[(hh * 16 + mm) * 16 + j] = v;
+            }
+        };
         auto fill_actions = [&](int h0) {
-            if constexpr (PHP > 0) return;                // (the policy makes the actions)
+            if constexpr (PHP > 0) {                      // (the policy makes the actions)
+                if (h0 % kPolNch == 0) fill_draws(h0);
+                return;
+            }
             const int nh = min(kTeamNch, a.H - h0), n = nh * 16 * A;
             for (int i = threadIdx.x; i < n; i += blockDim.x) {
                 const int hh = i / (16 * A), rem = i - hh * 16 * A, mm = rem / A, j = rem - mm * A;
@@ -409,6 +442,7 @@ void rollout_team(const RolloutArgs a) {
         gu64* const gb = (gu64*)a.team_buf;           // (global address space: never flat)
         bool dead = false;                                // a team exchange timed out: finish without waiting
         f4 ot[2];                                         // the step's summed output layer (rows 16 v + 4 q + r)
+        double gp = 0.0;                                  // (reward net) gamma**(h-1) for this step's tail
 
         stamp(9);
         for (int h = 0;; ++h) {
@@ -464,7 +498,7 @@ void rollout_team(const RolloutArgs a) {
                             if (r == ((S - 16) & 3)) o_s = ot[1][r];
                         const float nr = fmaf(o_s, fo, Bout[S]);                      // BiasAdd (f32)
                         const double rw = __dadd_rn(__dmul_rn((double)nr, a.std_reward), a.mean_reward);
-                        cost = __dadd_rn(cost, __dmul_rn(rw, a.gpow[h - 1]));
+                        cost = __dadd_rn(cost, __dmul_rn(rw, gp));
                     }
                 }
                 if (a.cost == BCMPC_COST_CHEETAH) {
@@ -482,9 +516,10 @@ void rollout_team(const RolloutArgs a) {
                         }
                 }
             }
+            if constexpr (RW) gp = h < a.H ? a.gpow[h] : 0.0;   // gamma**h for the next tail (requested early)
             stamp(0);
             if (h == a.H) break;
-            if (h > 0 && h % kTeamNch == 0) {
+            if (h > 0 && h % (PHP > 0 ? kPolNch : kTeamNch) == 0) {
                 fill_actions(h);
                 lds_barrier();                               // the chunk's action inputs (the previous chunk's
             }                                             // last reads were before the partials barrier)
@@ -571,7 +606,7 @@ void rollout_team(const RolloutArgs a) {
 #pragma unroll
                 for (int x = 1; x < NWV; ++x) o += parts[x * 64 + lane];    // fixed summation order
                 const float fo_p = a.pwinv[a.pL];
-                const uint64_t gcand = (uint64_t)(a.cand_offset + cand);
+                const double* const dr = pdr + ((h % kPolNch) * 16 + m) * 16;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int j = 16 + 4 * q + r - S;
@@ -579,14 +614,11 @@ void rollout_team(const RolloutArgs a) {
                     const float mean = o[r] * fo_p + pm[80 + 4 * q + r];       // dense bias (f32)
                     if (a.pol_mode == BCMPC_POLICY_STOCHASTIC) {
                         const float sd = expf(pm[64 + j]);
-                        pact[r] = (double)(mean + sd * rng_normal(a.seed ^ 0x9E3779B97F4A7C15ull, gcand, h, j));
+                        pact[r] = (double)(mean + sd * (float)dr[j]);
                     } else {
                         // (1 - explore) * mean in f32 (NumPy keeps the f32 dtype), + explore * U in f64
-                        const double uu = !valid ? 0.0
-                                          : a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
-                                                      : rng_action(a.seed, gcand, h, j, C[6 * 32 + j], C[7 * 32 + j]);
                         const float t1 = (float)(1.0 - a.explore) * mean;
-                        pact[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, uu));
+                        pact[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, dr[j]));
                     }
                     if (writer && a.act_out && h < a.act_out_steps && valid)   // action_paths (controllers.py:213)
                         __hip_atomic_store(&a.act_out[((int64_t)h * a.K + cand) * A + j], pact[r], __ATOMIC_RELAXED,
@@ -838,7 +870,7 @@ static TeamShape team_shape_of(int hidden_padded, int kind) {
         }
     }
     if (hidden_padded != 512) return {0, 0, 0};
-    return kind == 1 ? TeamShape{4, 2, 4} : TeamShape{8, 1, 8};   // reward: one head tile per wave
+    return kind == 1 ? TeamShape{4, 2, 4} : TeamShape{TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8};   // reward: delta / reward waves
 }
 
 int team_members(int hidden_padded, int kind) { return team_shape_of(hidden_padded, kind).members; }
@@ -905,8 +937,8 @@ hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStrea
         // the policy / reward variants: hidden 512, tanh, no LayerNorm (the run.sh recipe's nets)
         if (hidden_padded != 512 || a.act != BCMPC_ACT_TANH || a.ln) return hipErrorInvalidValue;
         if (kind == 1) return launch_team_t<512, 4, 2, 4, 0, 128, false>(a, st);
-        if (a.pL > 0) return launch_team_t<512, 8, 1, 8, 0, 128, true>(a, st);
-        return launch_team_t<512, 8, 1, 8, 0, 0, true>(a, st);
+        if (a.pL > 0) return launch_team_t<512, TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8, 0, 128, true>(a, st);
+        return launch_team_t<512, TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8, 0, 0, true>(a, st);
     }
     switch (hidden_padded) {
         case 64: return launch_team_ak<64, 2, 2, 1>(a, st);
