@@ -196,6 +196,115 @@ def dropin_parity_p50(K_global, H, hidden, L, act, ln, kernels, biases, ln_g, ln
     return out
 
 
+def synthetic_problem(wl):
+    """Synthetic inputs of a workload: glorot kernels, 0.1 N biases, synthetic stats /
+    state, the policy's normc kernels (random init: no checkpoints)."""
+    K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
+    reward = bool(wl.get("reward"))
+    if reward:   # dense, dense_1 (delta hidden), dense_2 (delta out), dense_3 (reward hidden), dense_4 (reward out)
+        shapes = [(S_DIM + A_DIM, hidden), (hidden, hidden), (hidden, S_DIM), (hidden, hidden), (hidden, 1)]
+    else:
+        dims = [S_DIM + A_DIM] + [hidden] * L + [S_DIM]
+        shapes = list(zip(dims[:-1], dims[1:]))
+    kernels, biases = [], []
+    for i, (fi, fo) in enumerate(shapes):
+        r = np.random.RandomState(1000 + i)
+        lim = np.sqrt(6.0 / (fi + fo))
+        kernels.append(r.uniform(-lim, lim, (fi, fo)).astype(np.float32))
+        biases.append((0.1 * r.standard_normal(fo)).astype(np.float32))
+    ln = bool(wl.get("ln"))
+    ln_g, ln_b = None, None
+    if ln:   # gamma ~ 1 + 0.1 N, beta ~ 0.1 N per hidden layer
+        rl = np.random.RandomState(99)
+        ln_g = [(1.0 + 0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
+        ln_b = [(0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
+    r7 = np.random.RandomState(7)
+    mean_obs = 0.1 * r7.standard_normal(S_DIM)
+    std_obs = np.abs(r7.standard_normal(S_DIM)) * 0.5 + 0.2
+    mean_d = 0.005 * r7.standard_normal(S_DIM)
+    std_d = 0.05 * (np.abs(r7.standard_normal(S_DIM)) + 0.2)
+    norm = [mean_obs, std_obs, np.zeros(A_DIM), np.full(A_DIM, 1 / np.sqrt(3)), np.full(1, 0.3), np.full(1, 1.2),
+            mean_obs, std_obs, mean_d, std_d]
+    state = mean_obs + 0.5 * std_obs * np.random.RandomState(11).standard_normal(S_DIM)
+    policy = wl.get("policy")
+    pol_arrays = None
+    if policy:
+        ph, pl = policy
+        rp = np.random.RandomState(2024)
+        pdims = [S_DIM] + [ph] * pl + [A_DIM]
+        pks, pbs = [], []
+        for i in range(len(pdims) - 1):
+            k = rp.standard_normal((pdims[i], pdims[i + 1]))
+            k *= (1.0 if i < pl else 0.5) / np.sqrt(np.square(k).sum(axis=0, keepdims=True))   # normc init
+            pks.append(k.astype(np.float32))
+            pbs.append((0.05 * rp.standard_normal(pdims[i + 1])).astype(np.float32))
+        pol_arrays = (pks, pbs, mean_obs.astype(np.float32), (std_obs + 0.05).astype(np.float32),
+                      np.full(A_DIM, -0.5, np.float32))
+    return dict(kernels=kernels, biases=biases, ln_g=ln_g, ln_b=ln_b, norm=norm, state=state, reward=reward, ln=ln,
+                model="reward" if reward else "delta", cost="reward" if reward else "cheetah",
+                gamma=float(wl.get("gamma", 1.0)), policy=policy, pol_arrays=pol_arrays)
+
+
+def make_engine(wl, prob, device, precision):
+    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
+    K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
+    if prob["policy"]:
+        ph, pl = prob["policy"]
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=device, policy_hidden=ph,
+                            policy_layers=pl, policy_mode=wl.get("policy_mode", "explore"), cost=prob["cost"],
+                            model=prob["model"], precision=precision)
+        eng.set_policy(PolicySpec(*prob["pol_arrays"]), wl["explore"], 1)
+    else:
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, prob["ln"], H, K, device=device, cost=prob["cost"],
+                            model=prob["model"], precision=precision)
+    eng.set_weights(MLPSpec(prob["kernels"], prob["biases"], act, prob["ln_g"], prob["ln_b"], model=prob["model"]),
+                    prob["norm"], 1)
+    if prob["reward"]:
+        eng.set_discount(prob["gamma"])
+    return eng
+
+
+SMALL_K = ("ppo_defaults", "runsh_recipe", "cfg1")    # the reference's own small configurations
+
+
+def small_k_lines(device, calls=200, warmup=20):
+    """get_action p50 (host state in, device-drawn actions, host result out) and the rollout kernel's
+    HIP-event time for the small-K workloads the reference actually runs (train_mpc_ppo.py:71,77: K=400;
+    run.sh:27-31; BASELINE cfg1), with the auto kernel (the team kernel, rollout_team.hip) and with the
+    slab kernel it replaced (BCMPC_TEAM=0), on this process's GPU."""
+    out = {}
+    for name in SMALL_K:
+        wl = WORKLOADS[name]
+        prob = synthetic_problem(wl)
+        row = {"K": wl["K"], "H": wl["H"]}
+        for tag, team in (("", None), ("slab_", "0")):
+            old = os.environ.get("BCMPC_TEAM")
+            if team is not None:
+                os.environ["BCMPC_TEAM"] = team
+            try:
+                eng = make_engine(wl, prob, device, "auto")
+            finally:
+                if team is not None:
+                    if old is None:
+                        os.environ.pop("BCMPC_TEAM", None)
+                    else:
+                        os.environ["BCMPC_TEAM"] = old
+            ts, ks = [], []
+            for i in range(warmup + calls):
+                t0 = time.perf_counter()
+                eng.get_action(prob["state"], None, seed=0x5EED + i)
+                if i >= warmup:
+                    ts.append(time.perf_counter() - t0)
+                    ks.append(eng.last_kernel_ms()[0])
+            row[tag + "kernel"] = eng.info()["kernel"]
+            row[tag + "p50_ms"] = float(np.percentile(ts, 50) * 1e3)
+            row[tag + "kernel_ms"] = float(np.mean(ks))
+            eng.close()
+        row["speedup_p50"] = row["slab_p50_ms"] / row["p50_ms"]
+        out[name] = row
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,6 +323,8 @@ def main():
                          "where it applies, else fp32")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-small-k", action="store_true",
+                    help="skip the small-K get_action lines (ppo_defaults, runsh_recipe, cfg1: team vs slab kernel)")
     args = ap.parse_args()
 
     import torch
@@ -247,65 +358,16 @@ def main():
         args.precision = "split" if (ok and (not wl.get("policy") or 448 < hidden <= top)) else "fp32"
     offset = rank * K
 
-    # synthetic inputs: glorot kernels, 0.1 N biases, synthetic stats/state
-    reward = bool(wl.get("reward"))
-    if reward:   # dense, dense_1 (delta hidden), dense_2 (delta out), dense_3 (reward hidden), dense_4 (reward out)
-        shapes = [(S_DIM + A_DIM, hidden), (hidden, hidden), (hidden, S_DIM), (hidden, hidden), (hidden, 1)]
-    else:
-        dims = [S_DIM + A_DIM] + [hidden] * L + [S_DIM]
-        shapes = list(zip(dims[:-1], dims[1:]))
-    kernels, biases = [], []
-    for i, (fi, fo) in enumerate(shapes):
-        r = np.random.RandomState(1000 + i)
-        lim = np.sqrt(6.0 / (fi + fo))
-        kernels.append(r.uniform(-lim, lim, (fi, fo)).astype(np.float32))
-        biases.append((0.1 * r.standard_normal(fo)).astype(np.float32))
-    ln = bool(wl.get("ln"))
-    ln_g, ln_b = None, None
-    if ln:   # gamma ~ 1 + 0.1 N, beta ~ 0.1 N per hidden layer
-        rl = np.random.RandomState(99)
-        ln_g = [(1.0 + 0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
-        ln_b = [(0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
-    r7 = np.random.RandomState(7)
-    mean_obs = 0.1 * r7.standard_normal(S_DIM)
-    std_obs = np.abs(r7.standard_normal(S_DIM)) * 0.5 + 0.2
-    mean_d = 0.005 * r7.standard_normal(S_DIM)
-    std_d = 0.05 * (np.abs(r7.standard_normal(S_DIM)) + 0.2)
-    norm = [mean_obs, std_obs, np.zeros(A_DIM), np.full(A_DIM, 1 / np.sqrt(3)), np.full(1, 0.3), np.full(1, 1.2),
-            mean_obs, std_obs, mean_d, std_d]
-    model = "reward" if reward else "delta"
-    cost = "reward" if reward else "cheetah"
-    gamma = float(wl.get("gamma", 1.0))
-    state = mean_obs + 0.5 * std_obs * np.random.RandomState(11).standard_normal(S_DIM)
-
-    policy = wl.get("policy")
-    pol_arrays = None
-    if policy:
-        ph, pl = policy
-        rp = np.random.RandomState(2024)
-        pdims = [S_DIM] + [ph] * pl + [A_DIM]
-        pks, pbs = [], []
-        for i in range(len(pdims) - 1):
-            k = rp.standard_normal((pdims[i], pdims[i + 1]))
-            k *= (1.0 if i < pl else 0.5) / np.sqrt(np.square(k).sum(axis=0, keepdims=True))   # normc init
-            pks.append(k.astype(np.float32))
-            pbs.append((0.05 * rp.standard_normal(pdims[i + 1])).astype(np.float32))
-        pol_arrays = (pks, pbs, mean_obs.astype(np.float32), (std_obs + 0.05).astype(np.float32),
-                      np.full(A_DIM, -0.5, np.float32))
-        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=local, policy_hidden=ph,
-                            policy_layers=pl, policy_mode=wl.get("policy_mode", "explore"), cost=cost, model=model,
-                            precision=args.precision)
-        eng.set_policy(PolicySpec(*pol_arrays), wl["explore"], 1)
-    else:
-        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, ln, H, K, device=local, cost=cost, model=model,
-                            precision=args.precision)
-    eng.set_weights(MLPSpec(kernels, biases, act, ln_g, ln_b, model=model), norm, 1)
-    if reward:
-        eng.set_discount(gamma)
+    prob = synthetic_problem(wl)
+    kernels, biases, ln_g, ln_b, norm, state = (prob[k] for k in ("kernels", "biases", "ln_g", "ln_b", "norm", "state"))
+    reward, ln, model, cost, gamma, policy, pol_arrays = (prob[k] for k in ("reward", "ln", "model", "cost", "gamma",
+                                                                            "policy", "pol_arrays"))
+    eng = make_engine(wl, prob, local, args.precision)
     info = eng.info()
     kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
                    "group8": "rollout_grp<NW=8>", "split1": "rollout_x3<NC=1>", "split2": "rollout_x3<NC=2>",
-                   "split4": "rollout_x3<NC=4>", "splitr": "rollout_rr (resident columns, LDS weight ring)"}.get(
+                   "split4": "rollout_x3<NC=4>", "splitr": "rollout_rr (resident columns, LDS weight ring)",
+                   "team": "rollout_team (weights in registers, one column per team of workgroups)"}.get(
         info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
     lib_comm = None
     if world > 1 and backend == "nccl" and not wl.get("cem") and args.actions == "device":
@@ -449,6 +511,7 @@ def main():
                      "flop_per_launch": K * H * fpcs,
                      "flop_per_cand_step": fpcs},
         "cpu_baseline": None,
+        "small_k": None,
     }
     prof = os.path.join(REPO, "profiles", "traffic_per_launch.json")
     if os.path.exists(prof):
@@ -470,6 +533,8 @@ def main():
             net += " (oracle policy in its deterministic explore branch: TF's sampler is not restatable)"
         out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, net,
                                            pol_arrays, wl.get("explore", 0.5), gamma, cem)
+    if rank == 0 and world == 1 and not args.no_small_k:
+        out["small_k"] = small_k_lines(local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if lib_comm is not None:
