@@ -74,6 +74,10 @@ constexpr int kPolNch = 8;               // steps of the policy's draws (f64) st
 #ifndef TEAM_RW_NWV
 #define TEAM_RW_NWV 4
 #endif
+// hidden 256 (train_mpc_ppo.py's 2x256 net): 4 waves x 4 tiles (512-register waves) or 8 waves x 2 tiles
+#ifndef TEAM_NWV256
+#define TEAM_NWV256 4
+#endif
 
 __device__ __forceinline__ f4 mm(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
 
@@ -864,7 +868,7 @@ static TeamShape team_shape_of(int hidden_padded, int kind) {
         switch (hidden_padded) {
             case 64: return {2, 2, 1};
             case 128: return {4, 2, 1};
-            case 256: return {4, 4, 1};
+            case 256: return {TEAM_NWV256, 16 / TEAM_NWV256, 1};
             case 512: return {4, 2, 4};
             default: return {0, 0, 0};
         }
@@ -943,7 +947,7 @@ hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStrea
     switch (hidden_padded) {
         case 64: return launch_team_ak<64, 2, 2, 1>(a, st);
         case 128: return launch_team_ak<128, 4, 2, 1>(a, st);
-        case 256: return launch_team_ak<256, 4, 4, 1>(a, st);
+        case 256: return launch_team_ak<256, TEAM_NWV256, 16 / TEAM_NWV256, 1>(a, st);
         case 512: return launch_team_ak<512, 4, 2, 4>(a, st);
         default: return hipErrorInvalidValue;
     }

@@ -84,12 +84,14 @@ typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")  
                                    layer-1 input in registers, weights streamed through an
                                    LDS ring, two workgroups per CU (rollout_rr.hip)          */
     BCMPC_KERNEL_TEAM = 9       /* BCMPC_PREC_SPLIT_F16, small K: 2-layer NNDynamicsModel (tanh
-                                   / relu, LayerNorm up to hidden 256), no policy / reward net:
-                                   one 16-candidate column per team of 1 (hidden <= 256) or 4
-                                   (hidden 512) workgroups, every weight resident in registers,
-                                   the output layer's partial sums exchanged between the team's
-                                   workgroups once per step (rollout_team.hip).  Needs the whole
-                                   grid resident: ceil(K/128)*8*members <= the device's CUs */
+                                   / relu, LayerNorm up to hidden 256), and at hidden 449..512
+                                   (tanh) with a fused policy (<= 2 x 128) and / or the
+                                   NNDynamicsRewardModel: one 16-candidate column per team of 1
+                                   (hidden <= 256), 4 (512) or 8 (reward net) workgroups, every
+                                   weight resident in registers, the output layer's partial sums
+                                   exchanged between the team's workgroups once per step
+                                   (rollout_team.hip).  Needs the whole grid resident:
+                                   ceil(K/128)*8*members <= the device's CUs                 */
 } bcmpc_kernel;
 
 typedef enum bcmpc_policy_mode {   /* MPCcontrollerPolicyNet.self_exp (controllers.py:201-208) */
