@@ -42,4 +42,47 @@ __device__ __forceinline__ void argmin_write(const ArgminArgs& a, Best best) {
     }
 }
 
+// The same record written by a whole block (best valid in thread 0; sc / si: >= 1 LDS slot): thread 0
+// applies the merge rule and writes index and cost, threads j < BCMPC_MAX_ACTION write first_action[j] in
+// parallel (the regenerated Philox / CEM actions are ~100 instructions each: one thread doing all A of
+// them was most of a small-K argmin launch), then thread 0 raises the done word.
+__device__ __forceinline__ void argmin_write_block(const ArgminArgs& a, Best best, double* sc, int64_t* si) {
+    bcmpc_result* out = a.out;
+    if (threadIdx.x == 0) {
+        bool write = true;
+        if (a.merge) {
+            const double prev = out->best_cost;
+            const Best ex{a.maximize ? -prev : prev, out->best_index - a.pos_base};
+            write = better(best, ex);
+        }
+        si[0] = write ? best.i : -1;
+        if (write) {
+            out->best_index = (a.merge || a.cem_mu ? a.pos_base : a.cand_offset) + best.i;
+            out->best_cost = a.maximize ? -best.c : best.c;
+        }
+    }
+    __syncthreads();
+    const int64_t bi = si[0];
+    const int j = threadIdx.x;
+    if (bi >= 0 && j < BCMPC_MAX_ACTION) {
+        double v = 0.0;
+        if (bi < a.K && j < a.A) {
+            const uint64_t g = (uint64_t)(a.cand_offset + bi);
+            const double lo = a.consts[6 * 32 + j], hi = a.consts[7 * 32 + j];
+            v = a.act_out ? a.act_out[bi * a.A + j]
+                : a.cem_mu ? cem_action(a.seed, g, 0, j, a.cem_iter, a.cem_mu[j], a.cem_sigma[j], lo, hi)
+                : a.actions ? a.actions[bi * a.A + j]
+                          : rng_action(a.seed, g, 0, j, lo, hi);
+        }
+        out->first_action[j] = v;
+    }
+    if (a.done) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 }  // namespace bcmpc

@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void argmin_final(const ArgminArgs a) {
         if (better(c, best)) best = c;
     }
     best = block_best(best, sc, si);
-    if (threadIdx.x == 0) argmin_write(a, best);
+    argmin_write_block(a, best, sc, si);
 }
 
 // argmin_partial + argmin_final in one block (nparts == 1)
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void argmin_single(const ArgminArgs a) {
         if (better(c, best)) best = c;
     }
     best = block_best(best, sc, si);
-    if (threadIdx.x == 0) argmin_write(a, best);
+    argmin_write_block(a, best, sc, si);
 }
 
 // ------------------------------------------------------------ launchers ----

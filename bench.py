@@ -301,6 +301,11 @@ def small_k_lines(device, calls=200, warmup=20):
             row[tag + "kernel_ms"] = float(np.mean(ks))
             eng.close()
         row["speedup_p50"] = row["slab_p50_ms"] / row["p50_ms"]
+        if not prob["policy"] and not prob["reward"]:
+            # the drop-in MPCcontroller.get_action in parity mode (NumPy's stream, controllers.py:53)
+            row["dropin_parity_p50_ms"] = dropin_parity_p50(
+                wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"], prob["ln"], prob["kernels"], prob["biases"],
+                prob["ln_g"], prob["ln_b"], prob["norm"], prob["state"], device, 100, 1)["p50_ms"]
         out[name] = row
     return out
 
