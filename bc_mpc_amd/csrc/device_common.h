@@ -38,6 +38,18 @@ __device__ __forceinline__ double rng_action(uint64_t seed, uint64_t g, int h, i
     return __dadd_rn(lo, __dmul_rn(__dsub_rn(hi, lo), u));   // low + (high-low)*u, no FMA
 }
 
+// Actions 2p and 2p + 1 of (g, h) from their ONE shared Philox block (words 0-1 and 2-3):
+// bit-identical to rng_action(.., 2p, ..) and rng_action(.., 2p + 1, ..) at half the VALU.
+__device__ __forceinline__ void rng_action_pair(uint64_t seed, uint64_t g, int h, int p, double lo0, double hi0,
+                                                double lo1, double hi1, double& a0, double& a1) {
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)h, (uint32_t)p};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const double u0 = ((double)(c[0] >> 5) * 67108864.0 + (double)(c[1] >> 6)) / 9007199254740992.0;
+    const double u1 = ((double)(c[2] >> 5) * 67108864.0 + (double)(c[3] >> 6)) / 9007199254740992.0;
+    a0 = __dadd_rn(lo0, __dmul_rn(__dsub_rn(hi0, lo0), u0));
+    a1 = __dadd_rn(lo1, __dmul_rn(__dsub_rn(hi1, lo1), u1));
+}
+
 // CEM sample (DESIGN.md "CEM"): z = Irwin-Hall(12) - 6 from three Philox blocks
 // (twelve 24-bit uniforms; their integer sum is exact, so z is exact in f64 and
 // restatable bit-for-bit), a = clip(mu + sd*z, lo, hi) with np.clip's NaN rule.

@@ -151,16 +151,31 @@ __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* _
         lds_barrier();                                                      // every wave's statistics published
     }
     if constexpr (LNK) {
-        float n = 0.f, mean = 0.f, m2 = 0.f;
+        float mean = 0.f, m2 = 0.f;
+        if (hidden == 16 * NTL * NWV) {
+            // every wave full (no padded rows): the merge weights nb / nn and n nb / nn are the same
+            // f32 quotients as below, folded at compile time -- a chain of 2 NWV dependent divisions
+            // per LayerNorm off the step's critical path (bit-identical)
 #pragma unroll
-        for (int v = 0; v < NWV; ++v) {
-            const float nb = (float)min(max(hidden - 16 * NTL * v, 0), 16 * NTL);
-            if (nb > 0.f) {
+            for (int v = 0; v < NWV; ++v) {
+                const float nb = (float)(16 * NTL), n = (float)(16 * NTL * v), nn = n + nb;
                 const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
-                const float nn = n + nb, d = st[0] - mean;
+                const float d = st[0] - mean;
                 mean = mean + d * (nb / nn);
                 m2 = m2 + st[1] + d * d * (n * nb / nn);
-                n = nn;
+            }
+        } else {
+            float n = 0.f;
+#pragma unroll
+            for (int v = 0; v < NWV; ++v) {
+                const float nb = (float)min(max(hidden - 16 * NTL * v, 0), 16 * NTL);
+                if (nb > 0.f) {
+                    const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
+                    const float nn = n + nb, d = st[0] - mean;
+                    mean = mean + d * (nb / nn);
+                    m2 = m2 + st[1] + d * d * (n * nb / nn);
+                    n = nn;
+                }
             }
         }
         const float eps = RELU ? 1e-12f : 1e-12f * 16777216.0f;        // tanh: activations carry x 2^12
@@ -351,7 +366,29 @@ void rollout_team(const RolloutArgs a) {
                 if (h0 % kPolNch == 0) fill_draws(h0);
                 return;
             }
-            const int nh = min(kTeamNch, a.H - h0), n = nh * 16 * A;
+            const int nh = min(kTeamNch, a.H - h0);
+            if (!a.cem_mu && !a.actions) {
+                // device Philox: one block feeds actions 2p and 2p + 1 (half the blocks per pass)
+                const int AP = (A + 1) >> 1, n = nh * 16 * AP;
+                for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                    const int hh = i / (16 * AP), rem = i - hh * 16 * AP, mm = rem / AP, p = rem - mm * AP;
+                    const int j0 = 2 * p, j1 = min(2 * p + 1, A - 1);
+                    const int64_t c = (int64_t)col * 16 + mm;
+                    float x0 = 0.f, x1 = 0.f;
+                    if (c < a.K) {
+                        double v0, v1;
+                        rng_action_pair(a.seed, (uint64_t)(a.cand_offset + c), h0 + hh, p, C[6 * 32 + j0],
+                                        C[7 * 32 + j0], C[6 * 32 + j1], C[7 * 32 + j1], v0, v1);
+                        x0 = (float)div_rn(__dsub_rn(v0, C[2 * 32 + j0]), C[3 * 32 + j0], C[9 * 32 + j0]);
+                        x1 = (float)div_rn(__dsub_rn(v1, C[2 * 32 + j1]), C[3 * 32 + j1], C[9 * 32 + j1]);
+                    }
+                    float* const dst = xas + (hh * 16 + mm) * 16;
+                    dst[j0] = x0;
+                    if (2 * p + 1 < A) dst[j1] = x1;
+                }
+                return;
+            }
+            const int n = nh * 16 * A;
             for (int i = threadIdx.x; i < n; i += blockDim.x) {
                 const int hh = i / (16 * A), rem = i - hh * 16 * A, mm = rem / A, j = rem - mm * A;
                 const int64_t c = (int64_t)col * 16 + mm;

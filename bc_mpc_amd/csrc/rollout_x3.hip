@@ -353,20 +353,36 @@ __device__ __forceinline__ void epi_colx(f4 (&acc)[TW][NC], const float (&f)[NC]
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         if constexpr (LNK) {
-            float n = 0.f, mean = 0.f, m2 = 0.f;
+            float mean = 0.f, m2 = 0.f;
+            if (hidden == 16 * TW * NW) {
+                // no padded rows: the merge weights nb / nn, n nb / nn below folded at compile time
+                // (bit-identical; 2 NW dependent divisions per column off the critical path)
 #pragma unroll
-            for (int g = 0; g < NW; ++g) {
-                const float nb = (float)min(max(hidden - 16 * TW * g, 0), 16 * TW);
-                if (nb > 0.f) {
+                for (int g = 0; g < NW; ++g) {
+                    const float nb = (float)(16 * TW), n = (float)(16 * TW * g), nn = n + nb;
                     const f2 st = *reinterpret_cast<const f2*>(xch + ((g * NC + c) * 16 + m) * 2);
-                    const float nn = n + nb, d = st[0] - mean;
+                    const float d = st[0] - mean;
                     mean = mean + d * (nb / nn);
                     m2 = m2 + st[1] + d * d * (n * nb / nn);
-                    n = nn;
+                }
+            } else {
+                float n = 0.f;
+#pragma unroll
+                for (int g = 0; g < NW; ++g) {
+                    const float nb = (float)min(max(hidden - 16 * TW * g, 0), 16 * TW);
+                    if (nb > 0.f) {
+                        const f2 st = *reinterpret_cast<const f2*>(xch + ((g * NC + c) * 16 + m) * 2);
+                        const float nn = n + nb, d = st[0] - mean;
+                        mean = mean + d * (nb / nn);
+                        m2 = m2 + st[1] + d * d * (n * nb / nn);
+                        n = nn;
+                    }
                 }
             }
             const float eps = RELU ? 1e-12f : 1e-12f * 16777216.0f;
-            const float rs = 1.0f / sqrtf(m2 / (float)hidden + eps);
+            // (the same quotient; a power-of-two width folds it to an exact multiply)
+            const float var = hidden == 16 * TW * NW ? m2 / (float)(16 * TW * NW) : m2 / (float)hidden;
+            const float rs = 1.0f / sqrtf(var + eps);
 #pragma unroll
             for (int j = 0; j < TW; ++j) {
                 const f4 gv = *reinterpret_cast<const f4*>(lg + 16 * (w * TW + j) + 4 * q);
@@ -557,6 +573,27 @@ void rollout_x3(const RolloutArgs a) {
     // cast to f32 (TF feed); threads [0, nt) of the block
     auto fill_actions = [&](int h0, int nt) __attribute__((always_inline)) {
         const int nhs = (a.H - h0 < X3_NCH) ? a.H - h0 : X3_NCH;
+        if (!a.cem_mu && !a.actions) {
+            // device Philox: one block feeds actions 2p and 2p + 1 (every thread's share of the
+            // chunk's blocks halves: this fill runs on every wave, on the step's critical path)
+            const int AP = (A + 1) >> 1, per = CB * AP;
+            for (int i = threadIdx.x; i < nhs * per; i += nt) {
+                const int hh = i / per, rem = i - hh * per, kl = rem / AP, p = rem - kl * AP;
+                const int j0 = 2 * p, j1 = min(2 * p + 1, A - 1);
+                float x0 = 0.f, x1 = 0.f;
+                if (cand0 + kl < a.K) {
+                    double v0, v1;
+                    rng_action_pair(a.seed, (uint64_t)(a.cand_offset + cand0 + kl), h0 + hh, p, C[6 * 32 + j0],
+                                    C[7 * 32 + j0], C[6 * 32 + j1], C[7 * 32 + j1], v0, v1);
+                    x0 = (float)div_rn(__dsub_rn(v0, C[2 * 32 + j0]), C[3 * 32 + j0], C[9 * 32 + j0]);
+                    x1 = (float)div_rn(__dsub_rn(v1, C[2 * 32 + j1]), C[3 * 32 + j1], C[9 * 32 + j1]);
+                }
+                float* const dst = xa + (hh * CB + kl) * A;
+                dst[j0] = x0;
+                if (2 * p + 1 < A) dst[j1] = x1;
+            }
+            return;
+        }
         const int per = CB * A;
         for (int i = threadIdx.x; i < nhs * per; i += nt) {
             const int hh = i / per, rem = i - hh * per, kl = rem / A, j = rem - kl * A;
