@@ -173,6 +173,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_double,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("bcmpc_stream", ctypes.c_void_p, [ctypes.c_void_p]),
+    ("bcmpc_engine_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     ("bcmpc_last_kernel_ms", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ("bcmpc_fit_create", ctypes.c_int, [ctypes.POINTER(FitConfig), ctypes.POINTER(ctypes.c_void_p)]),

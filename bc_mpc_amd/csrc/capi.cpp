@@ -190,7 +190,8 @@ struct bcmpc_engine {
     uint64_t version = 0;
     bool has_weights = false;
     hipEvent_t ev[3]{};
-    bool timed = false;
+    bool timed = false;                 // the last launch chain recorded ev[0..2]
+    bool timing = false;                // bcmpc_engine_set_timing: bracket launches with HIP events
     // fused policy (MPCcontrollerPolicyNet)
     int PHP = 0, TP = 0, PL = 0;
     float* d_pw = nullptr;  size_t pw_floats = 0;  size_t pw_off[BCMPC_MAX_LAYERS + 1]{};
@@ -934,6 +935,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.amin = m;
         a.amin_ticket = e->d_amin_ticket;
     }
+    record_events = record_events && e->timing;
+    e->timed = false;
     if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
     if (e->kernel == BCMPC_KERNEL_TEAM) {
         a.team_buf = e->d_team;
@@ -1054,7 +1057,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             return fail(BCMPC_ERR_HIP, err);
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[2], st));
-    e->timed = d_result != nullptr;
+    e->timed = record_events && d_result != nullptr;
     return BCMPC_OK;
 }
 
@@ -1488,7 +1491,7 @@ int bcmpc_cem_get_action(bcmpc_engine* e, const double* state, const bcmpc_cem* 
     HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(e->d_mu, mu, ha * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(e->d_sigma, sigma, ha * sizeof(double), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipEventRecord(e->ev[0], st));
+    if (e->timing) HIP_TRY(hipEventRecord(e->ev[0], st));
     for (int it = 0; it < p->iterations; ++it) {
         const CemLaunch cl{e->d_mu, e->d_sigma, it, it > 0, (int64_t)it * c.num_paths};
         rc = rollout_impl(e, e->d_state, 0, nullptr, seed, 0, e->d_costs, nullptr, e->d_result, st, &cl, false);
@@ -1498,9 +1501,11 @@ int bcmpc_cem_get_action(bcmpc_engine* e, const double* state, const bcmpc_cem* 
         rc = refit_impl(e, e->d_elite, e->d_count, seed, it, p->alpha, e->d_mu, e->d_sigma, st);
         if (rc != BCMPC_OK) return rc;
     }
-    HIP_TRY(hipEventRecord(e->ev[1], st));
-    HIP_TRY(hipEventRecord(e->ev[2], st));
-    e->timed = true;
+    if (e->timing) {
+        HIP_TRY(hipEventRecord(e->ev[1], st));
+        HIP_TRY(hipEventRecord(e->ev[2], st));
+    }
+    e->timed = e->timing;
     HIP_TRY(hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(mu, e->d_mu, ha * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(sigma, e->d_sigma, ha * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1546,8 +1551,15 @@ int bcmpc_engine_set_comm(bcmpc_engine* e, bcmpc_comm* comm) {
     return BCMPC_OK;
 }
 
+int bcmpc_engine_set_timing(bcmpc_engine* e, int32_t on) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    e->timing = on != 0;
+    return BCMPC_OK;
+}
+
 int bcmpc_last_kernel_ms(bcmpc_engine* e, float* rollout_ms, float* argmin_ms) {
     if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    if (!e->timed) return fail(BCMPC_ERR_ARG, "the last launch was not timed (bcmpc_engine_set_timing(eng, 1) first)");
     float r = 0.f, m = 0.f;
     HIP_TRY(hipEventSynchronize(e->ev[2]));
     HIP_TRY(hipEventElapsedTime(&r, e->ev[0], e->ev[1]));

@@ -289,13 +289,18 @@ def small_k_lines(device, calls=200, warmup=20):
                         os.environ.pop("BCMPC_TEAM", None)
                     else:
                         os.environ["BCMPC_TEAM"] = old
+            # p50 of the product path (no event markers: bcmpc_engine_set_timing off, its default), then
+            # the kernel's HIP-event time over a second, timed pass
             ts, ks = [], []
             for i in range(warmup + calls):
                 t0 = time.perf_counter()
                 eng.get_action(prob["state"], None, seed=0x5EED + i)
                 if i >= warmup:
                     ts.append(time.perf_counter() - t0)
-                    ks.append(eng.last_kernel_ms()[0])
+            eng.set_timing(True)
+            for i in range(max(20, calls // 4)):
+                eng.get_action(prob["state"], None, seed=0x5EED + i)
+                ks.append(eng.last_kernel_ms()[0])
             row[tag + "kernel"] = eng.info()["kernel"]
             row[tag + "p50_ms"] = float(np.percentile(ts, 50) * 1e3)
             row[tag + "kernel_ms"] = float(np.mean(ks))
@@ -368,6 +373,7 @@ def main():
     reward, ln, model, cost, gamma, policy, pol_arrays = (prob[k] for k in ("reward", "ln", "model", "cost", "gamma",
                                                                             "policy", "pol_arrays"))
     eng = make_engine(wl, prob, local, args.precision)
+    eng.set_timing(True)                               # the roofline's HIP events inside the timed region
     info = eng.info()
     kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
                    "group8": "rollout_grp<NW=8>", "split1": "rollout_x3<NC=1>", "split2": "rollout_x3<NC=2>",

@@ -385,9 +385,13 @@ int bcmpc_select_results(const bcmpc_result* recs, int32_t n, int32_t maximize, 
 /* Device stream the engine launches on (hipStream_t as void*). */
 void* bcmpc_stream(bcmpc_engine* eng);
 
+/* Kernel timing (off by default): with on != 0 every launch chain of this engine is bracketed
+ * by HIP event markers (~6 us per synchronous get_action at small K, measured), which
+ * bcmpc_last_kernel_ms reads.  Not part of the reference interface: a measurement switch. */
+int bcmpc_engine_set_timing(bcmpc_engine* eng, int32_t on);
 /* Timing of the last rollout kernel launched through bcmpc_get_action /
- * bcmpc_rollout_async, in milliseconds (HIP events on the launch stream);
- * requires the launch to have completed. */
+ * bcmpc_rollout_async / bcmpc_cem_get_action, in milliseconds (HIP events on the launch
+ * stream); requires timing on for that launch (else BCMPC_ERR_ARG) and waits for it. */
 int bcmpc_last_kernel_ms(bcmpc_engine* eng, float* rollout_ms, float* argmin_ms);
 
 /* Static shape facts for tests: padded hidden size and packed weight bytes. */

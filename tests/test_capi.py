@@ -121,6 +121,14 @@ def test_comm_arguments_validated_without_gpu():
     assert lib.bcmpc_select_results(None, 0, 0, None) == _lib.ERR_ARG
 
 
+def test_timing_switch_arguments_validated_without_gpu():
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    assert lib.bcmpc_engine_set_timing(None, 1) == _lib.ERR_ARG
+    r, m = ctypes.c_float(), ctypes.c_float()
+    assert lib.bcmpc_last_kernel_ms(None, ctypes.byref(r), ctypes.byref(m)) == _lib.ERR_ARG
+
+
 def test_integration_stub_structs_match_the_library():
     """The ctypes stub INTEGRATION.md shows a maintainer (no package import) declares the same struct
     layouts as include/bcmpc.h."""

@@ -12,7 +12,7 @@ from bc_mpc_amd.engine import MLPSpec, RolloutEngine
 from oracle import mpc_oracle as orc
 K, H, HID = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 w = orc.synthetic_weights(20, 6, HID, 2, "tanh", False); norm = orc.synthetic_normalization()
-e = RolloutEngine(20, 6, HID, 2, "tanh", False, H, K, kernel="splitr"); e.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+e = RolloutEngine(20, 6, HID, 2, "tanh", False, H, K, kernel="splitr"); e.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1); e.set_timing(True)
 st = orc.synthetic_state(norm); ks = []
 for i in range(25):
     e.get_action(st, None, seed=7); ks.append(e.last_kernel_ms()[0])

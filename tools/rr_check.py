@@ -23,6 +23,7 @@ res = {}
 for kern in ("splitr", "split4"):
     e = RolloutEngine(20, 6, HID, 2, "tanh", False, H, K, kernel=kern)
     e.set_weights(spec, norm, 1)
+    e.set_timing(True)
     r = e.get_action(state, None, seed=7, return_costs=True)
     ts, ks = [], []
     for _ in range(20):

@@ -9,6 +9,7 @@ w = orc.synthetic_weights(20, 6, HID, 2, "tanh", False)
 norm = orc.synthetic_normalization()
 e = RolloutEngine(20, 6, HID, 2, "tanh", False, H, K, kernel="splitr")
 e.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+e.set_timing(True)
 st = orc.synthetic_state(norm)
 for i in range(3):
     e.get_action(st, None, seed=7)
