@@ -164,6 +164,7 @@ struct bcmpc_engine {
     double* d_state = nullptr;
     double* d_actions = nullptr; size_t actions_cap = 0;
     double* h_stage = nullptr; size_t stage_cap = 0;   // pinned [H, K, A] staging (bcmpc_get_action_mt19937)
+    double* d_stage = nullptr;          // its device address (zero-copy reads of small draws)
     double* d_costs = nullptr;
     bcmpc_result* d_result = nullptr;
     double* d_amin_c = nullptr;         // argmin scratch: per-block best
@@ -1179,6 +1180,15 @@ static int mt_splits(int cj) {
     if (v && *v) return std::max(1, std::min(64, std::atoi(v)));
     return std::max(2, std::min(32, (4096 + cj - 1) / std::max(1, cj)));
 }
+// NumPy-stream draws of at most this many generator words (2 A H k_global; BCMPC_MT_ZC_WORDS overrides)
+// are drawn on the host straight into pinned memory that the rollout kernel reads over the bus
+// (zero copy): below it the device draw's serial generation chain (one workgroup, 227 words per
+// LDS-synchronised step) and its copies cost more than the host's ~0.45 ns per word
+static int64_t mt_zero_copy_words() {
+    const char* v = std::getenv("BCMPC_MT_ZC_WORDS");
+    return (v && *v) ? std::max<int64_t>(0, std::atoll(v)) : int64_t(1) << 18;
+}
+
 static bool mt_device_path() {
     const char* v = std::getenv("BCMPC_MT_PATH");
     return !(v && std::strcmp(v, "host") == 0);
@@ -1306,6 +1316,56 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         return fail(BCMPC_ERR_ARG, "this engine's candidates must lie inside [0, k_global)");
     if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
     HIP_TRY(hipSetDevice(c.device));
+    const int64_t draw_words = 2 * (int64_t)c.action_dim * c.horizon * k_global;
+    if (draw_words <= mt_zero_copy_words() && mt_device_path()) {
+        // small draw: the host generates the shard's rows of every step into pinned memory (the
+        // reference's own draw order), the kernel reads them in place; state in the kernel
+        // arguments, result into mapped memory, one spin -- no copy either way
+        const int64_t K = c.num_paths;
+        const int A = c.action_dim, H = c.horizon;
+        const size_t row = (size_t)K * A, n = (size_t)H * row;
+        if (n > e->stage_cap) {
+            if (e->h_stage) (void)hipHostFree(e->h_stage);
+            e->h_stage = nullptr;
+            e->d_stage = nullptr;
+            e->stage_cap = 0;
+            HIP_TRY(hipHostMalloc(&e->h_stage, n * sizeof(double), hipHostMallocDefault));
+            e->stage_cap = n;
+        }
+        if (!e->d_stage) HIP_TRY(hipHostGetDevicePointer((void**)&e->d_stage, e->h_stage, 0));
+        Mt19937 g;
+        std::memcpy(g.key, mt_key, sizeof(g.key));
+        g.pos = *mt_pos;
+        for (int h = 0; h < H; ++h)
+            mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_stage + h * row);
+        const bool lean = e->comm == nullptr;
+        if (!lean)
+            HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
+        e->want_done = lean && !costs_out;
+        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_stage, seed, cand_offset, e->d_costs, nullptr,
+                              lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
+                              lean ? state : nullptr);
+        const bool spin = e->want_done && rc == BCMPC_OK;
+        e->want_done = false;
+        if (rc == BCMPC_OK && !lean &&
+            hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            rc = fail(BCMPC_ERR_HIP, "result copy failed");
+        if (rc == BCMPC_OK && costs_out &&
+            hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * c.num_paths, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            rc = fail(BCMPC_ERR_HIP, "costs copy failed");
+        if (spin) {
+            if (const int wr = wait_done(e, e->seq)) return wr;
+        } else {
+            const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: the kernel reads h_stage)
+            if (rc != BCMPC_OK) return rc;
+            if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+        }
+        if (const int ts = team_status(e)) return ts;
+        std::memcpy(mt_key, g.key, sizeof(g.key));
+        *mt_pos = g.pos;
+        *out = lean ? *e->h_result_map : *e->h_result;
+        return BCMPC_OK;
+    }
     if (mt_device_path()) {
         // the draw on the device: state + (key, pos) up, draw, rollout, argmin, result + final state down,
         // one synchronisation.  NumPy's state is handed back only when the whole call succeeded.
@@ -1353,6 +1413,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     if (n > e->stage_cap) {                       // pinned staging: the generator writes, the DMA reads
         if (e->h_stage) (void)hipHostFree(e->h_stage);
         e->h_stage = nullptr;
+        e->d_stage = nullptr;
         e->stage_cap = 0;
         HIP_TRY(hipHostMalloc(&e->h_stage, n * sizeof(double), hipHostMallocDefault));
         e->stage_cap = n;
