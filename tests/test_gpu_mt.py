@@ -74,14 +74,17 @@ def test_device_draw_consecutive_calls_continue_the_stream():
     eng.close()
 
 
-@pytest.mark.parametrize("path", ["device", "host"])
-def test_get_action_numpy_stream_paths_agree(path, monkeypatch):
-    """bcmpc_get_action_mt19937 on either draw path: the same costs and argmin as the engine fed
+@pytest.mark.parametrize("path,K,H", [("device", 3000, 8), ("host", 3000, 8), ("zero_copy", 3000, 8),
+                                      ("device", 400, 7), ("zero_copy", 400, 7)])
+def test_get_action_numpy_stream_paths_agree(path, K, H, monkeypatch):
+    """bcmpc_get_action_mt19937 on every draw path (the device chain, the host split + upload, the host
+    draw read in place by the kernel for small draws): the same costs and argmin as the engine fed
     NumPy's own array, and NumPy's stream left where its one draw leaves it."""
     from bc_mpc_amd.engine import MLPSpec, RolloutEngine
     from oracle import mpc_oracle as orc
-    monkeypatch.setenv("BCMPC_MT_PATH", path)
-    S, A, H, K = 20, 6, 8, 3000
+    monkeypatch.setenv("BCMPC_MT_PATH", "host" if path == "host" else "device")
+    monkeypatch.setenv("BCMPC_MT_ZC_WORDS", str(1 << 30) if path == "zero_copy" else "0")
+    S, A = 20, 6
     w = orc.synthetic_weights(S, A, 128, 2, "tanh", False)
     norm = orc.synthetic_normalization(S, A)
     state = orc.synthetic_state(norm)
@@ -114,3 +117,31 @@ def test_failed_call_leaves_the_stream_untouched():
     st = np.random.get_state()
     eng.close()
     assert np.array_equal(st[1], st0[1]) and st[2] == st0[2]
+
+
+def test_zero_copy_shard_continues_the_stream(monkeypatch):
+    """A rank's shard of a small draw on the zero-copy path (k_global > K, offset > 0): its costs are
+    the engine's on NumPy's own rows, and the stream ends where the WHOLE draw leaves it."""
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    monkeypatch.setenv("BCMPC_MT_ZC_WORDS", str(1 << 30))
+    S, A, H, KG, K, off = 20, 6, 5, 1000, 333, 500
+    w = orc.synthetic_weights(S, A, 128, 2, "tanh", False)
+    norm = orc.synthetic_normalization(S, A)
+    state = orc.synthetic_state(norm)
+    low, high = -np.ones(A), np.ones(A)
+    eng = RolloutEngine(S, A, 128, 2, "tanh", False, H, K, device=0)
+    eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+    np.random.seed(77)
+    st0 = np.random.get_state()
+    actions = np.random.uniform(low, high, [H, KG, A])[:, off:off + K]
+    st_want = np.random.get_state()
+    ref = eng.get_action(state, np.ascontiguousarray(actions), cand_offset=off, return_costs=True)
+    for _ in range(2):                                     # twice: the staging buffer is reused
+        np.random.set_state(st0)
+        res = eng.get_action_numpy_stream(state, low, high, KG, cand_offset=off, return_costs=True)
+        st = np.random.get_state()
+        assert np.array_equal(res.costs, ref.costs) and res.best_index == ref.best_index
+        assert np.array_equal(res.first_action, ref.first_action)
+        assert np.array_equal(st[1], st_want[1]) and st[2] == st_want[2]
+    eng.close()
