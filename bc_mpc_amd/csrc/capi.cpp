@@ -164,7 +164,8 @@ struct bcmpc_engine {
     double* d_state = nullptr;
     double* d_actions = nullptr; size_t actions_cap = 0;
     double* h_stage = nullptr; size_t stage_cap = 0;   // pinned [H, K, A] staging (bcmpc_get_action_mt19937)
-    double* d_stage = nullptr;          // its device address (zero-copy reads of small draws)
+    double* h_zc = nullptr; size_t zc_cap = 0;   // small NumPy-stream draws: fine-grained (coherent) pinned rows
+    double* d_zc = nullptr;             // ... and their device address (the kernel reads them over the bus)
     double* d_costs = nullptr;
     bcmpc_result* d_result = nullptr;
     double* d_amin_c = nullptr;         // argmin scratch: per-block best
@@ -530,6 +531,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (e->h_team_err) (void)hipHostFree(e->h_team_err);
     if (e->h_done) (void)hipHostFree(e->h_done);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_zc) (void)hipHostFree(e->h_zc);
     if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1324,25 +1326,26 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         const int64_t K = c.num_paths;
         const int A = c.action_dim, H = c.horizon;
         const size_t row = (size_t)K * A, n = (size_t)H * row;
-        if (n > e->stage_cap) {
-            if (e->h_stage) (void)hipHostFree(e->h_stage);
-            e->h_stage = nullptr;
-            e->d_stage = nullptr;
-            e->stage_cap = 0;
-            HIP_TRY(hipHostMalloc(&e->h_stage, n * sizeof(double), hipHostMallocDefault));
-            e->stage_cap = n;
+        if (n > e->zc_cap) {
+            // fine-grained host memory: no GPU cache keeps an earlier call's rows (the rows change every call)
+            if (e->h_zc) (void)hipHostFree(e->h_zc);
+            e->h_zc = nullptr;
+            e->d_zc = nullptr;
+            e->zc_cap = 0;
+            HIP_TRY(hipHostMalloc(&e->h_zc, n * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostGetDevicePointer((void**)&e->d_zc, e->h_zc, 0));
+            e->zc_cap = n;
         }
-        if (!e->d_stage) HIP_TRY(hipHostGetDevicePointer((void**)&e->d_stage, e->h_stage, 0));
         Mt19937 g;
         std::memcpy(g.key, mt_key, sizeof(g.key));
         g.pos = *mt_pos;
         for (int h = 0; h < H; ++h)
-            mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_stage + h * row);
+            mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_zc + h * row);
         const bool lean = e->comm == nullptr;
         if (!lean)
             HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
         e->want_done = lean && !costs_out;
-        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_stage, seed, cand_offset, e->d_costs, nullptr,
+        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_zc, seed, cand_offset, e->d_costs, nullptr,
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
         const bool spin = e->want_done && rc == BCMPC_OK;
@@ -1356,7 +1359,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         if (spin) {
             if (const int wr = wait_done(e, e->seq)) return wr;
         } else {
-            const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: the kernel reads h_stage)
+            const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: the kernel reads h_zc)
             if (rc != BCMPC_OK) return rc;
             if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
         }
@@ -1413,7 +1416,6 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     if (n > e->stage_cap) {                       // pinned staging: the generator writes, the DMA reads
         if (e->h_stage) (void)hipHostFree(e->h_stage);
         e->h_stage = nullptr;
-        e->d_stage = nullptr;
         e->stage_cap = 0;
         HIP_TRY(hipHostMalloc(&e->h_stage, n * sizeof(double), hipHostMallocDefault));
         e->stage_cap = n;

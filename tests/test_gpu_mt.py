@@ -133,11 +133,11 @@ def test_zero_copy_shard_continues_the_stream(monkeypatch):
     eng = RolloutEngine(S, A, 128, 2, "tanh", False, H, K, device=0)
     eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
     np.random.seed(77)
-    st0 = np.random.get_state()
-    actions = np.random.uniform(low, high, [H, KG, A])[:, off:off + K]
-    st_want = np.random.get_state()
-    ref = eng.get_action(state, np.ascontiguousarray(actions), cand_offset=off, return_costs=True)
-    for _ in range(2):                                     # twice: the staging buffer is reused
+    for _ in range(4):           # consecutive control steps: new rows in the same pinned buffer every call
+        st0 = np.random.get_state()
+        actions = np.random.uniform(low, high, [H, KG, A])[:, off:off + K]
+        st_want = np.random.get_state()
+        ref = eng.get_action(state, np.ascontiguousarray(actions), cand_offset=off, return_costs=True)
         np.random.set_state(st0)
         res = eng.get_action_numpy_stream(state, low, high, KG, cand_offset=off, return_costs=True)
         st = np.random.get_state()
