@@ -52,7 +52,8 @@ namespace bcmpc {
 // TEAM_STAMP 1 (timing diagnostic, tools/team_variants.sh builds only): per-phase s_memtime totals of
 // every wave into a.stamps ([blocks][NWV][10]: 0 tail, 1 action fill, 2 layer-0 input, 3 layer 0,
 // 4 slab barrier, 5 layer-1 MFMAs, 6 layer-1 epilogue, 7 output + partials barrier, 8 member sums /
-// exchange, 9 prologue)
+// exchange, 9 prologue); TEAM_STAMP 2: the prologue split instead (0 parameters, 1 first fill, 2 weight
+// issue, 3 state set-up)
 #ifndef TEAM_STAMP
 #define TEAM_STAMP 0
 #endif
@@ -281,8 +282,16 @@ void rollout_team(const RolloutArgs a) {
     const int64_t ncol = (a.K + 15) / 16;
     uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp_ = TEAM_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    // TEAM_STAMP 2: the prologue's phases instead (slots 0 params, 1 first fill, 2 weight issue, 3 state)
+    auto pstamp = [&](int k) __attribute__((always_inline)) {
+        if constexpr (TEAM_STAMP == 2) {
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();
+            ph_[k] += t_ - tp_;
+            tp_ = t_;
+        }
+    };
     auto stamp = [&](int k) __attribute__((always_inline)) {
-        if constexpr (TEAM_STAMP) {
+        if constexpr (TEAM_STAMP == 1) {
             const uint64_t t_ = __builtin_amdgcn_s_memtime();
             ph_[k] += t_ - tp_;
             tp_ = t_;
@@ -336,6 +345,7 @@ void rollout_team(const RolloutArgs a) {
             for (int i = threadIdx.x; i < kTeamNch * 16 * 16; i += blockDim.x)
                 if ((i & 15) >= A) xas[i] = 0.f;            // action slots past A stay zero (fill writes j < A)
         __syncthreads();                                  // parameters in LDS
+        pstamp(0);
         // ---- actions, normalised (dynamics.py:110) and cast to f32 (the TF feed), staged in LDS for
         //      kTeamNch steps at a time by the whole workgroup (one action per thread and pass, not per
         //      lane in the step loop): the caller's [H,K,A] array (np.random.uniform,
@@ -408,6 +418,7 @@ void rollout_team(const RolloutArgs a) {
 
         fill_actions(0);                                  // (before the weight loads: its global loads
         lds_barrier();                                    //  would otherwise wait behind them)
+        pstamp(1);
         // ---- every weight fragment this wave uses, once (issued after the parameter barrier so the
         //      loads stay in flight through the first step's LDS barriers) (capi.cpp: layer 0 packed with TWp = L0T,
         //      layer 1 with TWp = TPW, the output layer [0][k-step][tile]) ----
@@ -460,6 +471,7 @@ void rollout_team(const RolloutArgs a) {
                 }
         }
 
+        pstamp(2);
         // ---- per-candidate state: lane (q, m) holds dims 16 v + 4 q + r (v = 0, 1) of candidate m,
         //      in every wave of every member ----
         const int64_t cand = (int64_t)col * 16 + m;
@@ -485,6 +497,7 @@ void rollout_team(const RolloutArgs a) {
         f4 ot[2];                                         // the step's summed output layer (rows 16 v + 4 q + r)
         double gp = 0.0;                                  // (reward net) gamma**(h-1) for this step's tail
 
+        pstamp(3);
         stamp(9);
         for (int h = 0;; ++h) {
             if constexpr (RW) {
