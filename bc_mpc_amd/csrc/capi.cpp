@@ -1172,10 +1172,16 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
 // slices per jump polynomial (BCMPC_MT_SPLITS): chunks trade jump work (one 624 x 19937 GF(2)
 // correlation each, ~0.35 us of the whole chip, VALU-bound) against serial generation (~0.9 words
 // per ns per workgroup).  cfg3 (15.7M words): 2^16 words -> 240 chunks x 17 slices, draw ~0.18 ms
-// (tools/mt_device_sweep.py, profiles/r02_mt_device_sweep.txt).
-static int64_t mt_chunk_words() {
+// (tools/mt_device_sweep.py, profiles/r02_mt_device_sweep.txt).  Smaller draws want smaller chunks (the
+// serial generation of one chunk is the draw's critical path once the chip has spare workgroups): ~60
+// chunks per draw, as a power of two in [2^14, 2^16] words -- cfg2 (983k words) 0.366 -> 0.322 ms and a
+// K = 1000 x 15 draw 0.262 -> 0.223 ms per drop-in get_action at 2^14 (profiles/r02c_mt_chunk_sweep.txt).
+static int64_t mt_chunk_words(int64_t shard_words) {
     const char* v = std::getenv("BCMPC_MT_CHUNK_WORDS");
-    return (v && *v) ? std::max<int64_t>(2, std::atoll(v)) & ~int64_t(1) : int64_t(1) << 16;
+    if (v && *v) return std::max<int64_t>(2, std::atoll(v)) & ~int64_t(1);
+    int64_t w = int64_t(1) << 14;
+    while (w < (int64_t(1) << 16) && 2 * w <= shard_words / 60) w *= 2;
+    return w;
 }
 static int mt_splits(int cj) {
     const char* v = std::getenv("BCMPC_MT_SPLITS");
@@ -1184,11 +1190,13 @@ static int mt_splits(int cj) {
 }
 // NumPy-stream draws of at most this many generator words (2 A H k_global; BCMPC_MT_ZC_WORDS overrides)
 // are drawn on the host straight into pinned memory that the rollout kernel reads over the bus
-// (zero copy): below it the device draw's serial generation chain (one workgroup, 227 words per
-// LDS-synchronised step) and its copies cost more than the host's ~0.45 ns per word
+// (zero copy): there the device draw is a few chunks whose serial generation chains (one workgroup,
+// 227 words per LDS-synchronised step) and copies cost more than the host's ~0.5 ns per word.  2^16:
+// the reference's K = 400 steps (33.6k words at H = 7); a K = 1000 x 15 draw (180k) is faster on the
+// device with 2^14-word chunks (0.223 vs 0.250 ms per drop-in get_action)
 static int64_t mt_zero_copy_words() {
     const char* v = std::getenv("BCMPC_MT_ZC_WORDS");
-    return (v && *v) ? std::max<int64_t>(0, std::atoll(v)) : int64_t(1) << 18;
+    return (v && *v) ? std::max<int64_t>(0, std::atoll(v)) : int64_t(1) << 16;
 }
 
 static bool mt_device_path() {
@@ -1198,7 +1206,7 @@ static bool mt_device_path() {
 
 // The draw's chunks for this engine's shard of [H, k_global, A]: the shard's rows of step h are the
 // draw words [2A (h kg + off), 2A (h kg + off + K)) (one run; all steps merge into one when the shard
-// is the whole draw), each run cut into pieces of <= mt_chunk_words() words; the chunk that draws
+// is the whole draw), each run cut into pieces of <= mt_chunk_words(..) words; the chunk that draws
 // the draw's last word also leaves NumPy's final state, else one extra chunk draws that word alone.
 static int mt_plan(bcmpc_engine* e, int64_t kg, int64_t off) {
     if (e->mt_kg == kg && e->mt_off == off) return BCMPC_OK;
@@ -1209,7 +1217,7 @@ static int mt_plan(bcmpc_engine* e, int64_t kg, int64_t off) {
     if (off == 0 && K == kg) runs.push_back({0, N, 0});
     else
         for (int64_t h = 0; h < H; ++h) runs.push_back({2 * A * (h * kg + off), 2 * A * K, h * K * A});
-    const int64_t target = mt_chunk_words();
+    const int64_t target = mt_chunk_words(2 * A * H * K);
     std::vector<MtChunk> ch;
     bool has_final = false;
     for (const Run& r : runs) {
