@@ -258,13 +258,12 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     if (c.precision != BCMPC_PREC_FP32 && c.precision != BCMPC_PREC_SPLIT_F16)
         return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32 or SPLIT_F16");
     const bool split = c.precision == BCMPC_PREC_SPLIT_F16;
+    // relu / LayerNorm hidden layers (per-column scales or statistics exchanged across the workgroup)
+    // on the split slab kernels: the plain delta net without a policy, hidden <= 512; beyond that only
+    // the small-K team kernel takes them (checked once the kernel is chosen, below)
+    const bool split_needs_team = split && (c.activation != BCMPC_ACT_TANH || c.layer_norm) &&
+                                  (reward || c.policy_hidden > 0 || padded_hidden(c.hidden) > 512);
     if (split) {
-        // relu / LayerNorm hidden layers (per-column scales or statistics exchanged across the
-        // workgroup): the plain delta net without a policy, hidden <= 512
-        if ((c.activation != BCMPC_ACT_TANH || c.layer_norm) &&
-            (reward || c.policy_hidden > 0 || padded_hidden(c.hidden) > 512))
-            return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports relu / LayerNorm nets only for the "
-                                               "delta net without a policy, hidden <= 512 (use FP32)");
         if (reward && c.state_dim < 16)
             return fail(BCMPC_ERR_UNSUPPORTED, "split reward engines need state_dim >= 16 (reward row in tile 1)");
         if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_TEAM))
@@ -336,16 +335,21 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device);
     const int tkind = reward ? 2 : e->PL > 0 ? 1 : 0;
     const int tmem = team_members(e->HP, tkind);
+    // (a LayerNorm over a layer split across members: only the reward net's heads, whose statistics
+    //  ride along with the output partials in the exchange -- rows 24..27, so S + 1 <= 24)
     const bool team_shape = split && c.n_layers == 2 && e->HP <= 512 && c.state_dim + c.action_dim <= 32 &&
-                            c.action_dim <= 15 && c.horizon <= 1022 && tmem > 0 && !(c.layer_norm && tmem > 1) &&
-                            (tkind == 0 || (c.activation == BCMPC_ACT_TANH && !c.layer_norm && c.state_dim >= 16 &&
-                                            e->PL <= 2));
+                            c.action_dim <= 15 && c.horizon <= 1022 && tmem > 0 &&
+                            !(c.layer_norm && tmem > 1 && tkind != 2) &&
+                            (tkind == 0 || (c.state_dim >= 16 && e->PL <= 2 &&
+                                            (tmem == 1 || c.activation == BCMPC_ACT_TANH))) &&
+                            !(tkind == 2 && c.layer_norm && (c.state_dim > 23 || !team_rw_ln_built()));
     const bool team_fits = team_shape && c.num_paths > 0 && team_blocks(c.num_paths, e->HP, tkind) <= (int64_t)ncu;
     bool use_team = c.kernel == BCMPC_KERNEL_TEAM;
     if (use_team && !team_fits) {
         delete e;
         return fail(BCMPC_ERR_UNSUPPORTED, "team kernel: 2-layer net, hidden <= 512 (LayerNorm: <= 256; with a "
-                                           "policy or the reward net: 512, tanh, no LayerNorm), S + A <= 32, "
+                                           "policy: hidden <= 256, or 512 tanh without LayerNorm; the reward "
+                                           "net: 512, tanh, LayerNorm with S <= 23), S + A <= 32, "
                                            "ceil(K / 128) * 8 * members workgroups <= the device's CUs");
     }
     if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr) {
@@ -393,6 +397,11 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->nw = nwx;
         kern = e->kernel;
     }
+    if (split_needs_team && !use_team) {
+        delete e;
+        return fail(BCMPC_ERR_UNSUPPORTED, "SPLIT_F16 precision supports relu / LayerNorm nets with a policy, the "
+                                           "reward net or hidden > 512 only on the small-K team kernel (use FP32)");
+    }
     if (kern < BCMPC_KERNEL_SOLO || kern > BCMPC_KERNEL_TEAM) { delete e; return fail(BCMPC_ERR_ARG, "unknown kernel"); }
     const int nw = split ? e->nw : kern_waves(kern);
     if (!split && kern != BCMPC_KERNEL_SOLO &&
@@ -421,15 +430,17 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->w_off[3] = off; off += (size_t)T * P * 512;
         e->w_off[4] = off; off += (size_t)P * 512;
         e->nwl = 5;
-        // biases: trunk | delta head | reward head | out (rows 0..S-1 dense_2, row S dense_4)
+        // biases: trunk | delta head | reward head | out (rows 0..S-1 dense_2, row S dense_4) | (team kernel,
+        // LayerNorm heads) the centring table [8 members][32 rows]
         e->b_off[0] = 0; e->b_off[1] = e->HP; e->b_off[2] = 2 * e->HP; e->b_off[3] = 3 * e->HP;
-        boff = 3 * e->HP + 32;
+        e->b_off[4] = 3 * e->HP + 32;
+        boff = 3 * e->HP + 32 + 8 * 32;
     } else if (reward) {
         // [S+A -> h] trunk, [h -> 2h] both heads' hidden layers, [2h -> S+1] block-diagonal output
         e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;
         e->w_off[1] = off; off += (size_t)2 * T * T * 64 * 4;
         e->w_off[2] = off; off += (size_t)2 * 2 * T * 64 * 4;
-        e->b_off[0] = 0; e->b_off[1] = e->HP; e->b_off[2] = 3 * e->HP; boff = 3 * e->HP + 32;
+        e->b_off[0] = 0; e->b_off[1] = e->HP; e->b_off[2] = 3 * e->HP; boff = 3 * e->HP + 32 + 8 * 32;   // (same size as the split layout)
     } else if (kern == BCMPC_KERNEL_SPLITR) {
         // one slot image (pack_rr_image) streamed by every workgroup; layers 1, 2 are inside it
         off = rr_image_bytes(e->HP) / sizeof(float);
@@ -561,32 +572,76 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
     HIP_TRY(hipSetDevice(c.device));
     std::vector<float> hw(e->w_floats, 0.f);
     const int tb = e->pack_tb;
-    std::vector<float> hb(rw ? 3 * (size_t)HP + 32 : (size_t)L * HP + 32, 0.f);
+    std::vector<float> hb(rw ? 3 * (size_t)HP + 32 + 8 * 32 : (size_t)L * HP + 32, 0.f);
     std::vector<float> hln(2 * (size_t)NLN * HP, 0.f);
     if (e->split && rw) {
         _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
         const int P = T / 2;
+        const bool ln = c.layer_norm != 0;                // (team kernel only: bcmpc_create)
         const float s0 = x3_scale(w->kernels[0], (size_t)(S + A) * h);
         pack_x3_layer(w->kernels[0], S + A, h, 1, T, tb, s0, hh + 2 * e->w_off[0]);
         e->winv[0] = 1.0f / s0;
+        // the heads' input: the trunk's tanh x 2^12, or its LayerNorm output x hsc[0] (|LN(x)_i| <=
+        // sqrt(h) |gamma_i| + |beta_i|, the power of two that keeps it below 2^12)
+        float hin = 4096.0f;
+        if (ln) {
+            float gm = 0.f, bm = 0.f;
+            for (int i = 0; i < h; ++i) {
+                gm = std::max(gm, std::fabs(w->ln_gamma[0][i]));
+                bm = std::max(bm, std::fabs(w->ln_beta[0][i]));
+            }
+            const float bound = std::sqrt((float)h) * gm + bm;
+            int ex = 0;
+            if (bound > 0.f && std::isfinite(bound)) (void)std::frexp(bound, &ex);
+            hin = std::ldexp(1.0f, std::max(-100, std::min(100, 12 - ex)));
+            e->hsc[0] = hin;
+        }
         const float sd = x3_scale(w->kernels[1], (size_t)h * h), sr = x3_scale(w->kernels[3], (size_t)h * h);
         const int tbh = e->kernel == BCMPC_KERNEL_TEAM ? team_layer1_tiles(HP, e->team_kind) : tb;   // (team: head tiles per wave)
         pack_x3_layer(w->kernels[1], h, h, P, T, tbh, sd, hh + 2 * e->w_off[1]);
         pack_x3_layer(w->kernels[3], h, h, P, T, tbh, sr, hh + 2 * e->w_off[3]);
-        e->winv[1] = (1.0f / sd) / 4096.0f;
-        e->winv[3] = (1.0f / sr) / 4096.0f;
+        e->winv[1] = (1.0f / sd) / hin;
+        e->winv[3] = (1.0f / sr) / hin;
+        // LayerNorm heads (rollout_team.hip HLN): out = rsqrt(var + eps) (dense_2 diag(gamma))^T (h - mean)
+        // + (dense_2^T beta + b): gamma folded into the output kernels, beta into their biases
+        std::vector<float> w2((size_t)h * S), w4((size_t)h);
+        for (int k = 0; k < h; ++k) {
+            const float gd = ln ? w->ln_gamma[1][k] : 1.0f, gr = ln ? w->ln_gamma[2][k] : 1.0f;
+            for (int n = 0; n < S; ++n) w2[(size_t)k * S + n] = w->kernels[2][(size_t)k * S + n] * gd;
+            w4[k] = w->kernels[4][k] * gr;
+        }
         // both output kernels feed one accumulator: one scale (the smaller of the two)
-        const float so = std::min(x3_scale(w->kernels[2], (size_t)h * S), x3_scale(w->kernels[4], (size_t)h));
-        pack_x3_layer(w->kernels[2], h, S, P, 2, 2, so, hh + 2 * e->w_off[2]);
+        const float so = std::min(x3_scale(w2.data(), (size_t)h * S), x3_scale(w4.data(), (size_t)h));
+        pack_x3_layer(w2.data(), h, S, P, 2, 2, so, hh + 2 * e->w_off[2]);
         std::vector<float> wr((size_t)h * 16, 0.f);      // dense_4 at row S of the second output tile
-        for (int k = 0; k < h; ++k) wr[(size_t)k * 16 + (S - 16)] = w->kernels[4][k];
+        for (int k = 0; k < h; ++k) wr[(size_t)k * 16 + (S - 16)] = w4[k];
         pack_x3_layer(wr.data(), h, 16, P, 1, 1, so, hh + 2 * e->w_off[4]);
-        e->winv[2] = e->winv[4] = (1.0f / so) / 4096.0f;
+        // (LN: the heads' normalised output carries no 2^12 -- rsqrt of the x 2^12 variance undoes it)
+        e->winv[2] = e->winv[4] = ln ? 1.0f / so : (1.0f / so) / 4096.0f;
         std::memcpy(hb.data() + e->b_off[0], w->biases[0], sizeof(float) * h);
         std::memcpy(hb.data() + e->b_off[1], w->biases[1], sizeof(float) * h);
         std::memcpy(hb.data() + e->b_off[2], w->biases[3], sizeof(float) * h);
         std::memcpy(hb.data() + e->b_off[3], w->biases[2], sizeof(float) * S);
         hb[e->b_off[3] + S] = w->biases[4][0];
+        if (ln) {
+            for (int n = 0; n <= S; ++n) {                // b + kernel^T beta (f64 sum, one rounding)
+                double acc = n < S ? (double)w->biases[2][n] : (double)w->biases[4][0];
+                for (int k = 0; k < h; ++k)
+                    acc += n < S ? (double)w->kernels[2][(size_t)k * S + n] * (double)w->ln_beta[1][k]
+                                 : (double)w->kernels[4][k] * (double)w->ln_beta[2][k];
+                hb[e->b_off[3] + n] = (float)acc;
+            }
+            // centring table: member t's rows [64 t, 64 t + 64) of the folded, scaled output kernels
+            for (int t = 0; t < 8; ++t)
+                for (int n = 0; n <= S; ++n) {
+                    double acc = 0.0;
+                    for (int k = 64 * t; k < std::min(h, 64 * t + 64); ++k)
+                        acc += n < S ? (double)w2[(size_t)k * S + n] * so : (double)w4[k] * so;
+                    hb[e->b_off[4] + (size_t)t * 32 + n] = (float)acc;
+                }
+            std::memcpy(hln.data(), w->ln_gamma[0], sizeof(float) * h);               // trunk gamma
+            std::memcpy(hln.data() + (size_t)3 * HP, w->ln_beta[0], sizeof(float) * h);   // trunk beta
+        }
         e->mean_reward = w->mean_reward[0];
         e->std_reward = w->std_reward[0];
     } else if (e->kernel == BCMPC_KERNEL_SPLITR) {
@@ -862,6 +917,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     if (e->reward) {   // trunk LN, then the two heads' LN params side by side (2*HP)
         a.lng[0] = e->d_ln;               a.lng[1] = e->d_ln + e->HP;
         a.lnb[0] = e->d_ln + 3 * e->HP;   a.lnb[1] = e->d_ln + 4 * e->HP;
+        if (e->split) a.head_rs = e->d_b + e->b_off[4];
         a.model = BCMPC_MODEL_REWARD;
         a.mean_reward = e->mean_reward;
         a.std_reward = e->std_reward;

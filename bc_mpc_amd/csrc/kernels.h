@@ -93,6 +93,9 @@ struct RolloutArgs {
     unsigned long long* team_buf;
     unsigned* team_ctl;
     unsigned* team_err;
+    // (team kernel, the reward net with LayerNorm heads) [8 members][32 rows]: sum over member t's head
+    // rows of the gamma-folded, scaled output weights (the centring correction, rollout_team.hip)
+    const float* head_rs;
 };
 
 struct SelectArgs {                          // top-E of (cost, index) pairs, NaN last, ties -> lower index
@@ -177,6 +180,7 @@ int team_layer0_tiles(int hidden_padded, int kind);     // layer-0 tiles per wav
 int team_layer1_tiles(int hidden_padded, int kind);     // hidden-layer (head) tiles per wave
 int64_t team_blocks(int64_t K, int hidden_padded, int kind);
 size_t team_buf_bytes(int64_t K, int hidden_padded, int kind);
+bool team_rw_ln_built();                                // the reward net's LayerNorm heads are in this build
 hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 hipError_t launch_select(const SelectArgs& a, hipStream_t st);

@@ -239,13 +239,13 @@ __device__ __forceinline__ void split_tiles(const f4 (&v)[NTL], int odd, h8 (&xh
 
 // LDS: consts | biases [2 or 3][HP] + 32 | LN gamma [2][HP], beta [2][HP] | slab [P][hi|lo][64] f4 |
 // column exchange [2 layers][NWV][16][2] | output partials [NWV][2][64] f4 | members' partials [T][2][64] f4 |
-// action inputs [kTeamNch][16][16] (no policy) | policy biases + params, policy hidden->hidden weights
+// (policy, T == 1) the policy's output partials [NWV][64] f4 | action inputs [kTeamNch][16][16] (no policy) | policy biases + params, policy hidden->hidden weights
 // (PHP > 0; its first and output layers live in registers)
 __host__ __device__ constexpr int team_lds_bytes(int HP, int NWV, int T, int AK, bool RW = false, int PHP = 0,
                                                  int PL = 0, int pw_bytes = 0) {
     return param_bytes(RW ? 3 : 2, HP) + ((AK & 2) ? 4 * HP * 4 : 0) + (HP / 32) * 2048 + (AK ? 2 * NWV * 16 * 2 * 4 : 0) +
-           NWV * 2048 + (T > 1 ? T * 2048 : 0) + (PHP > 0 ? pol_param_bytes(PL, PHP) + pw_bytes + kPolNch * 16 * 16 * 8
-                                                          : kTeamNch * 16 * 16 * 4);
+           NWV * 2048 + (T > 1 ? T * 2048 : 0) + (PHP > 0 && T == 1 ? NWV * 1024 : 0) +
+           (PHP > 0 ? pol_param_bytes(PL, PHP) + pw_bytes + kPolNch * 16 * 16 * 8 : kTeamNch * 16 * 16 * 4);
 }
 
 template <int HP, int NWV, int TPW, int T, int AK, int PHP = 0, bool RW = false>
@@ -256,15 +256,21 @@ void rollout_team(const RolloutArgs a) {
     constexpr int NT = HP / 16, P = HP / 32;
     constexpr int L0T = NT / NWV, L0P = L0T / 2;        // layer-0 tiles / k-steps per wave (whole layer per member)
     constexpr int PPW = (TPW + 1) / 2;                  // output-layer k-steps per wave (TPW = 1: half of one)
-    static_assert(!LNK || T == 1, "a LayerNorm after layer 1 needs the whole layer in one workgroup");
+    // a LayerNorm after layer 1 needs the whole layer in one workgroup -- except the reward net's heads,
+    // whose per-member statistics ride along with the output partials (below)
+    static_assert(!LNK || T == 1 || RW, "LayerNorm geometry");
+    constexpr bool HLN = RW && LNK;                     // the reward net's LayerNorm heads (dynamics.py:165-177)
     // fused policy (MPCcontrollerPolicyNet, ppo_bc_policy.py:54-88): each wave owns one policy tile
-    // pair; it shares the dynamics slab and the partials buffer (both free during the policy phase
-    // only when a team barrier ends the step, T > 1).  Reward net (NNDynamicsRewardModel): no LN.
+    // pair; it shares the dynamics slab (free once the step's partials barrier has passed) and, when
+    // a team barrier ends the step (T > 1), the partials buffer; at T == 1 waves may still be summing
+    // the previous step's dynamics partials while the first ones publish their policy partials, so
+    // those get a buffer of their own.  Any dynamics activation / LayerNorm (train_mpc_ppo.py's
+    // 2x256 relu + LN net under the 2x128 tanh policy, :178, :198-216).
     // Reward net (NNDynamicsRewardModel): waves [0, NWV/2) hold delta-head tiles, waves [NWV/2, NWV)
     // reward-head tiles (TPW each), so every wave keeps one head's weights: NH waves per head.
     constexpr int PTW = PHP / 16 / NWV;                 // policy tiles per wave (1: half a k-step, 2: one)
-    static_assert(PHP == 0 || ((PTW == 1 || PTW == 2) && T > 1 && AK == 0), "policy geometry");
-    static_assert(!RW || (AK == 0 && NWV % 2 == 0), "reward net: tanh, no LayerNorm, delta / reward waves");
+    static_assert(PHP == 0 || PTW == 1 || PTW == 2, "policy geometry");
+    static_assert(!RW || ((AK == 0 || AK == 2) && NWV % 2 == 0), "reward net: tanh (+ LayerNorm), delta / reward waves");
     constexpr int NB = RW ? 3 : 2;                      // hidden bias arrays (trunk, delta head, reward head)
     constexpr int NH = RW ? NWV / 2 : NWV;              // waves per head
     static_assert(HP == 16 * TPW * NH * T && (TPW == 1 || TPW % 2 == 0) && L0T % 2 == 0, "team geometry");
@@ -315,6 +321,8 @@ void rollout_team(const RolloutArgs a) {
         off += NWV * 2048;
         f4* const tot = reinterpret_cast<f4*>(base + off);
         off += T > 1 ? T * 2048 : 0;
+        f4* const pparts = PHP > 0 && T == 1 ? reinterpret_cast<f4*>(base + off) : parts;   // policy partials
+        off += PHP > 0 && T == 1 ? NWV * 1024 : 0;
         float* const xas = reinterpret_cast<float*>(base + off);          // (no policy)
         float* const Pb = reinterpret_cast<float*>(base + off);           // (policy) biases [pL][PHP] + params
         const char* const plw = base + off + (PHP > 0 ? pol_param_bytes(a.pL, PHP) : 0);   // policy weights
@@ -334,12 +342,30 @@ void rollout_team(const RolloutArgs a) {
             for (int i = threadIdx.x; i < pw_total / 16; i += blockDim.x)
                 reinterpret_cast<f4*>(const_cast<char*>(plw))[i] = src[i];
         }
-        if constexpr (LNK)
+        if constexpr (HLN) {
+            // the trunk's gamma / beta at [0, HP) / [2 HP, 3 HP); [HP, ..): the heads' centring table
+            // head_rs [T][32], then Chan's merge weights (nb / nn, n nb / nn) of the T members in order
+            for (int i = threadIdx.x; i < HP; i += blockDim.x) {
+                lnp[i] = a.lng[0][i];
+                lnp[2 * HP + i] = a.lnb[0][i];
+            }
+            for (int i = threadIdx.x; i < T * 32; i += blockDim.x) lnp[HP + i] = a.head_rs[i];
+            if (threadIdx.x == 0) {
+                float n = 0.f;
+                for (int t = 0; t < T; ++t) {
+                    const float nb = (float)min(max(a.hidden - 16 * TPW * NH * t, 0), 16 * TPW * NH), nn = n + nb;
+                    lnp[HP + T * 32 + 2 * t] = nb > 0.f ? nb / nn : 0.f;
+                    lnp[HP + T * 32 + 2 * t + 1] = nb > 0.f ? n * nb / nn : 0.f;
+                    n = nn;
+                }
+            }
+        } else if constexpr (LNK) {
             for (int l = 0; l < 2; ++l)
                 for (int i = threadIdx.x; i < HP; i += blockDim.x) {
                     lnp[l * HP + i] = a.lng[l][i];
                     lnp[(2 + l) * HP + i] = a.lnb[l][i];
                 }
+        }
 
         if constexpr (PHP == 0)
             for (int i = threadIdx.x; i < kTeamNch * 16 * 16; i += blockDim.x)
@@ -654,11 +680,11 @@ void rollout_team(const RolloutArgs a) {
                 }
                 // output layer [PHP -> one 16-row tile], K-split: this wave's (half) k-step, from registers
                 const f4 po_ = mm3(pwoh, pwol, xh, xl, (f4){0.f, 0.f, 0.f, 0.f});
-                parts[w * 64 + lane] = po_;
+                pparts[w * 64 + lane] = po_;
                 lds_barrier();                            // the output layer's partials
-                f4 o = parts[0 * 64 + lane];
+                f4 o = pparts[0 * 64 + lane];
 #pragma unroll
-                for (int x = 1; x < NWV; ++x) o += parts[x * 64 + lane];    // fixed summation order
+                for (int x = 1; x < NWV; ++x) o += pparts[x * 64 + lane];   // fixed summation order
                 const float fo_p = a.pwinv[a.pL];
                 const double* const dr = pdr + ((h % kPolNch) * 16 + m) * 16;
 #pragma unroll
@@ -782,7 +808,61 @@ void rollout_team(const RolloutArgs a) {
             const float* const Bh = Bl + (rw_wave ? 2 : 1) * HP;
             h8 oh[PPW], ol[PPW];
             float fcol1 = 1.f;
-            if constexpr (AK == 0 && TPW >= 2) {
+            float hst[4] = {0.f, 0.f, 0.f, 0.f};          // (HLN) the member's (mean, M2) of both heads
+            if constexpr (HLN) {
+                // LayerNorm over a head split across the team (dynamics.py:171, :177; TF1 layer_norm, eps
+                // 1e-12): tanh x 2^12, this wave's (mean, M2) over its valid rows, merged with its head's
+                // other waves in wave order (Chan) into the MEMBER's statistics; the output layer then sees
+                // h - mean_member (gamma is folded into the output weights, beta into their bias: capi.cpp),
+                // and the team's exact (h - mean) sums are rebuilt after the exchange from the members'
+                // statistics: sum_t P_t + sum_t (mean_t - mean) rs_t, times rsqrt(var + eps)
+                const int nwr = min(max(a.hidden - 16 * TPW * g, 0), 16 * TPW);
+                float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) {
+                    const f4 b = *reinterpret_cast<const f4*>(Bh + 16 * (TPW * g + j) + 4 * q);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        acc1[j][r] = tanh4096(fmaf(acc1[j][r], f1, b[r]));     // pad rows: exactly 0
+                        s0 += acc1[j][r];
+                    }
+                }
+                s0 = add_rows(s0) * (nwr > 0 ? 1.0f / (float)nwr : 0.f);
+#pragma unroll
+                for (int j = 0; j < TPW; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float d = acc1[j][r] - s0;
+                        s1 += (16 * (TPW * g + j) + 4 * q + r < a.hidden) ? d * d : 0.f;
+                    }
+                s1 = add_rows(s1);
+                float* const hx = xch + NWV * 32;
+                if (q == 0) *reinterpret_cast<f2*>(hx + (w * 16 + m) * 2) = (f2){s0, s1};
+                lds_barrier();                               // every wave's head statistics
+#pragma unroll
+                for (int hd = 0; hd < 2; ++hd) {
+                    float mean = 0.f, m2 = 0.f, n = 0.f;
+#pragma unroll
+                    for (int v = 0; v < NH; ++v) {
+                        const float nb = (float)min(max(a.hidden - 16 * TPW * (tm * NH + v), 0), 16 * TPW);
+                        if (nb > 0.f) {
+                            const f2 st = *reinterpret_cast<const f2*>(hx + ((hd * NH + v) * 16 + m) * 2);
+                            const float nn = n + nb, d = st[0] - mean;
+                            mean = mean + d * (nb / nn);
+                            m2 = m2 + st[1] + d * d * (n * nb / nn);
+                            n = nn;
+                        }
+                    }
+                    hst[2 * hd] = mean;
+                    hst[2 * hd + 1] = m2;
+                }
+                const float mc = rw_wave ? hst[2] : hst[0];
+#pragma unroll
+                for (int j = 0; j < TPW; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc1[j][r] -= mc;        // (pad rows: zero output weights)
+                split_tiles<TPW>(acc1, g & 1, oh, ol);
+            } else if constexpr (AK == 0 && TPW >= 2) {
 #pragma unroll
                 for (int pp = 0; pp < PPW; ++pp)
                     epi_pair_tanh(acc1[2 * pp], acc1[2 * pp + 1], f1, Bh, TPW * g + 2 * pp, q, oh[pp], ol[pp]);
@@ -839,11 +919,17 @@ void rollout_team(const RolloutArgs a) {
                 const unsigned ep = (gen << 10) + (unsigned)h + 1u;
                 const size_t slot = ((size_t)col * 2 + (h & 1)) * T;
                 const int R = S + (RW ? 1 : 0);           // rows exchanged: delta rows (+ the reward row)
+                // (+ rows 24..27: the member's head statistics mean_d, M2_d, mean_r, M2_r, lane row q = 2)
+                auto xrow = [&](int row) __attribute__((always_inline)) { return row < R || (HLN && (row >> 2) == 6); };
+                if constexpr (HLN)
+                    if (q == 2)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) mp[1][r] = hst[r];
                 if (w == 0) {
                     gu64* const mine = gb + (slot + tm) * 512;
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
-                        if (16 * (k >> 2) + 4 * q + (k & 3) < R)
+                        if (xrow(16 * (k >> 2) + 4 * q + (k & 3)))
                             __hip_atomic_store(mine + k * 64 + lane,
                                                ((unsigned long long)ep << 32) | __float_as_uint(mp[k >> 2][k & 3]),
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -861,7 +947,7 @@ void rollout_team(const RolloutArgs a) {
                         bool ok = true;
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
-                            if (16 * (k >> 2) + 4 * q + (k & 3) < R) {
+                            if (xrow(16 * (k >> 2) + 4 * q + (k & 3))) {
                                 const unsigned long long xv =
                                     __hip_atomic_load(src + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 got[k >> 2][k & 3] = __uint_as_float((unsigned)xv);
@@ -885,6 +971,50 @@ void rollout_team(const RolloutArgs a) {
                     ot[v] = tot[(0 * 2 + v) * 64 + lane];
 #pragma unroll
                     for (int t = 1; t < T; ++t) ot[v] += tot[(t * 2 + v) * 64 + lane];     // member order
+                }
+                if constexpr (HLN) {
+                    // the heads' LayerNorm, completed: the team's (mean, M2) per head from the members'
+                    // statistics (Chan, member order, identical in every member), then per output row i
+                    // (delta rows < S: the delta head; row S: the reward head)
+                    //   ot_i = rsqrt(M2 / hidden + eps) (sum_t P_t,i + sum_t (mean_t - mean) rs_t,i)
+                    const float* const rs = lnp + HP;
+                    const float* const tw = rs + T * 32;
+                    float mean[2] = {0.f, 0.f}, m2[2] = {0.f, 0.f};
+#pragma unroll
+                    for (int t = 0; t < T; ++t) {
+                        const f4 st = tot[(t * 2 + 1) * 64 + 32 + m];
+                        const float w0 = tw[2 * t], w1 = tw[2 * t + 1];
+#pragma unroll
+                        for (int hd = 0; hd < 2; ++hd) {
+                            const float d = st[2 * hd] - mean[hd];
+                            mean[hd] = mean[hd] + d * w0;
+                            m2[hd] = m2[hd] + st[2 * hd + 1] + d * d * w1;
+                        }
+                    }
+                    float inv[2];
+#pragma unroll
+                    for (int hd = 0; hd < 2; ++hd)
+                        inv[hd] = __builtin_amdgcn_rsqf(m2[hd] * (1.0f / (float)a.hidden) + 1e-12f * 16777216.0f);
+                    f4 corr[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                    for (int t = 0; t < T; ++t) {
+                        const f4 st = tot[(t * 2 + 1) * 64 + 32 + m];
+                        const float dd = st[0] - mean[0], dr = st[2] - mean[1];
+#pragma unroll
+                        for (int v = 0; v < 2; ++v) {
+                            const f4 rv = *reinterpret_cast<const f4*>(rs + t * 32 + 16 * v + 4 * q);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                corr[v][r] = fmaf(16 * v + 4 * q + r == S ? dr : dd, rv[r], corr[v][r]);
+                        }
+                    }
+#pragma unroll
+                    for (int v = 0; v < 2; ++v)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i = 16 * v + 4 * q + r;
+                            ot[v][r] = i > S ? 0.f : (ot[v][r] + corr[v][r]) * inv[i == S ? 1 : 0];
+                        }
                 }
             }
             stamp(8);
@@ -923,8 +1053,16 @@ static TeamShape team_shape_of(int hidden_padded, int kind) {
             default: return {0, 0, 0};
         }
     }
+    if (kind == 1) {                                   // + fused policy (2 policy tiles per wave)
+        switch (hidden_padded) {
+            case 128: return {4, 2, 1};
+            case 256: return {4, 4, 1};
+            case 512: return {4, 2, 4};
+            default: return {0, 0, 0};
+        }
+    }
     if (hidden_padded != 512) return {0, 0, 0};
-    return kind == 1 ? TeamShape{4, 2, 4} : TeamShape{TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8};   // reward: delta / reward waves
+    return TeamShape{TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8};   // reward: delta / reward waves
 }
 
 int team_members(int hidden_padded, int kind) { return team_shape_of(hidden_padded, kind).members; }
@@ -941,6 +1079,7 @@ size_t team_buf_bytes(int64_t K, int hidden_padded, int kind) {
     const int T = team_members(hidden_padded, kind);
     return T > 1 ? (size_t)((K + 15) / 16 + 8) * 2 * T * 512 * sizeof(unsigned long long) : 0;
 }
+bool team_rw_ln_built() { return true; }
 static int team_kind(const RolloutArgs& a) { return a.model == BCMPC_MODEL_REWARD ? 2 : a.pL > 0 ? 1 : 0; }
 
 template <int HP, int NWV, int TPW, int T, int AK, int PHP = 0, bool RW = false>
@@ -969,17 +1108,17 @@ static hipError_t launch_team_t(const RolloutArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int HP, int NWV, int TPW, int T>
+template <int HP, int NWV, int TPW, int T, int PHP = 0>
 static hipError_t launch_team_ak(const RolloutArgs& a, hipStream_t st) {
     const int ak = (a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0);
     switch (ak) {
-        case 0: return launch_team_t<HP, NWV, TPW, T, 0>(a, st);
-        case 1: return launch_team_t<HP, NWV, TPW, T, 1>(a, st);
+        case 0: return launch_team_t<HP, NWV, TPW, T, 0, PHP>(a, st);
+        case 1: return launch_team_t<HP, NWV, TPW, T, 1, PHP>(a, st);
         case 2:
-            if constexpr (T == 1) return launch_team_t<HP, NWV, TPW, T, 2>(a, st);
+            if constexpr (T == 1) return launch_team_t<HP, NWV, TPW, T, 2, PHP>(a, st);
             return hipErrorInvalidValue;
         case 3:
-            if constexpr (T == 1) return launch_team_t<HP, NWV, TPW, T, 3>(a, st);
+            if constexpr (T == 1) return launch_team_t<HP, NWV, TPW, T, 3, PHP>(a, st);
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
@@ -987,10 +1126,26 @@ static hipError_t launch_team_ak(const RolloutArgs& a, hipStream_t st) {
 
 hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
     const int kind = team_kind(a);
+    if (kind == 1) {
+        // + fused policy: any activation / LayerNorm at hidden <= 256 (one workgroup per column, e.g.
+        // train_mpc_ppo.py's 2x256 relu + LN net); hidden 512: tanh, no LayerNorm (4 members)
+        switch (hidden_padded) {
+            case 128: return launch_team_ak<128, 4, 2, 1, 128>(a, st);
+            case 256: return launch_team_ak<256, 4, 4, 1, 128>(a, st);
+            case 512:
+                if (a.act != BCMPC_ACT_TANH || a.ln) return hipErrorInvalidValue;
+                return launch_team_t<512, 4, 2, 4, 0, 128, false>(a, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (kind > 0) {
-        // the policy / reward variants: hidden 512, tanh, no LayerNorm (the run.sh recipe's nets)
-        if (hidden_padded != 512 || a.act != BCMPC_ACT_TANH || a.ln) return hipErrorInvalidValue;
-        if (kind == 1) return launch_team_t<512, 4, 2, 4, 0, 128, false>(a, st);
+        // the reward net: hidden 512, tanh (+ LayerNorm: the run.sh recipe's net, train_mpc_ppo.py:52)
+        if (hidden_padded != 512 || a.act != BCMPC_ACT_TANH) return hipErrorInvalidValue;
+        if (a.ln) {
+            if (a.S > 23 || !a.head_rs) return hipErrorInvalidValue;
+            if (a.pL > 0) return launch_team_t<512, TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8, 2, 128, true>(a, st);
+            return launch_team_t<512, TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8, 2, 0, true>(a, st);
+        }
         if (a.pL > 0) return launch_team_t<512, TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8, 0, 128, true>(a, st);
         return launch_team_t<512, TEAM_RW_NWV, 8 / TEAM_RW_NWV, 8, 0, 0, true>(a, st);
     }

@@ -163,7 +163,14 @@ class RolloutEngine:
                         and (model == "delta" or state_dim >= 16)
                         and (not policy_hidden or 448 < hidden <= top)
                         and kernel in ("auto", "split1", "split2", "split4", "splitr", "team"))
-            precision = "split" if split_ok else "fp32"
+            # the small-K team kernel also takes relu / LayerNorm dynamics under a fused policy (hidden
+            # <= 256: train_mpc_ppo.py's 2x256 relu + LN net) and the LayerNorm reward net (the run.sh
+            # recipe) when its grid is resident: tried in split, fp32 when bcmpc_create refuses
+            team_try = (not split_ok and kernel == "auto" and n_layers == 2 and state_dim >= 16
+                        and bool(policy_hidden or model == "reward"))
+            precision = "split" if split_ok or team_try else "fp32"
+        else:
+            team_try = False
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"unknown precision {precision!r}; one of {sorted(_lib.PRECISIONS)}")
         cfg.precision = _lib.PRECISIONS[precision]
@@ -173,7 +180,13 @@ class RolloutEngine:
         cfg.policy_hidden, cfg.policy_layers = int(policy_hidden), int(policy_layers)
         cfg.policy_mode = _lib.POLICY_MODES[policy_mode]
         h = ctypes.c_void_p()
-        _lib.check(self._lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h)))
+        rc = self._lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc == _lib.ERR_UNSUPPORTED and team_try:
+            precision = "fp32"
+            cfg.precision = _lib.PRECISIONS[precision]
+            self.precision = precision
+            rc = self._lib.bcmpc_create(ctypes.byref(cfg), ctypes.byref(h))
+        _lib.check(rc)
         self._h = h
         self.state_dim, self.action_dim = state_dim, action_dim
         self.hidden, self.n_layers, self.activation = hidden, n_layers, activation

@@ -315,6 +315,18 @@ def _split_policy_ok(hidden, act, ln):
     return act == "tanh" and not ln and 448 < hidden <= 1024
 
 
+def team_policy_ok(hidden, act, ln, K, ph, pl):
+    """Shapes the team kernel takes with a fused policy (capi.cpp bcmpc_create): <= 2 x 128 policy; dynamics
+    hidden 65..256 with any activation / LayerNorm (one workgroup per column: ceil(K/128)*8 <= 256 CUs) or
+    449..512 tanh without LayerNorm (4 members per column)."""
+    if ph > 128 or pl > 2 or K < 1:
+        return False
+    blocks = -(-(-(-K // 16)) // 8) * 8
+    if 64 < hidden <= 256:
+        return blocks <= 256
+    return 448 < hidden <= 512 and act == "tanh" and not ln and 4 * blocks <= 256
+
+
 @pytest.mark.parametrize("kernel", ["fp32", "split1", "split2", "split4", "team"])
 @pytest.mark.parametrize("name", golden_names("policy"))
 def test_policy_engine_matches_reference_fixture(name, kernel):
@@ -323,10 +335,10 @@ def test_policy_engine_matches_reference_fixture(name, kernel):
     from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
     g = Golden(name)
     w, p = g.weights, g.policy
-    if kernel != "fp32" and not _split_policy_ok(w.hidden, w.activation, w.layer_norm):
+    if kernel.startswith("split") and not _split_policy_ok(w.hidden, w.activation, w.layer_norm):
         pytest.skip("split kernel with a policy: tanh dynamics without LayerNorm, hidden 449..1024")
-    if kernel == "team" and not (w.hidden <= 512 and p.hidden <= 128 and p.n_layers <= 2 and g.K <= 2048):
-        pytest.skip("team kernel with a policy: hidden 449..512, policy <= 2 x 128, small K")
+    if kernel == "team" and not team_policy_ok(w.hidden, w.activation, w.layer_norm, g.K, p.hidden, p.n_layers):
+        pytest.skip("team kernel with a policy: hidden 65..256 (any net) or 449..512 tanh, policy <= 2 x 128, small K")
     kw = dict(precision="fp32") if kernel == "fp32" else dict(kernel=kernel)
     eng = RolloutEngine(g.S, g.A, w.hidden, w.n_layers, w.activation, w.layer_norm, g.H, g.K,
                         policy_hidden=p.hidden, policy_layers=p.n_layers, policy_mode="explore", **kw)
@@ -363,7 +375,7 @@ def test_policy_controller_dropin(name):
     assert np.random.random() == float(g.z["next_draw"])        # same RNG side effect as the reference
 
 
-@pytest.mark.parametrize("kernel", ["fp32", "split2", "team"])
+@pytest.mark.parametrize("kernel", ["fp32", "split2", "team", "team_relu_ln"])
 def test_policy_stochastic_mode_pinned_every_step(kernel):
     """self_exp=True (run.sh's recipe, controllers.py:202-203): at EVERY horizon step the action the
     kernel rolled out equals mean(s_h) + exp(logstd) * z_h, where s_h is the GPU's own trajectory
@@ -379,6 +391,9 @@ def test_policy_stochastic_mode_pinned_every_step(kernel):
     if kernel == "fp32":
         w = orc.synthetic_weights(S, A, 256, 2, "relu", False)
         kw = dict(precision="fp32")
+    elif kernel == "team_relu_ln":      # train_mpc_ppo.py's own dynamics net (:52, :74-75, :539)
+        w = orc.synthetic_weights(S, A, 256, 2, "relu", True)
+        kw = dict(kernel="team")
     else:
         w = orc.synthetic_weights(S, A, 500, 2, "tanh", False)
         kw = dict(kernel=kernel)
@@ -388,9 +403,9 @@ def test_policy_stochastic_mode_pinned_every_step(kernel):
     dyn, pol = orc.NumpyDynamics(w, norm), orc.NumpyPolicy(p)
 
     def mk(k):
-        e = RolloutEngine(S, A, w.hidden, 2, w.activation, False, H, k, policy_hidden=128, policy_layers=2,
-                          policy_mode="stochastic", **kw)
-        e.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+        e = RolloutEngine(S, A, w.hidden, 2, w.activation, w.layer_norm, H, k, policy_hidden=128,
+                          policy_layers=2, policy_mode="stochastic", **kw)
+        e.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), norm, 1)
         e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.5, 1)
         return e
     full = mk(K)

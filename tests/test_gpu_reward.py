@@ -87,8 +87,8 @@ def test_reward_engine_matches_reference_fixture(name, kernel):
     from bc_mpc_amd.engine import RolloutEngine
     g = RewardGolden(name)
     _skip_split(g, kernel)
-    if kernel == "team" and not (448 < g.weights.hidden <= 512 and not g.weights.layer_norm and 0 < g.K <= 1024):
-        pytest.skip("team kernel, reward net: hidden 449..512, no LayerNorm, K <= 1024")
+    if kernel == "team" and not (448 < g.weights.hidden <= 512 and 0 < g.K <= 512):
+        pytest.skip("team kernel, reward net: hidden 449..512, K <= 512")
     eng = RolloutEngine(g.S, g.A, g.weights.hidden, 2, "tanh", g.weights.layer_norm, g.H, g.K, device=0,
                         cost="reward", model="reward", kernel=kernel)
     assert eng.info()["kernel"] == kernel
@@ -136,12 +136,14 @@ def test_policy_reward_engine_matches_reference_fixture(name, kernel):
     from bc_mpc_amd.engine import PolicySpec, RolloutEngine
     g = RewardGolden(name)
     p = g.policy
-    if kernel == "team" and not (448 < g.weights.hidden <= 512 and not g.weights.layer_norm and 0 < g.K <= 1024
+    if kernel == "team" and not (448 < g.weights.hidden <= 512 and 0 < g.K <= 512
                                  and p.hidden <= 128 and p.n_layers <= 2):
-        pytest.skip("team kernel, reward net + policy: hidden 449..512, no LayerNorm, policy <= 2 x 128")
+        pytest.skip("team kernel, reward net + policy: hidden 449..512, policy <= 2 x 128, K <= 512")
     eng = RolloutEngine(g.S, g.A, g.weights.hidden, 2, "tanh", g.weights.layer_norm, g.H, g.K, device=0,
                         cost="reward", model="reward", kernel=kernel, policy_hidden=p.hidden,
                         policy_layers=p.n_layers, policy_mode="explore")
+    if kernel == "team":
+        assert eng.info()["kernel"] == "team"
     eng.set_weights(_spec(g), g.norm, 1)
     eng.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), g.explore, 1)
     expl = np.random.RandomState(g.meta["seed"]).uniform(g.low, g.high, size=[g.H, g.K, g.A])
@@ -284,16 +286,19 @@ def test_split_policy_reward_matches_fp32_engine(mode):
     assert rsp.best_index == int(np.argmax(rsp.costs))
 
 
+@pytest.mark.parametrize("ln", [False, True], ids=["noln", "ln"])
 @pytest.mark.parametrize("mode", ["explore", "stochastic", "none"])
-def test_team_policy_reward_matches_fp32_engine(mode):
+def test_team_policy_reward_matches_fp32_engine(mode, ln):
     """The run.sh recipe's shape on the small-K team kernel (rollout_team.hip: reward-head and
     delta-head waves, fused policy, 8 workgroups per 16-candidate column, one exchange per step)
-    against the fp32 group kernel on the same draws: K = 400 (train_mpc_ppo.py:71), hidden 500."""
+    against the fp32 group kernel on the same draws: K = 400 (train_mpc_ppo.py:71), hidden 500;
+    ln=True is the recipe as run.sh:31 runs it (LAYER_NORM defaults to True, train_mpc_ppo.py:52:
+    the trunk and both heads LayerNorm'd, dynamics.py:165-177)."""
     from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
     from oracle import mpc_oracle as orc
     S, A, K, H, h = 20, 6, 400, 12, 500
     norm = orc.synthetic_normalization(S, A, seed=5, reward=True)
-    w = orc.synthetic_reward_weights(S, A, h, False, seed_base=123)
+    w = orc.synthetic_reward_weights(S, A, h, ln, seed_base=123)
     p = orc.synthetic_policy(S, A, 128, 2, seed=9)
     state = orc.synthetic_state(norm, seed=6)
     expl = np.random.RandomState(4).uniform(-1, 1, (H, K, A))
@@ -301,8 +306,8 @@ def test_team_policy_reward_matches_fp32_engine(mode):
     for kern in ("fp32", "team"):
         kw = dict(precision="fp32") if kern == "fp32" else dict(kernel="team")
         pol = dict(policy_hidden=128, policy_layers=2, policy_mode=mode) if mode != "none" else {}
-        e = RolloutEngine(S, A, h, 2, "tanh", False, H, K, cost="reward", model="reward", **pol, **kw)
-        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh", model="reward"), norm, 1)
+        e = RolloutEngine(S, A, h, 2, "tanh", ln, H, K, cost="reward", model="reward", **pol, **kw)
+        e.set_weights(MLPSpec(w.kernels, w.biases, "tanh", w.ln_gamma, w.ln_beta, model="reward"), norm, 1)
         e.set_discount(0.99)
         if mode != "none":
             e.set_policy(PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd), 0.5, 1)
@@ -319,5 +324,5 @@ def test_team_policy_reward_matches_fp32_engine(mode):
         err = np.abs(at - a32)
         print(f"[team polrew {mode}] max|dfirst|={err.max():.3e}")
         assert (err <= 2e-6).all()
-    assert_rewards_close(rt.costs, r32.costs, f"team polrew {mode}")
+    assert_rewards_close(rt.costs, r32.costs, f"team polrew {mode} ln={ln}")
     assert rt.best_index == int(np.argmax(rt.costs))

@@ -131,6 +131,24 @@ def test_team_auto_rule():
         eng.close()
 
 
+def test_team_auto_rule_reference_controllers():
+    """The reference's two real control configurations pick the team kernel under auto (split
+    precision), and fall back to the fp32 group kernel once the grid would not be resident:
+    MPCcontrollerPolicyNet over the 2x256 relu + LN net with the 2x128 policy (train_mpc_ppo.py:178,
+    :198-216) and MPCcontrollerPolicyNetReward over the LayerNorm reward net (run.sh:31)."""
+    from bc_mpc_amd.engine import RolloutEngine
+    cases = [(dict(hidden=256, act="relu", ln=True, model="delta", cost="cheetah"), 400, "team"),
+             (dict(hidden=256, act="relu", ln=True, model="delta", cost="cheetah"), 8192, "group4"),
+             (dict(hidden=500, act="tanh", ln=True, model="reward", cost="reward"), 400, "team"),
+             (dict(hidden=500, act="tanh", ln=True, model="reward", cost="reward"), 4096, "group4")]
+    for c, K, want in cases:
+        e = RolloutEngine(20, 6, c["hidden"], 2, c["act"], c["ln"], 7, K, cost=c["cost"], model=c["model"],
+                          policy_hidden=128, policy_layers=2, policy_mode="stochastic")
+        assert e.info()["kernel"] == want, (c, K, e.info()["kernel"])
+        assert e.precision == ("split" if want == "team" else "fp32")
+        e.close()
+
+
 def test_team_cem_iterations_match_oracle():
     """CEM on the team kernel: every iteration's sampled sequences are scored like the
     oracle's, and the fused single-call path agrees with the per-iteration one."""
