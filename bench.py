@@ -60,8 +60,14 @@ WORKLOADS = {
     # BASELINE cfg5: K=65536, H=50, 3x1024 tanh with the CEM outer loop (4 iterations; elites 10%, smoothing 0.1;
     # DESIGN.md "CEM" -- the reference has no CEM).  One step = one CEMcontroller.get_action = 4 rollout passes.
     "cfg5": dict(K=65536, H=50, hidden=1024, L=3, act="tanh", cem=dict(iterations=4, elite_frac=0.1, alpha=0.1)),
-    "runsh_recipe": dict(K=400, H=30, hidden=500, L=2, act="tanh", reward=True, policy=(128, 2), explore=0.5,
-                         policy_mode="stochastic"),
+    # (LAYER_NORM is not passed by run.sh, so its default True holds, train_mpc_ppo.py:52: the trunk and both heads
+    # are LayerNorm'd, dynamics.py:165-177)
+    "runsh_recipe": dict(K=400, H=30, hidden=500, L=2, act="tanh", ln=True, reward=True, policy=(128, 2),
+                         explore=0.5, policy_mode="stochastic"),
+    # the default MPC-aug path of train_mpc_ppo.py (:198-216, flags :36-37, :52, :71, :74-77, :178, :539):
+    # MPCcontrollerPolicyNet over the 2x256 relu + LayerNorm NNDynamicsModel with the 2x128 tanh MlpPolicy,
+    # self_exp=False, explore=0.5, 400 paths, horizon 7
+    "ppo_mpc_default": dict(K=400, H=7, hidden=256, L=2, act="relu", ln=True, policy=(128, 2), explore=0.5),
 }
 S_DIM, A_DIM = 20, 6
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix, v_mfma_f32_16x16x4_f32
@@ -214,10 +220,11 @@ def synthetic_problem(wl):
         biases.append((0.1 * r.standard_normal(fo)).astype(np.float32))
     ln = bool(wl.get("ln"))
     ln_g, ln_b = None, None
-    if ln:   # gamma ~ 1 + 0.1 N, beta ~ 0.1 N per hidden layer
+    if ln:   # gamma ~ 1 + 0.1 N, beta ~ 0.1 N per hidden layer (reward net: trunk, delta head, reward head)
         rl = np.random.RandomState(99)
-        ln_g = [(1.0 + 0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
-        ln_b = [(0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(L)]
+        nln = 3 if reward else L
+        ln_g = [(1.0 + 0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(nln)]
+        ln_b = [(0.1 * rl.standard_normal(hidden)).astype(np.float32) for _ in range(nln)]
     r7 = np.random.RandomState(7)
     mean_obs = 0.1 * r7.standard_normal(S_DIM)
     std_obs = np.abs(r7.standard_normal(S_DIM)) * 0.5 + 0.2
@@ -250,7 +257,7 @@ def make_engine(wl, prob, device, precision):
     K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
     if prob["policy"]:
         ph, pl = prob["policy"]
-        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, False, H, K, device=device, policy_hidden=ph,
+        eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, prob["ln"], H, K, device=device, policy_hidden=ph,
                             policy_layers=pl, policy_mode=wl.get("policy_mode", "explore"), cost=prob["cost"],
                             model=prob["model"], precision=precision)
         eng.set_policy(PolicySpec(*prob["pol_arrays"]), wl["explore"], 1)
@@ -264,14 +271,19 @@ def make_engine(wl, prob, device, precision):
     return eng
 
 
-SMALL_K = ("ppo_defaults", "runsh_recipe", "cfg1")    # the reference's own small configurations
+# the reference's own small configurations: MPCcontroller at train_mpc_ppo.py's defaults, its default MPC-aug
+# controller (MPCcontrollerPolicyNet), run.sh's recipe (MPCcontrollerPolicyNetReward, LayerNorm reward net,
+# stochastic policy), BASELINE cfg1
+SMALL_K = ("ppo_defaults", "ppo_mpc_default", "runsh_recipe", "cfg1")
 
 
 def small_k_lines(device, calls=200, warmup=20):
     """get_action p50 (host state in, device-drawn actions, host result out) and the rollout kernel's
     HIP-event time for the small-K workloads the reference actually runs (train_mpc_ppo.py:71,77: K=400;
     run.sh:27-31; BASELINE cfg1), with the auto kernel (the team kernel, rollout_team.hip) and with the
-    slab kernel it replaced (BCMPC_TEAM=0), on this process's GPU."""
+    kernel it replaced (BCMPC_TEAM=0: the split slab kernel, or for the nets only the team kernel takes in
+    split precision -- a policy over relu + LN, the LayerNorm reward net -- the fp32 group kernel), on
+    this process's GPU."""
     out = {}
     for name in SMALL_K:
         wl = WORKLOADS[name]
@@ -302,6 +314,7 @@ def small_k_lines(device, calls=200, warmup=20):
                 eng.get_action(prob["state"], None, seed=0x5EED + i)
                 ks.append(eng.last_kernel_ms()[0])
             row[tag + "kernel"] = eng.info()["kernel"]
+            row[tag + "precision"] = eng.precision
             row[tag + "p50_ms"] = float(np.percentile(ts, 50) * 1e3)
             row[tag + "kernel_ms"] = float(np.mean(ks))
             eng.close()
@@ -361,12 +374,7 @@ def main():
 
     wl = WORKLOADS[args.workload]
     K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
-    if args.precision == "auto":
-        top = 512 if wl.get("reward") else 1024
-        plain = act == "tanh" and not wl.get("ln")     # relu / LN: the plain delta net, hidden <= 512
-        ok = plain or (not wl.get("reward") and not wl.get("policy") and hidden <= 512)
-        args.precision = "split" if (ok and (not wl.get("policy") or 448 < hidden <= top)) else "fp32"
-    offset = rank * K
+    offset = rank * K                                  # (precision "auto": the engine's rule, engine.py)
 
     prob = synthetic_problem(wl)
     kernels, biases, ln_g, ln_b, norm, state = (prob[k] for k in ("kernels", "biases", "ln_g", "ln_b", "norm", "state"))
@@ -537,7 +545,7 @@ def main():
             pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import mpc_oracle as orc
-        w = orc.RewardMLPWeights(kernels, biases) if reward else orc.MLPWeights(kernels, biases, act, ln_g, ln_b)
+        w = orc.RewardMLPWeights(kernels, biases, ln_g, ln_b) if reward else orc.MLPWeights(kernels, biases, act, ln_g, ln_b)
         net = (f"reward net {hidden}" if reward else f"{L}x{hidden} {act}" + (" + LN" if ln else "")) + \
             (f" + policy {policy}" if policy else "")
         if policy and wl.get("policy_mode") == "stochastic":
