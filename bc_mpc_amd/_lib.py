@@ -25,7 +25,7 @@ MAX_LAYERS = 8
 MAX_STATE = 32
 MAX_ACTION = 16
 COMM_ID_BYTES = 128
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
 ACT_TANH, ACT_RELU = 0, 1
@@ -173,6 +173,10 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_double,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("bcmpc_stream", ctypes.c_void_p, [ctypes.c_void_p]),
+    ("bcmpc_engine_status", ctypes.c_int, [ctypes.c_void_p]),
+    ("bcmpc_engine_team_reruns", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    ("bcmpc_select_results_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     ("bcmpc_engine_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     ("bcmpc_last_kernel_ms", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),

@@ -184,6 +184,9 @@ class _EngineShard:
         self.eng.cem_rollout_async(d_state.data_ptr(), d_mu.data_ptr(), d_sigma.data_ptr(), seed, it, lo, k_global,
                                    d_costs.data_ptr(), d_res.data_ptr(), merge, self.stream())
 
+    def check_status(self):
+        self.eng.check_status()
+
     def select(self, d_pairs, d_costs, m, index_base, n_elite, d_out, d_count):
         self.eng.select_async(d_pairs.data_ptr() if d_pairs is not None else None,
                               d_costs.data_ptr() if d_costs is not None else None, m, index_base, n_elite,
@@ -228,6 +231,8 @@ def cem_multi_rank(shard, state, mu0, sd0, iterations, n_elite, alpha, seed, lo,
         shard.select(d_gath, None, ws * n_elite, 0, n_elite, d_elite, d_gcount)
         shard.refit(d_elite, d_gcount, seed, it, alpha, d_mu, d_sigma)
     raw = d_res.cpu().numpy()
+    if hasattr(shard, "check_status"):                 # a team-kernel launch that gave up raises here
+        shard.check_status()
     best_i = int(raw[:8].view(np.int64)[0])
     best_c = float(raw[8:16].view(np.float64)[0])
     first = raw[16:16 + 8 * A].view(np.float64).copy()

@@ -104,17 +104,22 @@ def _attach_comm(ctrl, eng: RolloutEngine, fused: bool = True) -> RolloutEngine:
     collective on the first call every rank makes together): its get_action then returns the global
     best itself.  Only when every rank holds candidates (K >= world) and the cost is fused."""
     rank, ws = _dist.world(ctrl._group)
-    if (fused and getattr(eng, "comm", None) is None and ws > 1 and int(ctrl.num_simulated_paths) >= ws
-            and _dist.use_library_comm(ctrl._group)):
+    want = fused and ws > 1 and int(ctrl.num_simulated_paths) >= ws and _dist.use_library_comm(ctrl._group)
+    if want and getattr(eng, "comm", None) is None:
         if getattr(ctrl, "_comm", None) is None:
             ctrl._comm = _dist.LibraryComm(eng.device, ctrl._group)
         eng.set_comm(ctrl._comm)
+    elif not want and getattr(eng, "comm", None) is not None:
+        # (K fell below the world size: a rank may hold no candidates and must join the torch
+        #  all-gather, so every rank's engine drops the communicator -- every rank decides alike)
+        eng.set_comm(None)
     return eng
 
 
 def _minloc(ctrl, eng, valid, cost, index, first, A):
     """The ranks' agreement on (cost, index, first action): already made inside the library when the
-    engine has a communicator, else one torch all-gather of the records."""
+    engine that ran THIS step (``eng``: None when this rank launched nothing) has a communicator, else
+    one torch all-gather of the records."""
     if eng is not None and getattr(eng, "comm", None) is not None:
         return float(cost), int(index), np.asarray(first, dtype=np.float64).copy()
     return _dist.allgather_minloc(valid, cost, index, first, A, ctrl._group, device=_comm_device(ctrl))
@@ -248,7 +253,7 @@ class MPCcontroller(Controller):
                 valid, cost, index, first = True, float(costs[i]), lo + i, local[0, i, :].copy()
                 self.last_costs = costs
 
-        cost, index, first_g = _minloc(self, self._engine, valid, cost, index, first, A)
+        cost, index, first_g = _minloc(self, self._engine if valid else None, valid, cost, index, first, A)
         self.last_cost, self.last_index = cost, index
         if action_paths is not None:
             opt_action_path = action_paths[:, index, :]     # controllers.py:84-85
@@ -269,6 +274,7 @@ class MPCcontroller(Controller):
         eng.rollout_async(d_state.data_ptr(), 0, d_act.data_ptr(), 0, 0, None, d_traj.data_ptr(), None,
                           stream.cuda_stream)
         traj = d_traj.cpu().numpy()                       # synchronises the stream
+        eng.check_status()
         return np.asarray(trajectory_cost_fn(self.cost_fn, traj[:-1], local_actions, traj[1:]), dtype=np.float64)
 
 
@@ -396,7 +402,7 @@ class MPCcontrollerPolicyNet(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, cost, index, first = True, res.best_cost, res.best_index, res.first_action
             self.last_costs = res.costs
-        cost, index, first_g = _minloc(self, self._engine, valid, sign * cost, index, first, A)
+        cost, index, first_g = _minloc(self, self._engine if valid else None, valid, sign * cost, index, first, A)
         self.last_cost, self.last_index = sign * cost, index
         return first_g                                         # copy of action_paths[0, argmin] (:233-235)
 
@@ -514,7 +520,7 @@ class MPCcontrollerReward(Controller):
             res = eng.get_action(state, local, seed=seed, cand_offset=lo, return_costs=self.keep_costs)
             valid, neg, index, first = True, -res.best_cost, res.best_index, res.first_action
             self.last_rewards = res.costs
-        neg, index, first_g = _minloc(self, self._engine, valid, neg, index, first, A)
+        neg, index, first_g = _minloc(self, self._engine if valid else None, valid, neg, index, first, A)
         self.last_reward, self.last_index = -neg, index
         if action_paths is not None:
             return copy.copy(action_paths[:, index, :][0])    # controllers.py:154-156
@@ -665,6 +671,7 @@ class MCTScontrollerPolicyNetReward(Controller):
         e1.rollout_async(d_state.data_ptr(), 0, d_act.data_ptr() if d_act is not None else None, seed1, 0,
                          d_r1.data_ptr(), d_traj.data_ptr(), None, stream)
         reward_1s = d_r1.cpu().numpy()                           # reward_1[0][0] of each predict (:418)
+        e1.check_status()
         first = e1.first_actions()
         if action_1s is None:                                    # policy.act's f32 [1, A] rows
             action_1s = [first[i:i + 1].astype(np.float32) for i in range(N)]
@@ -678,6 +685,7 @@ class MCTScontrollerPolicyNetReward(Controller):
             d_rsum = torch.empty(N * R, dtype=torch.float64, device=tdev)
             e2.rollout_async(d_states.data_ptr(), S, None, seed2, 0, d_rsum.data_ptr(), None, None, stream)
             rewards_all = d_rsum.cpu().numpy().reshape((-1, 1))  # sum over steps of [N*R, 1] (:442-443)
+            e2.check_status()
         else:
             seed2 = None
             rewards_all = np.sum(np.asarray([]), axis=0)         # the reference's empty horizon

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <chrono>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -141,6 +142,8 @@ namespace bcmpc {
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace bcmpc
 
+static thread_local bool g_no_team = false;         // bcmpc_create: never pick the team kernel (fallbacks)
+
 struct bcmpc_engine {
     bcmpc_config cfg{};
     int HP = 0, T = 0, wpb = 4;
@@ -222,6 +225,22 @@ struct bcmpc_engine {
     uint32_t* d_mt_part = nullptr;      // [Cj][S][624]
     uint32_t* h_mt_io = nullptr;        // pinned mirror of d_mt_io (+ bounds at word 1280)
     bcmpc_comm* comm = nullptr;         // attached communicator: results exchanged after every argmin
+    // team kernel: a team that could not meet (its workgroups not all resident: another process or
+    // kernel holding CUs for ~1 s) makes a synchronous call rerun on this fallback engine -- the same
+    // net on the split slab kernel, or the fp32 group kernel where only the team kernel takes the net
+    // in split precision -- created on first need and synced from the host copies kept below
+    bcmpc_engine* fb = nullptr;
+    uint64_t fb_wver = 0, fb_pver = 0;
+    bool fb_wset = false, fb_pset = false;
+    uint64_t team_reruns = 0;
+    struct HostNet {                    // the last bcmpc_set_weights / bcmpc_set_policy, copied
+        std::vector<std::vector<float>> k, b, g, beta;
+        std::vector<double> st[8];      // mean/std obs, action, deltas, reward
+        std::vector<float> pvec[3];     // (policy) ob_mean, ob_std, logstd
+        double explore = 0.0;
+        bool ln = false;
+    } hw_copy, hp_copy;
+    double gamma = 1.0;
 };
 
 extern "C" {
@@ -352,7 +371,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                                            "net: 512, tanh, LayerNorm with S <= 23), S + A <= 32, "
                                            "ceil(K / 128) * 8 * members workgroups <= the device's CUs");
     }
-    if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr) {
+    if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr && !g_no_team) {
         const char* ev = std::getenv("BCMPC_TEAM");
         use_team = !(ev && ev[0] == '0');
     }
@@ -529,6 +548,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
 
 int bcmpc_destroy(bcmpc_engine* e) {
     if (!e) return BCMPC_OK;
+    if (e->fb) (void)bcmpc_destroy(e->fb);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
@@ -757,6 +777,28 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
     HIP_TRY(hipMemcpyAsync(e->d_ln, hln.data(), hln.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemcpyAsync(e->d_consts, C, sizeof(e->h_consts), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));   // host vectors die at scope exit
+    if (e->kernel == BCMPC_KERNEL_TEAM) {
+        // (the fallback engine's copy: created only if a team ever fails to meet)
+        auto& hc = e->hw_copy;
+        hc = bcmpc_engine::HostNet{};
+        const int nin[5] = {S + A, h, h, h, h}, nout[5] = {h, h, S, h, 1};   // (reward net: dense .. dense_4)
+        for (int l = 0; l < NK; ++l) {
+            const int in = rw ? nin[l] : (l == 0 ? S + A : h), out = rw ? nout[l] : (l == L ? S : h);
+            hc.k.emplace_back(w->kernels[l], w->kernels[l] + (size_t)in * out);
+            hc.b.emplace_back(w->biases[l], w->biases[l] + out);
+        }
+        hc.ln = c.layer_norm != 0;
+        if (hc.ln)
+            for (int l = 0; l < NLN; ++l) {
+                hc.g.emplace_back(w->ln_gamma[l], w->ln_gamma[l] + h);
+                hc.beta.emplace_back(w->ln_beta[l], w->ln_beta[l] + h);
+            }
+        const double* sp[8] = {w->mean_obs, w->std_obs, w->mean_action, w->std_action, w->mean_deltas,
+                               w->std_deltas, rw ? w->mean_reward : nullptr, rw ? w->std_reward : nullptr};
+        const int sn[8] = {S, S, A, A, S, S, 1, 1};
+        for (int i = 0; i < 8; ++i)
+            if (sp[i]) hc.st[i].assign(sp[i], sp[i] + sn[i]);
+    }
     e->version = version;
     e->has_weights = true;
     return BCMPC_OK;
@@ -816,6 +858,18 @@ int bcmpc_set_policy(bcmpc_engine* e, const bcmpc_policy* p, uint64_t version) {
     HIP_TRY(hipMemcpyAsync(e->d_pw, hw.data(), hw.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemcpyAsync(e->d_pb, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->kernel == BCMPC_KERNEL_TEAM) {               // (the fallback engine's copy)
+        auto& hc = e->hp_copy;
+        hc = bcmpc_engine::HostNet{};
+        for (int l = 0; l <= PL; ++l) {
+            const int in = l == 0 ? S : ph, out = l == PL ? A : ph;
+            hc.k.emplace_back(p->kernels[l], p->kernels[l] + (size_t)in * out);
+            hc.b.emplace_back(p->biases[l], p->biases[l] + out);
+        }
+        hc.pvec[0].assign(p->ob_mean, p->ob_mean + S);
+        hc.pvec[1].assign(p->ob_std, p->ob_std + S);
+        hc.pvec[2].assign(p->logstd, p->logstd + A);
+    }
     e->explore = p->explore;
     e->pol_version = version;
     e->has_policy = true;
@@ -847,6 +901,7 @@ int bcmpc_set_discount(bcmpc_engine* e, double gamma) {
     if (!e->reward) return fail(BCMPC_ERR_STATE, "discount applies to reward engines (config.model == BCMPC_MODEL_REWARD)");
     std::vector<double> g((size_t)e->cfg.horizon);
     for (int i = 0; i < e->cfg.horizon; ++i) g[i] = std::pow(gamma, (double)i);   // Python float ** int
+    e->gamma = gamma;
     HIP_TRY(hipSetDevice(e->cfg.device));
     HIP_TRY(hipMemcpyAsync(e->d_gpow, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -864,13 +919,118 @@ struct CemLaunch {           // one CEM iteration's sampling distribution + resu
 };
 
 // team kernel: a team whose workgroups could not all become resident gives up after its bounded
-// spin and raises the mapped flag (rollout_team.hip); checked after every synchronous call
+// spin and raises the mapped flag (rollout_team.hip).  Synchronous calls check it after their
+// synchronisation and rerun on the fallback engine (team_rerun); stream-ordered callers read it with
+// bcmpc_engine_status once their stream is done.  Reading clears it.
+static bool team_failed(bcmpc_engine* e) {
+    if (e->h_team_err && __atomic_load_n(e->h_team_err, __ATOMIC_ACQUIRE) != 0) {
+        __atomic_store_n(e->h_team_err, 0u, __ATOMIC_RELEASE);
+        return true;
+    }
+    return false;
+}
 static int team_status(bcmpc_engine* e) {
-    if (e->h_team_err && *reinterpret_cast<volatile unsigned*>(e->h_team_err) != 0) {
-        *e->h_team_err = 0;
+    if (team_failed(e))
         return fail(BCMPC_ERR_HIP, "team kernel: a workgroup team did not meet (its grid was not resident -- "
                                    "another kernel holding the CUs?)");
+    return BCMPC_OK;
+}
+
+// the fallback engine of a team engine, created on first need and kept in sync with the team
+// engine's weights / policy / discount / action bounds (host copies)
+static int team_fallback(bcmpc_engine* e) {
+    if (e->comm)
+        return fail(BCMPC_ERR_HIP, "team kernel: a workgroup team did not meet; with a communicator attached "
+                                   "the ranks cannot rerun the step alone");
+    if (!e->fb) {
+        bcmpc_config c = e->cfg;
+        c.kernel = BCMPC_KERNEL_AUTO;
+        c.precision = BCMPC_PREC_SPLIT_F16;
+        g_no_team = true;
+        int rc = bcmpc_create(&c, &e->fb);
+        if (rc == BCMPC_ERR_UNSUPPORTED) {               // split precision only on the team kernel: fp32
+            c.precision = BCMPC_PREC_FP32;
+            rc = bcmpc_create(&c, &e->fb);
+        }
+        g_no_team = false;
+        if (rc != BCMPC_OK) return rc;
     }
+    bcmpc_engine* f = e->fb;
+    if (!e->fb_wset || e->fb_wver != e->version) {
+        const auto& hc = e->hw_copy;
+        std::vector<const float*> k, b, g, be;
+        for (auto& v : hc.k) k.push_back(v.data());
+        for (auto& v : hc.b) b.push_back(v.data());
+        for (auto& v : hc.g) g.push_back(v.data());
+        for (auto& v : hc.beta) be.push_back(v.data());
+        bcmpc_weights w{};
+        w.kernels = k.data(); w.biases = b.data();
+        w.ln_gamma = hc.ln ? g.data() : nullptr; w.ln_beta = hc.ln ? be.data() : nullptr;
+        w.mean_obs = hc.st[0].data(); w.std_obs = hc.st[1].data(); w.mean_action = hc.st[2].data();
+        w.std_action = hc.st[3].data(); w.mean_deltas = hc.st[4].data(); w.std_deltas = hc.st[5].data();
+        w.mean_reward = hc.st[6].empty() ? nullptr : hc.st[6].data();
+        w.std_reward = hc.st[7].empty() ? nullptr : hc.st[7].data();
+        if (const int rc = bcmpc_set_weights(f, &w, e->version)) return rc;
+        e->fb_wver = e->version;
+        e->fb_wset = true;
+    }
+    if (e->PL > 0) {
+        if (!e->fb_pset || e->fb_pver != e->pol_version) {
+            const auto& hc = e->hp_copy;
+            std::vector<const float*> k, b;
+            for (auto& v : hc.k) k.push_back(v.data());
+            for (auto& v : hc.b) b.push_back(v.data());
+            const bcmpc_policy p{k.data(), b.data(), hc.pvec[0].data(), hc.pvec[1].data(), hc.pvec[2].data(),
+                                 e->explore};
+            if (const int rc = bcmpc_set_policy(f, &p, e->pol_version)) return rc;
+            e->fb_pver = e->pol_version;
+            e->fb_pset = true;
+        }
+        f->explore = e->explore;
+    }
+    if (e->reward)
+        if (const int rc = bcmpc_set_discount(f, e->gamma)) return rc;
+    double lo[BCMPC_MAX_ACTION], hi[BCMPC_MAX_ACTION];
+    for (int j = 0; j < e->cfg.action_dim; ++j) {
+        lo[j] = e->h_consts[6 * kConstCols + j];
+        hi[j] = e->h_consts[7 * kConstCols + j];
+    }
+    if (const int rc = bcmpc_set_action_bounds(f, lo, hi)) return rc;
+    f->timing = e->timing;
+    ++e->team_reruns;
+    return BCMPC_OK;
+}
+
+// Team launches of different streams on one device are serialised (stream-ordered, in this process):
+// two team grids running at once could each hold part of the CUs the other needs.  Single-stream use
+// pays nothing; from the second stream on, a launch on stream s waits for the previous team launch.
+static int team_stream_order(int device, hipStream_t st) {
+    struct Dev {
+        std::mutex mu;
+        hipStream_t last = nullptr;
+        bool seen = false, multi = false;
+        hipEvent_t ev = nullptr;
+    };
+    static Dev devs[64];
+    if (device < 0 || device >= 64) return BCMPC_OK;
+    Dev& d = devs[device];
+    std::lock_guard<std::mutex> lk(d.mu);
+    if (!d.seen) {
+        d.seen = true;
+        d.last = st;
+        return BCMPC_OK;
+    }
+    if (d.last == st) return BCMPC_OK;
+    hipStreamCaptureStatus cs0 = hipStreamCaptureStatusNone, cs1 = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs0);
+    (void)hipStreamIsCapturing(d.last, &cs1);
+    if (cs0 == hipStreamCaptureStatusNone && cs1 == hipStreamCaptureStatusNone) {
+        if (!d.ev) HIP_TRY(hipEventCreateWithFlags(&d.ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(d.ev, d.last));        // everything queued on the previous team stream so far
+        HIP_TRY(hipStreamWaitEvent(st, d.ev, 0));
+    }
+    d.multi = true;
+    d.last = st;
     return BCMPC_OK;
 }
 
@@ -1001,6 +1161,11 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.team_buf = e->d_team;
         a.team_ctl = e->d_team_ctl;
         a.team_err = e->d_team_err;
+        // BCMPC_TEAM_SPINS (tests): exchange polls before a member gives up; -1: give up at the first
+        // exchange (forces the fallback path)
+        const char* sv = std::getenv("BCMPC_TEAM_SPINS");
+        a.team_spins = sv && *sv ? std::max(-1, std::atoi(sv)) : 0;
+        if (const int rc = team_stream_order(c.device, st)) return rc;
         // diagnostics: TEAM_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_tst = nullptr;
         static size_t tst_n = 0;
@@ -1218,7 +1383,10 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
     } else {
         HIP_TRY(hipStreamSynchronize(e->stream));
     }
-    if (const int ts = team_status(e)) return ts;
+    if (team_failed(e)) {
+        if (const int fr = team_fallback(e)) return fr;
+        return bcmpc_get_action(e->fb, state, actions, seed, cand_offset, out, costs_out);
+    }
     *out = lean ? *e->h_result_map : *e->h_result;
     return BCMPC_OK;
 }
@@ -1427,7 +1595,11 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             if (rc != BCMPC_OK) return rc;
             if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
         }
-        if (const int ts = team_status(e)) return ts;
+        if (team_failed(e)) {                         // (NumPy's state not yet advanced)
+            if (const int fr = team_fallback(e)) return fr;
+            return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
+                                            out, costs_out);
+        }
         std::memcpy(mt_key, g.key, sizeof(g.key));
         *mt_pos = g.pos;
         *out = lean ? *e->h_result_map : *e->h_result;
@@ -1461,7 +1633,11 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             if (rc != BCMPC_OK) return rc;
             if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
         }
-        if (const int ts = team_status(e)) return ts;
+        if (team_failed(e)) {                         // (NumPy's state not yet advanced)
+            if (const int fr = team_fallback(e)) return fr;
+            return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
+                                            out, costs_out);
+        }
         std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
         *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];
         *out = lean ? *e->h_result_map : *e->h_result;
@@ -1532,7 +1708,11 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     const hipError_t se = hipStreamSynchronize(e->stream);
     if (rc != BCMPC_OK) return rc;
     if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
-    if (const int ts = team_status(e)) return ts;
+    if (team_failed(e)) {
+        if (const int fr = team_fallback(e)) return fr;
+        return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed, out,
+                                        costs_out);
+    }
     std::memcpy(mt_key, g.key, sizeof(g.key));      // NumPy's state advances only when the call succeeded
     *mt_pos = g.pos;
     *out = *e->h_result;
@@ -1615,6 +1795,11 @@ int bcmpc_cem_get_action(bcmpc_engine* e, const double* state, const bcmpc_cem* 
     if (rc != BCMPC_OK) return rc;
     const size_t ha = (size_t)c.horizon * c.action_dim;
     hipStream_t st = e->stream;
+    std::vector<double> mu0, sigma0;                   // (team engines: the inputs, for a rerun)
+    if (e->kernel == BCMPC_KERNEL_TEAM) {
+        mu0.assign(mu, mu + ha);
+        sigma0.assign(sigma, sigma + ha);
+    }
     HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(e->d_mu, mu, ha * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(e->d_sigma, sigma, ha * sizeof(double), hipMemcpyHostToDevice, st));
@@ -1637,7 +1822,12 @@ int bcmpc_cem_get_action(bcmpc_engine* e, const double* state, const bcmpc_cem* 
     HIP_TRY(hipMemcpyAsync(mu, e->d_mu, ha * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(sigma, e->d_sigma, ha * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (const int ts = team_status(e)) return ts;
+    if (team_failed(e)) {
+        if (const int fr = team_fallback(e)) return fr;
+        std::memcpy(mu, mu0.data(), ha * sizeof(double));
+        std::memcpy(sigma, sigma0.data(), ha * sizeof(double));
+        return bcmpc_cem_get_action(e->fb, state, p, seed, mu, sigma, out);
+    }
     *out = *e->h_result;
     return BCMPC_OK;
 }
@@ -1675,6 +1865,17 @@ int bcmpc_engine_set_comm(bcmpc_engine* e, bcmpc_comm* comm) {
     if (comm && e->cfg.cost == BCMPC_COST_NONE)
         return fail(BCMPC_ERR_ARG, "the exchange needs the fused objective (argmin records)");
     e->comm = comm;
+    return BCMPC_OK;
+}
+
+int bcmpc_engine_status(bcmpc_engine* e) {
+    if (!e) return fail(BCMPC_ERR_ARG, "null argument");
+    return team_status(e);
+}
+
+int bcmpc_engine_team_reruns(const bcmpc_engine* e, uint64_t* reruns) {
+    if (!e || !reruns) return fail(BCMPC_ERR_ARG, "null argument");
+    *reruns = e->team_reruns;
     return BCMPC_OK;
 }
 

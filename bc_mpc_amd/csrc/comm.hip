@@ -89,6 +89,13 @@ __global__ __launch_bounds__(64) void select_records_kernel(const bcmpc_result* 
 
 int comm_fail(int code, const std::string& msg) { return set_error(code, msg); }   // -> bcmpc_last_error()
 
+// the exchange's select (also bcmpc_select_results_async): "" or the launch error
+std::string launch_select_records(const bcmpc_result* recs, int n, int maximize, bcmpc_result* out, hipStream_t st) {
+    hipLaunchKernelGGL(select_records_kernel, dim3(1), dim3(64), 0, st, recs, n, maximize, out);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? std::string() : std::string("select_records_kernel: ") + hipGetErrorString(e);
+}
+
 }  // namespace
 
 }  // namespace bcmpc
@@ -109,13 +116,8 @@ int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream
         *err = std::string("ncclAllGather: ") + r.error_string(rc);
         return BCMPC_ERR_HIP;
     }
-    hipLaunchKernelGGL(select_records_kernel, dim3(1), dim3(64), 0, st, c->d_gather, c->nranks, maximize, d_result);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        *err = std::string("select_records_kernel: ") + hipGetErrorString(e);
-        return BCMPC_ERR_HIP;
-    }
-    return BCMPC_OK;
+    *err = launch_select_records(c->d_gather, c->nranks, maximize, d_result, st);
+    return err->empty() ? BCMPC_OK : BCMPC_ERR_HIP;
 }
 
 int comm_rank(const bcmpc_comm* c) { return c->rank; }
@@ -182,6 +184,16 @@ int bcmpc_select_results(const bcmpc_result* recs, int32_t n, int32_t maximize, 
     using namespace bcmpc;
     if (!recs || !out || n < 1) return comm_fail(BCMPC_ERR_ARG, "need n >= 1 records");
     *out = recs[select_index(recs, n, maximize)];
+    return BCMPC_OK;
+}
+
+int bcmpc_select_results_async(const bcmpc_result* d_recs, int32_t n, int32_t maximize, bcmpc_result* d_out,
+                               void* stream) {
+    using namespace bcmpc;
+    if (!d_recs || !d_out || n < 1 || n > 4096) return comm_fail(BCMPC_ERR_ARG, "need 1 <= n <= 4096 records");
+    if (d_out + 1 > d_recs && d_out < d_recs + n) return comm_fail(BCMPC_ERR_ARG, "d_out overlaps d_recs");
+    const std::string err = launch_select_records(d_recs, n, maximize, d_out, (hipStream_t)stream);
+    if (!err.empty()) return comm_fail(BCMPC_ERR_HIP, err);
     return BCMPC_OK;
 }
 

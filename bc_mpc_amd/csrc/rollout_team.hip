@@ -238,13 +238,13 @@ __device__ __forceinline__ void split_tiles(const f4 (&v)[NTL], int odd, h8 (&xh
 }  // namespace
 
 // LDS: consts | biases [2 or 3][HP] + 32 | LN gamma [2][HP], beta [2][HP] | slab [P][hi|lo][64] f4 |
-// column exchange [2 layers][NWV][16][2] | output partials [NWV][2][64] f4 | members' partials [T][2][64] f4 |
-// (policy, T == 1) the policy's output partials [NWV][64] f4 | action inputs [kTeamNch][16][16] (no policy) | policy biases + params, policy hidden->hidden weights
+// column exchange [2 layers][NWV][16][2] | output partials [NWV][2][64] f4 | members' partials [T][2][64] f4 +
+// the team's "gave up" word (16 B) | (policy, T == 1) the policy's output partials [NWV][64] f4 | action inputs [kTeamNch][16][16] (no policy) | policy biases + params, policy hidden->hidden weights
 // (PHP > 0; its first and output layers live in registers)
 __host__ __device__ constexpr int team_lds_bytes(int HP, int NWV, int T, int AK, bool RW = false, int PHP = 0,
                                                  int PL = 0, int pw_bytes = 0) {
     return param_bytes(RW ? 3 : 2, HP) + ((AK & 2) ? 4 * HP * 4 : 0) + (HP / 32) * 2048 + (AK ? 2 * NWV * 16 * 2 * 4 : 0) +
-           NWV * 2048 + (T > 1 ? T * 2048 : 0) + (PHP > 0 && T == 1 ? NWV * 1024 : 0) +
+           NWV * 2048 + (T > 1 ? T * 2048 + 16 : 0) + (PHP > 0 && T == 1 ? NWV * 1024 : 0) +
            (PHP > 0 ? pol_param_bytes(PL, PHP) + pw_bytes + kPolNch * 16 * 16 * 8 : kTeamNch * 16 * 16 * 4);
 }
 
@@ -320,7 +320,8 @@ void rollout_team(const RolloutArgs a) {
         f4* const parts = reinterpret_cast<f4*>(base + off);
         off += NWV * 2048;
         f4* const tot = reinterpret_cast<f4*>(base + off);
-        off += T > 1 ? T * 2048 : 0;
+        int* const tdead = reinterpret_cast<int*>(base + off + T * 2048);   // (T > 1) this member gave up
+        off += T > 1 ? T * 2048 + 16 : 0;
         f4* const pparts = PHP > 0 && T == 1 ? reinterpret_cast<f4*>(base + off) : parts;   // policy partials
         off += PHP > 0 && T == 1 ? NWV * 1024 : 0;
         float* const xas = reinterpret_cast<float*>(base + off);          // (no policy)
@@ -367,6 +368,8 @@ void rollout_team(const RolloutArgs a) {
                 }
         }
 
+        if constexpr (T > 1)
+            if (threadIdx.x == 0) *tdead = 0;
         if constexpr (PHP == 0)
             for (int i = threadIdx.x; i < kTeamNch * 16 * 16; i += blockDim.x)
                 if ((i & 15) >= A) xas[i] = 0.f;            // action slots past A stay zero (fill writes j < A)
@@ -519,7 +522,8 @@ void rollout_team(const RolloutArgs a) {
         float* const Bout = Bl + NB * HP;
         const int qc = RW ? (S - 16) >> 2 : 0;           // lane row holding the cost: dim 17 / reward row S
         gu64* const gb = (gu64*)a.team_buf;           // (global address space: never flat)
-        bool dead = false;                                // a team exchange timed out: finish without waiting
+        bool dead = false;                                // the team cannot meet: finish without waiting
+        const int spin_limit = a.team_spins != 0 ? a.team_spins : kTeamSpins;   // (-1: give up at once)
         f4 ot[2];                                         // the step's summed output layer (rows 16 v + 4 q + r)
         double gp = 0.0;                                  // (reward net) gamma**(h-1) for this step's tail
 
@@ -917,6 +921,10 @@ void rollout_team(const RolloutArgs a) {
                 // as granules {epoch, f32} at k * 64 + lane (k = 4 v + r); member (tm + o) % T's are
                 // collected by wave o % NWV; every partial lands in the LDS slot of its member
                 const unsigned ep = (gen << 10) + (unsigned)h + 1u;
+                // a member that gave up tags its granules of both parities with this launch's "dead" epoch
+                // (h + 1 <= H <= 1022 never reaches 1023), so its partners -- and a member that only becomes
+                // resident later -- give up at their next poll instead of spinning to their own limit
+                const unsigned dep = (gen << 10) | 1023u;
                 const size_t slot = ((size_t)col * 2 + (h & 1)) * T;
                 const int R = S + (RW ? 1 : 0);           // rows exchanged: delta rows (+ the reward row)
                 // (+ rows 24..27: the member's head statistics mean_d, M2_d, mean_r, M2_r, lane row q = 2)
@@ -929,7 +937,7 @@ void rollout_team(const RolloutArgs a) {
                     gu64* const mine = gb + (slot + tm) * 512;
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
-                        if (xrow(16 * (k >> 2) + 4 * q + (k & 3)))
+                        if (!dead && xrow(16 * (k >> 2) + 4 * q + (k & 3)))
                             __hip_atomic_store(mine + k * 64 + lane,
                                                ((unsigned long long)ep << 32) | __float_as_uint(mp[k >> 2][k & 3]),
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -944,7 +952,7 @@ void rollout_team(const RolloutArgs a) {
                     const gu64* const src = gb + (slot + t) * 512;
                     f4 got[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
                     for (int spins = 0; !dead; ++spins) {
-                        bool ok = true;
+                        bool ok = true, gone = false;
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
                             if (xrow(16 * (k >> 2) + 4 * q + (k & 3))) {
@@ -952,12 +960,26 @@ void rollout_team(const RolloutArgs a) {
                                     __hip_atomic_load(src + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 got[k >> 2][k & 3] = __uint_as_float((unsigned)xv);
                                 ok &= (unsigned)(xv >> 32) == ep;
+                                gone |= (unsigned)(xv >> 32) == dep;
                             }
-                        if (__all(ok)) break;
-                        if (spins >= kTeamSpins) {
+                        if (__all(ok) && spin_limit >= 0) break;
+                        if (__any(gone) || spins >= spin_limit) {
+                            // give up: raise the mapped error word (the host reruns the call on its fallback
+                            // engine), tell this member's other waves (LDS) and the team (dead tags)
                             dead = true;
-                            if (lane == 0 && a.team_err)
-                                __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            if (lane == 0) {
+                                *tdead = 1;
+                                if (a.team_err)
+                                    __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            }
+#pragma unroll
+                            for (int par = 0; par < 2; ++par) {
+                                gu64* const mine = gb + (((size_t)col * 2 + par) * T + tm) * 512;
+#pragma unroll
+                                for (int k = 0; k < 8; ++k)
+                                    __hip_atomic_store(mine + k * 64 + lane, (unsigned long long)dep << 32,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            }
                             break;
                         }
                         __builtin_amdgcn_s_sleep(1);
@@ -966,6 +988,7 @@ void rollout_team(const RolloutArgs a) {
                     tot[(t * 2 + 1) * 64 + lane] = got[1];
                 }
                 lds_barrier();                               // every member's partial in LDS
+                dead = dead || *tdead != 0;
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
                     ot[v] = tot[(0 * 2 + v) * 64 + lane];

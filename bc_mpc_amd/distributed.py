@@ -75,11 +75,12 @@ class LibraryComm:
 
 
 def use_library_comm(group=None) -> bool:
-    """The library exchanges the records itself under RCCL (backend "nccl"); BCMPC_LIBRARY_COMM=0
-    keeps the torch all-gather."""
+    """BCMPC_LIBRARY_COMM=1 (opt-in until a multi-GPU run has exercised it): the library exchanges the
+    records itself under RCCL (backend "nccl", csrc/comm.hip); by default the torch all-gather of the
+    records (allgather_minloc) carries the one exchange of a control step."""
     import os
     rank, ws = world(group)
-    if ws == 1 or os.environ.get("BCMPC_LIBRARY_COMM", "1") == "0":
+    if ws == 1 or os.environ.get("BCMPC_LIBRARY_COMM", "0") != "1":
         return False
     import torch.distributed as dist
     return dist.get_backend(group) == "nccl"

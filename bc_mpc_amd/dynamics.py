@@ -115,7 +115,9 @@ class NNDynamicsModel():
         d_traj = torch.empty((2, K, self.state_dim), dtype=torch.float64, device=dev)
         eng.rollout_async(d_s.data_ptr(), self.state_dim, d_a.data_ptr(), 0, 0, None, d_traj.data_ptr(), None,
                           torch.cuda.current_stream(dev).cuda_stream)
-        return d_traj[1].cpu().numpy()
+        out = d_traj[1].cpu().numpy()
+        eng.check_status()
+        return out
 
     def fit(self, data):  # dynamics.py:81-104
         """``iterations`` Adam steps on the GPU (bc_mpc_amd/fit.py, csrc/fit.hip) on batches drawn
@@ -232,7 +234,9 @@ class NNDynamicsRewardModel():
         d_r = torch.empty(K, dtype=torch.float64, device=dev)        # reward * gamma**0
         eng.rollout_async(d_s.data_ptr(), self.state_dim, d_a.data_ptr(), 0, 0, d_r.data_ptr(), d_traj.data_ptr(),
                           None, torch.cuda.current_stream(dev).cuda_stream)
-        return d_traj[1].cpu().numpy(), d_r.cpu().numpy().reshape(K, 1)
+        out = d_traj[1].cpu().numpy(), d_r.cpu().numpy().reshape(K, 1)
+        eng.check_status()
+        return out
 
     def fit(self, data):  # dynamics.py:179-223
         raise NotImplementedError("dynamics training is outside the rollout engine (SURVEY 8f rank 4); "

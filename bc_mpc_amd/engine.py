@@ -488,6 +488,20 @@ class RolloutEngine:
     def stream(self) -> int:
         return int(self._lib.bcmpc_stream(self._h) or 0)
 
+    def check_status(self) -> None:
+        """After the stream of a stream-ordered launch (rollout_async, rollout_policy_async,
+        cem_rollout_async) has completed: raise BcmpcError when a team-kernel launch of this engine
+        gave up because its workgroups could not all be resident (its outputs are not valid);
+        bcmpc_engine_status.  Synchronous calls rerun on a fallback engine instead."""
+        _lib.check(self._lib.bcmpc_engine_status(self._h))
+
+    @property
+    def team_reruns(self) -> int:
+        """Synchronous calls of this engine rerun on its fallback engine (bcmpc_engine_team_reruns)."""
+        n = ctypes.c_uint64()
+        _lib.check(self._lib.bcmpc_engine_team_reruns(self._h, ctypes.byref(n)))
+        return int(n.value)
+
     def set_timing(self, on: bool = True) -> None:
         """Bracket this engine's launches with HIP events (off by default: ~6 us per synchronous
         get_action at small K) so that last_kernel_ms() can read them (bcmpc_engine_set_timing)."""

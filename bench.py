@@ -389,9 +389,11 @@ def main():
                    "team": "rollout_team (weights in registers, one column per team of workgroups)"}.get(
         info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
     lib_comm = None
-    if world > 1 and backend == "nccl" and not wl.get("cem") and args.actions == "device":
-        # the library's own communicator: get_action all-gathers the ranks' result records over RCCL
-        # and selects on the device (csrc/comm.hip); torch.distributed only carried its RCCL id
+    if (world > 1 and backend == "nccl" and not wl.get("cem") and args.actions == "device"
+            and os.environ.get("BCMPC_LIBRARY_COMM", "0") == "1"):
+        # opt-in (BCMPC_LIBRARY_COMM=1): the library's own communicator -- get_action all-gathers the ranks'
+        # result records over RCCL and selects on the device (csrc/comm.hip); torch.distributed only carried
+        # its RCCL id.  Default: the torch all-gather of the records (allgather_minloc)
         lib_comm = bdist.LibraryComm(local)
         eng.set_comm(lib_comm)
     d_state = torch.from_numpy(state).to(dev)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BCMPC_ABI_VERSION 2
+#define BCMPC_ABI_VERSION 3
 #define BCMPC_MAX_LAYERS 8      /* hidden layers supported (dynamics.py:66 n_layers) */
 #define BCMPC_MAX_STATE 32      /* S: observation dim (HalfCheetah: 20, cheetah_env.py:21-27) */
 #define BCMPC_MAX_INPUT 32      /* S + A (dynamics.py:26 concat) */
@@ -381,9 +381,26 @@ int bcmpc_engine_set_comm(bcmpc_engine* eng, bcmpc_comm* comm);
 /* Host only: the np.argmin (maximize: np.argmax) winner of n result records, for hosts
  * that exchange the records themselves (e.g. MPI / gloo). */
 int bcmpc_select_results(const bcmpc_result* recs, int32_t n, int32_t maximize, bcmpc_result* out);
+/* The same select on the device, stream-ordered (the kernel the library's exchange runs after its
+ * all-gather): d_recs [n] records -> d_out (must not overlap d_recs), 1 <= n <= 4096. */
+int bcmpc_select_results_async(const bcmpc_result* d_recs, int32_t n, int32_t maximize, bcmpc_result* d_out,
+                               void* stream);
 
 /* Device stream the engine launches on (hipStream_t as void*). */
 void* bcmpc_stream(bcmpc_engine* eng);
+
+/* Small-K team kernel (bcmpc_engine_info kernel == BCMPC_KERNEL_TEAM): its workgroups wait for each
+ * other once per step, so they must all be resident.  A team that cannot meet within ~1 s (another
+ * process or kernel holding CUs) gives up and flags it; the synchronous entry points then rerun the
+ * call on a fallback engine of the same net (the split slab kernel, else the fp32 group kernel;
+ * not with a communicator attached: BCMPC_ERR_HIP).  Stream-ordered callers (bcmpc_rollout_async,
+ * bcmpc_rollout_policy_async, bcmpc_cem_rollout_async) call bcmpc_engine_status once their stream has
+ * completed: BCMPC_ERR_HIP when a launch of this engine since the last check gave up (its outputs
+ * are not valid), BCMPC_OK otherwise; reading clears the flag.  Team launches of one process on
+ * different streams of a device are serialised (stream-ordered) by the library. */
+int bcmpc_engine_status(bcmpc_engine* eng);
+/* number of synchronous calls of this engine rerun on the fallback engine */
+int bcmpc_engine_team_reruns(const bcmpc_engine* eng, uint64_t* reruns);
 
 /* Kernel timing (off by default): with on != 0 every launch chain of this engine is bracketed
  * by HIP event markers (~6 us per synchronous get_action at small K, measured), which
