@@ -129,6 +129,7 @@ class FitConfig(ctypes.Structure):
         ("beta1", ctypes.c_float),
         ("beta2", ctypes.c_float),
         ("epsilon", ctypes.c_float),
+        ("model", ctypes.c_int32),
     ]
 
 
@@ -189,6 +190,8 @@ SIGNATURES = [
     ("bcmpc_fit_run", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, _FP]),
     ("bcmpc_fit_last_error", ctypes.c_char_p, []),
+    ("bcmpc_fit_set_rewards", ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int64]),
+    ("bcmpc_fit_reward_losses", ctypes.c_int, [ctypes.c_void_p, _FP]),
     ("bcmpc_comm_unique_id", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint8)]),
     ("bcmpc_comm_init", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),

@@ -233,6 +233,7 @@ struct bcmpc_engine {
     uint64_t fb_wver = 0, fb_pver = 0;
     bool fb_wset = false, fb_pset = false;
     uint64_t team_reruns = 0;
+    bool sync_call = false;             // inside a synchronous entry point (its launches complete before it returns)
     struct HostNet {                    // the last bcmpc_set_weights / bcmpc_set_policy, copied
         std::vector<std::vector<float>> k, b, g, beta;
         std::vector<double> st[8];      // mean/std obs, action, deltas, reward
@@ -1001,36 +1002,53 @@ static int team_fallback(bcmpc_engine* e) {
     return BCMPC_OK;
 }
 
-// Team launches of different streams on one device are serialised (stream-ordered, in this process):
-// two team grids running at once could each hold part of the CUs the other needs.  Single-stream use
-// pays nothing; from the second stream on, a launch on stream s waits for the previous team launch.
-static int team_stream_order(int device, hipStream_t st) {
-    struct Dev {
-        std::mutex mu;
-        hipStream_t last = nullptr;
-        bool seen = false, multi = false;
-        hipEvent_t ev = nullptr;
-    };
-    static Dev devs[64];
+// Team launches of one process on a device are ordered across streams: two team grids running at
+// once could each hold part of the CUs the other needs.  A synchronous call's launch has completed
+// when the call returns (the host waits for its argmin), so only stream-ordered launches can still
+// be in flight: each records an event, and a team launch on another stream waits for it while it is
+// pending.  No call on the earlier stream is made later (it may be gone by then); graph capture
+// skips the ordering.
+struct TeamOrder {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;
+    hipStream_t ev_stream = nullptr;
+    bool pending = false;
+};
+static TeamOrder g_team_order[64];
+
+struct SyncCall {                                   // marks a synchronous entry point's launches
+    bcmpc_engine* e;
+    explicit SyncCall(bcmpc_engine* x) : e(x) { e->sync_call = true; }
+    ~SyncCall() { e->sync_call = false; }
+};
+
+static int team_order_before(int device, hipStream_t st) {
     if (device < 0 || device >= 64) return BCMPC_OK;
-    Dev& d = devs[device];
+    TeamOrder& d = g_team_order[device];
     std::lock_guard<std::mutex> lk(d.mu);
-    if (!d.seen) {
-        d.seen = true;
-        d.last = st;
+    if (!d.pending || d.ev_stream == st) return BCMPC_OK;
+    const hipError_t q = hipEventQuery(d.ev);
+    if (q == hipSuccess) {
+        d.pending = false;
         return BCMPC_OK;
     }
-    if (d.last == st) return BCMPC_OK;
-    hipStreamCaptureStatus cs0 = hipStreamCaptureStatusNone, cs1 = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs0);
-    (void)hipStreamIsCapturing(d.last, &cs1);
-    if (cs0 == hipStreamCaptureStatusNone && cs1 == hipStreamCaptureStatusNone) {
-        if (!d.ev) HIP_TRY(hipEventCreateWithFlags(&d.ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(d.ev, d.last));        // everything queued on the previous team stream so far
-        HIP_TRY(hipStreamWaitEvent(st, d.ev, 0));
-    }
-    d.multi = true;
-    d.last = st;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs == hipStreamCaptureStatusNone) HIP_TRY(hipStreamWaitEvent(st, d.ev, 0));
+    return BCMPC_OK;
+}
+
+static int team_order_after(int device, hipStream_t st) {
+    if (device < 0 || device >= 64) return BCMPC_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) return BCMPC_OK;
+    TeamOrder& d = g_team_order[device];
+    std::lock_guard<std::mutex> lk(d.mu);
+    if (!d.ev) HIP_TRY(hipEventCreateWithFlags(&d.ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(d.ev, st));
+    d.ev_stream = st;
+    d.pending = true;
     return BCMPC_OK;
 }
 
@@ -1165,7 +1183,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         // exchange (forces the fallback path)
         const char* sv = std::getenv("BCMPC_TEAM_SPINS");
         a.team_spins = sv && *sv ? std::max(-1, std::atoi(sv)) : 0;
-        if (const int rc = team_stream_order(c.device, st)) return rc;
+        if (const int rc = team_order_before(c.device, st)) return rc;
         // diagnostics: TEAM_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_tst = nullptr;
         static size_t tst_n = 0;
@@ -1182,6 +1200,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             a.stamps = d_tst;
         }
         HIP_TRY(launch_rollout_team(a, e->HP, st));
+        if (!e->sync_call)
+            if (const int rc = team_order_after(c.device, st)) return rc;
         if (stamps) {
             std::vector<uint64_t> h(blocks * nwv * 10);
             HIP_TRY(hipMemcpyAsync(h.data(), d_tst, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -1350,6 +1370,7 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
     const bcmpc_config& c = e->cfg;
     if (c.cost == BCMPC_COST_NONE) return fail(BCMPC_ERR_ARG, "get_action needs a fused objective (cheetah cost or learned reward)");
     HIP_TRY(hipSetDevice(c.device));
+    const SyncCall sync_guard(e);
     // one launch chain per control step: the state travels in the kernel arguments and the argmin
     // writes the result record straight into mapped host memory (a communicator all-gathers the
     // device record instead)
@@ -1550,6 +1571,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         return fail(BCMPC_ERR_ARG, "this engine's candidates must lie inside [0, k_global)");
     if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
     HIP_TRY(hipSetDevice(c.device));
+    const SyncCall sync_guard(e);
     const int64_t draw_words = 2 * (int64_t)c.action_dim * c.horizon * k_global;
     if (draw_words <= mt_zero_copy_words() && mt_device_path()) {
         // small draw: the host generates the shard's rows of every step into pinned memory (the
@@ -1791,6 +1813,7 @@ int bcmpc_cem_get_action(bcmpc_engine* e, const double* state, const bcmpc_cem* 
         return fail(BCMPC_ERR_ARG, "single-device CEM: k_global must be 0 or num_paths");
     if (c.num_paths == 0) return fail(BCMPC_ERR_EMPTY, "attempt to get argmin of an empty sequence");
     HIP_TRY(hipSetDevice(c.device));
+    const SyncCall sync_guard(e);
     int rc = cem_buffers(e, p->n_elite);
     if (rc != BCMPC_OK) return rc;
     const size_t ha = (size_t)c.horizon * c.action_dim;

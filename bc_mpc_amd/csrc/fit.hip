@@ -221,6 +221,23 @@ __global__ void fit_gather(const double* __restrict__ st, const double* __restri
     }
 }
 
+// NNDynamicsRewardModel: R[b] = (reward - mean_r) / (std_r + 1e-10) (f64, then f32: dynamics.py:203,
+// :210's [-1, 1] column); nc rows 6 / 7 hold mean_r / std_r + 1e-10
+__global__ void fit_gather_reward(const double* __restrict__ rw, const int64_t* __restrict__ idx_base, int stride,
+                                  const int32_t* __restrict__ iter, const double* __restrict__ nc,
+                                  float* __restrict__ R, int B) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int64_t r = (idx_base + (int64_t)(*iter) * stride)[b];
+    R[b] = (float)__ddiv_rn(__dsub_rn(rw[r], nc[6 * 32]), nc[7 * 32]);
+}
+
+// dst += src (the trunk's gradient: the sum (AddN) of the two heads' data gradients)
+__global__ void fit_add(float* __restrict__ dst, const float* __restrict__ src, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = dst[i] + src[i];
+}
+
 // ------------------------------------------------------------ row kernels ---
 // one wave per row of width F (<= 1024): act in place Z -> A; with LN, H = LN(A)
 // (tf.contrib.layers.layer_norm: nn.moments over the row, batch_normalization
@@ -351,11 +368,13 @@ __global__ __launch_bounds__(256) void fit_colsum(const float* __restrict__ X, f
     if (threadIdx.x == 0) tickets[blockIdx.x] = 0;       // ready for the next launch (stream order)
 }
 
-// loss = mean((T - P)^2) (one block), dP = -((2 * (1/N)) * (T - P))
+// loss = mean((T - P)^2) (one block), dP = -((2 * (1/N)) * (T - P)); tick: this call ends the
+// iteration's losses (advances the counter and the beta powers) -- the reward model's reward loss
+// runs first with tick = 0, its dynamics loss second
 __global__ __launch_bounds__(1024) void fit_loss(const float* __restrict__ P, const float* __restrict__ T,
                                                  float* __restrict__ dP, float* __restrict__ loss_base,
                                                  int32_t* __restrict__ iter, float* __restrict__ bp, float b1,
-                                                 float b2, int n) {
+                                                 float b2, int n, int tick = 1) {
     const int it = *iter;
     float* loss = loss_base + it;
     __shared__ float red[16];
@@ -373,6 +392,7 @@ __global__ __launch_bounds__(1024) void fit_loss(const float* __restrict__ P, co
         float t = 0.f;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
         *loss = t * inv;
+        if (!tick) return;
         // the previous iteration's end (TF1 _finish: beta powers *= beta), then the counter;
         // the iteration's Adam (after this kernel) reads bp = beta^(it+1)
         if (it > 0) {
@@ -906,6 +926,7 @@ struct bcmpc_fitter {
     int IN = 0, L = 0, h = 0, S = 0, A = 0, Bmax = 0;
     // flat parameters: per layer W_l [in][out], b_l [out]; then per hidden layer gamma, beta [h]
     std::vector<size_t> w_off, b_off, g_off, be_off;
+    std::vector<int> lin, lout;                   // per dense layer: in / out width
     size_t n_params = 0;
     float *d_w = nullptr, *d_m = nullptr, *d_v = nullptr, *d_g = nullptr;
     // activations: X0 [B][IN], per hidden layer Z/A [B][h] and H (LN out) [B][h], mean/rs [B]; P/T/dP [B][S]
@@ -935,6 +956,14 @@ struct bcmpc_fitter {
     FitTile* d_tiles = nullptr;
     int32_t ntiles = 0, rows_ld = 0;
     size_t rows_lds = 0;
+    // NNDynamicsRewardModel (cfg.model == BCMPC_MODEL_REWARD): parameters dense .. dense_4 (w/b_off[0..4]),
+    // LayerNorm trunk / delta / reward (g/be_off[0..2]); activation slots 0 trunk, 1 delta head, 2 reward head
+    bool rw = false;
+    float *d_r = nullptr, *d_pr = nullptr, *d_dpr = nullptr, *d_dh2 = nullptr, *d_loss2 = nullptr;
+    double* d_rwd = nullptr;                      // the buffer's rewards [n]
+    int64_t rw_cap = 0;
+    bool has_rewards = false;
+    int32_t last_iters = 0;                       // iterations of the last run (its reward losses in d_loss2)
 };
 
 extern "C" {
@@ -952,6 +981,10 @@ int bcmpc_fit_create(const bcmpc_fit_config* c, bcmpc_fitter** out) {
     if (c->activation != BCMPC_ACT_TANH && c->activation != BCMPC_ACT_RELU)
         return ffail(BCMPC_ERR_UNSUPPORTED, "activation must be tanh or relu");
     if (c->batch_size < 1) return ffail(BCMPC_ERR_ARG, "batch_size must be >= 1");
+    if (c->model != BCMPC_MODEL_DELTA && c->model != BCMPC_MODEL_REWARD) return ffail(BCMPC_ERR_ARG, "unknown model");
+    const bool rw = c->model == BCMPC_MODEL_REWARD;
+    if (rw && (c->n_layers != 2 || c->activation != BCMPC_ACT_TANH))
+        return ffail(BCMPC_ERR_UNSUPPORTED, "reward model: n_layers 2 (trunk + heads), tanh (dynamics.py:150-177)");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || c->device < 0 || c->device >= ndev)
         return ffail(BCMPC_ERR_ARG, "device ordinal out of range");
@@ -960,18 +993,26 @@ int bcmpc_fit_create(const bcmpc_fit_config* c, bcmpc_fitter** out) {
     f->cfg = *c;
     f->S = c->state_dim; f->A = c->action_dim; f->IN = f->S + f->A; f->L = c->n_layers; f->h = c->hidden;
     f->Bmax = c->batch_size;
+    f->rw = rw;
     size_t off = 0;
-    for (int l = 0; l <= f->L; ++l) {
-        const int in = l == 0 ? f->IN : f->h, o = l == f->L ? f->S : f->h;
+    const int nk = rw ? 5 : f->L + 1, nln = rw ? 3 : f->L;
+    for (int l = 0; l < nk; ++l) {
+        int in = l == 0 ? f->IN : f->h, o = l == f->L ? f->S : f->h;
+        if (rw) {                                         // dense, dense_1, dense_2, dense_3, dense_4
+            const int ro[5] = {f->h, f->h, f->S, f->h, 1};
+            o = ro[l];
+        }
         f->w_off.push_back(off); off += (size_t)in * o;
         f->b_off.push_back(off); off += o;
+        f->lin.push_back(in);
+        f->lout.push_back(o);
     }
-    for (int l = 0; l < f->L; ++l) {
+    for (int l = 0; l < nln; ++l) {
         f->g_off.push_back(off); off += f->h;
         f->be_off.push_back(off); off += f->h;
     }
     f->n_params = off;
-    const size_t B = (size_t)f->Bmax, H = (size_t)f->h, L = (size_t)f->L;
+    const size_t B = (size_t)f->Bmax, H = (size_t)f->h, L = (size_t)nln;   // (activation slots)
     auto al = [&](void** p, size_t bytes) { return hipMalloc(p, bytes > 0 ? bytes : 4) == hipSuccess; };
     bool ok = hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) == hipSuccess &&
               al((void**)&f->d_w, off * 4) && al((void**)&f->d_m, off * 4) && al((void**)&f->d_v, off * 4) &&
@@ -984,10 +1025,12 @@ int bcmpc_fit_create(const bcmpc_fit_config* c, bcmpc_fitter** out) {
               al((void**)&f->d_nc, kConstRows * kConstCols * 8) && al((void**)&f->d_iter, 4) &&
               al((void**)&f->d_bp, 8) &&
               al((void**)&f->d_cpart, (size_t)kColChunks * 2 * std::max(f->h, f->S) * 4) &&
-              al((void**)&f->d_tickets, 64 * 4);
+              al((void**)&f->d_tickets, 64 * 4) &&
+              (!rw || (al((void**)&f->d_r, B * 4) && al((void**)&f->d_pr, B * 4) && al((void**)&f->d_dpr, B * 4) &&
+                       al((void**)&f->d_dh2, B * H * 4)));
     if (!ok) { bcmpc_fit_destroy(f); return ffail(BCMPC_ERR_HIP, "device allocation failed"); }
     const char* fe = std::getenv("BCMPC_FIT_FUSED");
-    f->fused = !(fe && fe[0] == '0');
+    f->fused = !(fe && fe[0] == '0') && !rw;          // (the reward model: the per-op kernels, one graph)
     if (f->fused) {
         // LDS of fit_rows_kernel: bufA/B/C, targets, loss partials, K-split partials, row statistics,
         // then (when it fits) LayerNorm parameters and every hidden layer's activation rows
@@ -1039,7 +1082,8 @@ int bcmpc_fit_destroy(bcmpc_fitter* f) {
                     (void*)f->d_p, (void*)f->d_dp, (void*)f->d_act, (void*)f->d_hln, (void*)f->d_mean,
                     (void*)f->d_rs, (void*)f->d_dh, (void*)f->d_dz, (void*)f->d_loss, (void*)f->d_st,
                     (void*)f->d_ac, (void*)f->d_de, (void*)f->d_nc, (void*)f->d_idx, (void*)f->d_split,
-                    (void*)f->d_wt, (void*)f->d_dzs, (void*)f->d_lnpart, (void*)f->d_lpart, (void*)f->d_tiles})
+                    (void*)f->d_wt, (void*)f->d_dzs, (void*)f->d_lnpart, (void*)f->d_lpart, (void*)f->d_tiles,
+                    (void*)f->d_r, (void*)f->d_pr, (void*)f->d_dpr, (void*)f->d_dh2, (void*)f->d_loss2, (void*)f->d_rwd})
         if (p) (void)hipFree(p);
     if (f->stream) (void)hipStreamDestroy(f->stream);
     delete f;
@@ -1051,14 +1095,16 @@ int bcmpc_fit_set_params(bcmpc_fitter* f, const bcmpc_weights* w) {
     if (f->cfg.layer_norm && (!w->ln_gamma || !w->ln_beta)) return ffail(BCMPC_ERR_ARG, "LayerNorm params missing");
     if (!w->mean_obs || !w->std_obs || !w->mean_action || !w->std_action || !w->mean_deltas || !w->std_deltas)
         return ffail(BCMPC_ERR_ARG, "normalization stats missing");
+    if (f->rw && (!w->mean_reward || !w->std_reward)) return ffail(BCMPC_ERR_ARG, "mean_reward / std_reward missing");
     std::vector<float> hw(f->n_params, 0.f);
-    for (int l = 0; l <= f->L; ++l) {
-        const int in = l == 0 ? f->IN : f->h, o = l == f->L ? f->S : f->h;
+    const int nk = (int)f->w_off.size(), nln = (int)f->g_off.size();
+    for (int l = 0; l < nk; ++l) {
+        const size_t in = f->lin[l], o = f->lout[l];
         if (!w->kernels[l] || !w->biases[l]) return ffail(BCMPC_ERR_ARG, "null kernel / bias");
-        std::copy(w->kernels[l], w->kernels[l] + (size_t)in * o, hw.begin() + f->w_off[l]);
+        std::copy(w->kernels[l], w->kernels[l] + in * o, hw.begin() + f->w_off[l]);
         std::copy(w->biases[l], w->biases[l] + o, hw.begin() + f->b_off[l]);
     }
-    for (int l = 0; l < f->L; ++l) {
+    for (int l = 0; l < nln; ++l) {
         for (int i = 0; i < f->h; ++i) {
             hw[f->g_off[l] + i] = f->cfg.layer_norm ? w->ln_gamma[l][i] : 1.f;
             hw[f->be_off[l] + i] = f->cfg.layer_norm ? w->ln_beta[l][i] : 0.f;
@@ -1072,6 +1118,10 @@ int bcmpc_fit_set_params(bcmpc_fitter* f, const bcmpc_weights* w) {
         nc[3 * 32 + i] = i < f->A ? w->std_action[i] + 1e-10 : 1.0;
         nc[4 * 32 + i] = i < f->S ? w->mean_deltas[i] : 0.0;
         nc[5 * 32 + i] = i < f->S ? w->std_deltas[i] + 1e-10 : 1.0;
+    }
+    if (f->rw) {                                      // dynamics.py:203 normalize(reward, std_reward, mean_reward)
+        nc[6 * 32] = w->mean_reward[0];
+        nc[7 * 32] = w->std_reward[0] + 1e-10;
     }
     std::vector<float> hwt;
     if (f->fused) {                                   // W_l^T [out][in] at the same offsets (fit_rows_kernel)
@@ -1100,13 +1150,13 @@ int bcmpc_fit_get_params(bcmpc_fitter* f, float* const* kernels, float* const* b
         hipMemcpyAsync(hw.data(), f->d_w, hw.size() * 4, hipMemcpyDeviceToHost, f->stream) != hipSuccess ||
         hipStreamSynchronize(f->stream) != hipSuccess)
         return ffail(BCMPC_ERR_HIP, "parameter download failed");
-    for (int l = 0; l <= f->L; ++l) {
-        const int in = l == 0 ? f->IN : f->h, o = l == f->L ? f->S : f->h;
-        std::copy(hw.begin() + f->w_off[l], hw.begin() + f->w_off[l] + (size_t)in * o, kernels[l]);
-        std::copy(hw.begin() + f->b_off[l], hw.begin() + f->b_off[l] + o, biases[l]);
+    const int nk = (int)f->w_off.size(), nln = (int)f->g_off.size();
+    for (int l = 0; l < nk; ++l) {
+        std::copy(hw.begin() + f->w_off[l], hw.begin() + f->w_off[l] + (size_t)f->lin[l] * f->lout[l], kernels[l]);
+        std::copy(hw.begin() + f->b_off[l], hw.begin() + f->b_off[l] + f->lout[l], biases[l]);
     }
     if (f->cfg.layer_norm && ln_gamma && ln_beta)
-        for (int l = 0; l < f->L; ++l) {
+        for (int l = 0; l < nln; ++l) {
             std::copy(hw.begin() + f->g_off[l], hw.begin() + f->g_off[l] + f->h, ln_gamma[l]);
             std::copy(hw.begin() + f->be_off[l], hw.begin() + f->be_off[l] + f->h, ln_beta[l]);
         }
@@ -1160,7 +1210,104 @@ static int fit_iteration_fused(bcmpc_fitter* f, const int64_t* d_idx, int stride
     return BCMPC_OK;
 }
 
+// NNDynamicsRewardModel (dynamics.py:153-160, 195-219): loss_dynamic + loss_reward over the two-head net
+// (dynamics.py:165-177), the same per-op kernels as the delta net; the run is one captured graph
+//   forward : Z0 = X0 W0 + b0 -> tanh (+LN) = H0; per head: Z = H0 W + b -> tanh (+LN) = Hd / Hr;
+//             Pd = Hd W2 + b2 [B][S], Pr = Hr W4 + b4 [B][1]
+//   losses  : reward (tick 0, d_loss2) then dynamics (tick 1: ends the iteration)
+//   backward: per head (output grads, dH = dP Wo^T, LN / tanh backward, head weight grads, its data
+//             gradient into the trunk); dH0 = the delta head's + the reward head's (AddN); trunk
+//   adam    : every parameter
+static int fit_iteration_reward(bcmpc_fitter* f, const int64_t* d_idx, int stride, int B, float* d_loss) {
+    hipStream_t st = f->stream;
+    const int S = f->S, IN = f->IN, h = f->h, act = BCMPC_ACT_TANH, ln = f->cfg.layer_norm;
+    const size_t BH = (size_t)f->Bmax * h;
+    float* W = f->d_w;
+    float* G = f->d_g;
+#define FIT_TRY(x) do { if ((x) != hipSuccess) return ffail(BCMPC_ERR_HIP, #x); } while (0)
+    const int ng = B * (IN + S);
+    hipLaunchKernelGGL(fit_gather, dim3((ng + 255) / 256), dim3(256), 0, st, f->d_st, f->d_ac, f->d_de, d_idx,
+                       stride, f->d_iter, f->d_nc, f->d_x0, f->d_t, B, S, f->A);
+    FIT_TRY(hipGetLastError());
+    hipLaunchKernelGGL(fit_gather_reward, dim3((B + 255) / 256), dim3(256), 0, st, f->d_rwd, d_idx, stride,
+                       f->d_iter, f->d_nc, f->d_r, B);
+    FIT_TRY(hipGetLastError());
+    const dim3 rows((B + 3) / 4), rthreads(256);
+    auto slot_a = [&](int s) { return f->d_act + (size_t)s * BH; };
+    auto slot_h = [&](int s) { return ln ? f->d_hln + (size_t)s * BH : f->d_act + (size_t)s * BH; };
+    auto mean_of = [&](int s) { return f->d_mean + (size_t)s * f->Bmax; };
+    auto rs_of = [&](int s) { return f->d_rs + (size_t)s * f->Bmax; };
+    // ---- forward: trunk (slot 0, dense / LayerNorm), heads (slot 1: dense_1 / LayerNorm_1, slot 2: dense_3 /
+    //      LayerNorm_2) ----
+    auto hidden_layer = [&](const float* Hin, int in, int l, int s) -> int {
+        FIT_TRY((gemm<false, false>(Hin, W + f->w_off[l], slot_a(s), W + f->b_off[l], B, h, in, in, h, h, st)));
+        hipLaunchKernelGGL(fit_act_fwd, rows, rthreads, 0, st, slot_a(s), f->d_hln + (size_t)s * BH, mean_of(s),
+                           rs_of(s), W + f->g_off[s], W + f->be_off[s], B, h, act, ln);
+        FIT_TRY(hipGetLastError());
+        return BCMPC_OK;
+    };
+    if (int rc = hidden_layer(f->d_x0, IN, 0, 0)) return rc;
+    if (int rc = hidden_layer(slot_h(0), h, 1, 1)) return rc;
+    if (int rc = hidden_layer(slot_h(0), h, 3, 2)) return rc;
+    FIT_TRY((gemm<false, false>(slot_h(1), W + f->w_off[2], f->d_p, W + f->b_off[2], B, S, h, h, S, S, st)));
+    FIT_TRY((gemm<false, false>(slot_h(2), W + f->w_off[4], f->d_pr, W + f->b_off[4], B, 1, h, h, 1, 1, st)));
+    hipLaunchKernelGGL(fit_loss, dim3(1), dim3(1024), 0, st, f->d_pr, f->d_r, f->d_dpr, f->d_loss2, f->d_iter, f->d_bp,
+                       f->cfg.beta1, f->cfg.beta2, B, 0);
+    FIT_TRY(hipGetLastError());
+    hipLaunchKernelGGL(fit_loss, dim3(1), dim3(1024), 0, st, f->d_p, f->d_t, f->d_dp, d_loss, f->d_iter, f->d_bp,
+                       f->cfg.beta1, f->cfg.beta2, B * S, 1);
+    FIT_TRY(hipGetLastError());
+    // ---- backward ----
+    const int nch = std::max(1, std::min(kColChunks, B / 32));
+    // one head: its output layer lo (width o, dP) and hidden layer lh on activation slot s; its data
+    // gradient w.r.t. the trunk's output goes to dH0 (d_dh or d_dh2)
+    auto head = [&](int lo, int o, const float* dP, int lh, int s, float* dH0) -> int {
+        FIT_TRY((gemm<true, false>(slot_h(s), dP, G + f->w_off[lo], nullptr, h, o, B, h, o, o, st, f->d_split,
+                                   f->split_floats)));
+        hipLaunchKernelGGL(fit_colsum, dim3((o + 63) / 64, nch), dim3(256), 0, st, dP, G + f->b_off[lo], B, o, nullptr,
+                           nullptr, nullptr, nullptr, f->d_cpart, f->d_tickets);
+        FIT_TRY(hipGetLastError());
+        FIT_TRY((gemm<false, true>(dP, W + f->w_off[lo], f->d_dh, nullptr, B, h, o, o, o, h, st)));
+        if (ln)
+            hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64, nch), dim3(256), 0, st, f->d_dh, G + f->be_off[s], B, h,
+                               slot_a(s), mean_of(s), rs_of(s), G + f->g_off[s], f->d_cpart, f->d_tickets);
+        hipLaunchKernelGGL(fit_act_bwd, rows, rthreads, 0, st, f->d_dh, f->d_dz, slot_a(s), mean_of(s), rs_of(s),
+                           W + f->g_off[s], B, h, act, ln);
+        FIT_TRY(hipGetLastError());
+        FIT_TRY((gemm<true, false>(slot_h(0), f->d_dz, G + f->w_off[lh], nullptr, h, h, B, h, h, h, st, f->d_split,
+                                   f->split_floats)));
+        hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64, nch), dim3(256), 0, st, f->d_dz, G + f->b_off[lh], B, h,
+                           nullptr, nullptr, nullptr, nullptr, f->d_cpart, f->d_tickets);
+        FIT_TRY(hipGetLastError());
+        FIT_TRY((gemm<false, true>(f->d_dz, W + f->w_off[lh], dH0, nullptr, B, h, h, h, h, h, st)));
+        return BCMPC_OK;
+    };
+    if (int rc = head(2, S, f->d_dp, 1, 1, f->d_dh2)) return rc;     // delta head -> d_dh2
+    if (int rc = head(4, 1, f->d_dpr, 3, 2, f->d_dz)) return rc;     // reward head -> d_dz (its last use)
+    hipLaunchKernelGGL(fit_add, dim3((B * h + 255) / 256), dim3(256), 0, st, f->d_dh2, f->d_dz, B * h);
+    FIT_TRY(hipGetLastError());
+    // trunk: dH0 (d_dh2) -> LN / tanh backward -> dense's gradients
+    if (ln)
+        hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64, nch), dim3(256), 0, st, f->d_dh2, G + f->be_off[0], B, h,
+                           slot_a(0), mean_of(0), rs_of(0), G + f->g_off[0], f->d_cpart, f->d_tickets);
+    hipLaunchKernelGGL(fit_act_bwd, rows, rthreads, 0, st, f->d_dh2, f->d_dz, slot_a(0), mean_of(0), rs_of(0),
+                       W + f->g_off[0], B, h, act, ln);
+    FIT_TRY(hipGetLastError());
+    FIT_TRY((gemm<true, false>(f->d_x0, f->d_dz, G + f->w_off[0], nullptr, IN, h, B, IN, h, h, st, f->d_split,
+                               f->split_floats)));
+    hipLaunchKernelGGL(fit_colsum, dim3((h + 63) / 64, nch), dim3(256), 0, st, f->d_dz, G + f->b_off[0], B, h,
+                       nullptr, nullptr, nullptr, nullptr, f->d_cpart, f->d_tickets);
+    FIT_TRY(hipGetLastError());
+    const int64_t n = (int64_t)f->n_params;
+    hipLaunchKernelGGL(fit_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, f->d_m, f->d_v, G, n,
+                       f->d_bp, f->cfg.learning_rate, f->cfg.beta1, f->cfg.beta2, f->cfg.epsilon);
+    FIT_TRY(hipGetLastError());
+#undef FIT_TRY
+    return BCMPC_OK;
+}
+
 static int fit_iteration(bcmpc_fitter* f, const int64_t* d_idx, int stride, int B, float* d_loss) {
+    if (f->rw) return fit_iteration_reward(f, d_idx, stride, B, d_loss);
     if (f->fused) return fit_iteration_fused(f, d_idx, stride, B, d_loss);
     hipStream_t st = f->stream;
     const int S = f->S, IN = f->IN, L = f->L, h = f->h, act = f->cfg.activation, ln = f->cfg.layer_norm;
@@ -1231,6 +1378,7 @@ int bcmpc_fit_run(bcmpc_fitter* f, const int64_t* indices, const int32_t* batch_
                   float* losses) {
     if (!f || !indices || !batch_sizes || iterations < 0) return ffail(BCMPC_ERR_ARG, "null argument");
     if (!f->has_weights) return ffail(BCMPC_ERR_STATE, "bcmpc_fit_set_params has not been called");
+    if (f->rw && !f->has_rewards) return ffail(BCMPC_ERR_STATE, "reward model: bcmpc_fit_set_rewards has not been called");
     if (hipSetDevice(f->cfg.device) != hipSuccess) return ffail(BCMPC_ERR_HIP, "hipSetDevice failed");
     int64_t total = 0;
     for (int i = 0; i < iterations; ++i) {
@@ -1251,10 +1399,11 @@ int bcmpc_fit_run(bcmpc_fitter* f, const int64_t* indices, const int32_t* batch_
         hipMemcpyAsync(f->d_idx, indices, (size_t)total * 8, hipMemcpyHostToDevice, f->stream) != hipSuccess)
         return ffail(BCMPC_ERR_HIP, "index upload failed");
     if (iterations > f->loss_cap) {
-        if (f->d_loss) (void)hipFree(f->d_loss);
-        f->d_loss = nullptr;
+        for (float** p : {&f->d_loss, &f->d_loss2})
+            if (*p) { (void)hipFree(*p); *p = nullptr; }
         f->loss_cap = 0;
-        if (hipMalloc(&f->d_loss, (size_t)iterations * 4) != hipSuccess)
+        if (hipMalloc(&f->d_loss, (size_t)iterations * 4) != hipSuccess ||
+            (f->rw && hipMalloc(&f->d_loss2, (size_t)iterations * 4) != hipSuccess))
             return ffail(BCMPC_ERR_HIP, "loss buffer allocation failed");
         f->loss_cap = iterations;
     }
@@ -1310,6 +1459,36 @@ int bcmpc_fit_run(bcmpc_fitter* f, const int64_t* indices, const int32_t* batch_
         hipMemcpyAsync(losses, f->d_loss, (size_t)iterations * 4, hipMemcpyDeviceToHost, f->stream) != hipSuccess)
         return ffail(BCMPC_ERR_HIP, "loss download failed");
     if (hipStreamSynchronize(f->stream) != hipSuccess) return ffail(BCMPC_ERR_HIP, "fit failed");
+    f->last_iters = iterations;
+    return BCMPC_OK;
+}
+
+int bcmpc_fit_set_rewards(bcmpc_fitter* f, const double* rewards, int64_t n) {
+    if (!f || (n > 0 && !rewards) || n < 0) return ffail(BCMPC_ERR_ARG, "bad argument");
+    if (!f->rw) return ffail(BCMPC_ERR_STATE, "the fitter was created for the delta model (config.model)");
+    if (n != f->n_data) return ffail(BCMPC_ERR_ARG, "rewards: one per row of bcmpc_fit_set_data");
+    if (hipSetDevice(f->cfg.device) != hipSuccess) return ffail(BCMPC_ERR_HIP, "hipSetDevice failed");
+    if (n > f->rw_cap) {
+        if (f->d_rwd) (void)hipFree(f->d_rwd);
+        f->d_rwd = nullptr;
+        f->rw_cap = 0;
+        if (hipMalloc(&f->d_rwd, (size_t)std::max<int64_t>(n, 1) * 8) != hipSuccess)
+            return ffail(BCMPC_ERR_HIP, "reward buffer allocation failed");
+        f->rw_cap = n;
+    }
+    if (n > 0 && (hipMemcpyAsync(f->d_rwd, rewards, (size_t)n * 8, hipMemcpyHostToDevice, f->stream) != hipSuccess ||
+                  hipStreamSynchronize(f->stream) != hipSuccess))
+        return ffail(BCMPC_ERR_HIP, "reward upload failed");
+    f->has_rewards = true;
+    return BCMPC_OK;
+}
+
+int bcmpc_fit_reward_losses(bcmpc_fitter* f, float* losses) {
+    if (!f || !losses) return ffail(BCMPC_ERR_ARG, "null argument");
+    if (!f->rw) return ffail(BCMPC_ERR_STATE, "the fitter was created for the delta model (config.model)");
+    if (f->last_iters > 0 &&
+        (hipMemcpy(losses, f->d_loss2, (size_t)f->last_iters * 4, hipMemcpyDeviceToHost) != hipSuccess))
+        return ffail(BCMPC_ERR_HIP, "loss download failed");
     return BCMPC_OK;
 }
 

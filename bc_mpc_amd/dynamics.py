@@ -238,6 +238,31 @@ class NNDynamicsRewardModel():
         eng.check_status()
         return out
 
-    def fit(self, data):  # dynamics.py:179-223
-        raise NotImplementedError("dynamics training is outside the rollout engine (SURVEY 8f rank 4); "
-                                  "fit elsewhere and call load_weights()")
+    def fit(self, data):  # dynamics.py:195-219
+        """``iterations`` Adam steps on the GPU (bc_mpc_amd/fit.py, csrc/fit.hip, model "reward") on the
+        sum loss_dynamic + loss_reward (dynamics.py:153-157), batches drawn exactly as
+        DataBufferGeneral.sample draws them; returns the last step's (model_loss, reward_loss) like the
+        reference (:219)."""
+        import torch
+        from .fit import GPUFitter, buffer_arrays_reward, sample_batches
+        dev = self.device if self.device is not None else torch.cuda.current_device()
+        if getattr(self, "_fitter", None) is None:
+            self._fitter = GPUFitter(self.state_dim, self.action_dim, self.size, 2, "tanh", self.layer_norm,
+                                     int(self.batch_size), float(self.learning_rate), dev, model="reward")
+            self._fit_version = None
+        if self._fit_version != self.version:               # weights changed outside fit: re-upload
+            self._fitter.set_params(self.mlp_spec(), self.normalization())
+        states, actions, rewards, deltas = buffer_arrays_reward(data)
+        self._fitter.set_data(states, actions, deltas)
+        self._fitter.set_rewards(rewards)
+        size = int(getattr(data, "size", states.shape[0]))
+        print("Model fitting for ", self.iterations, "times ... ")   # dynamics.py:185
+        iters = int(self.iterations)
+        losses = self._fitter.run(sample_batches(size, int(self.batch_size), iters))
+        rlosses = self._fitter.reward_losses(iters)
+        ks, bs, gs, bes = self._fitter.get_params()
+        self.load_weights(ks, bs, gs if self.layer_norm else None, bes if self.layer_norm else None)
+        self._fit_version = self.version
+        if not iters:
+            return None, None
+        return float(losses[-1]), float(rlosses[-1])

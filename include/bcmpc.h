@@ -335,6 +335,9 @@ typedef struct bcmpc_fit_config {
     int32_t device;
     float learning_rate;   /* dynamics.py:47 */
     float beta1, beta2, epsilon;   /* tf.train.AdamOptimizer defaults 0.9, 0.999, 1e-8 */
+    int32_t model;         /* bcmpc_model: BCMPC_MODEL_REWARD fits NNDynamicsRewardModel (dynamics.py:153-160,
+                              195-219: loss_dynamic + loss_reward over the two-head net; n_layers 2, tanh;
+                              kernels / biases dense .. dense_4, LayerNorm trunk / delta / reward) */
 } bcmpc_fit_config;
 
 typedef struct bcmpc_fitter bcmpc_fitter;
@@ -352,6 +355,11 @@ int bcmpc_fit_set_data(bcmpc_fitter* f, const double* states, const double* acti
  * losses (optional, host, [iterations]) = each step's loss before its update */
 int bcmpc_fit_run(bcmpc_fitter* f, const int64_t* indices, const int32_t* batch_sizes, int32_t iterations,
                   float* losses);
+/* reward model: the buffer's rewards (one f64 per row of bcmpc_fit_set_data; normalised with
+ * mean_reward / std_reward of bcmpc_fit_set_params, dynamics.py:203); after a run, its per-step
+ * reward losses ([iterations], before each update; bcmpc_fit_run's losses are the dynamics losses) */
+int bcmpc_fit_set_rewards(bcmpc_fitter* f, const double* rewards, int64_t n);
+int bcmpc_fit_reward_losses(bcmpc_fitter* f, float* losses);
 const char* bcmpc_fit_last_error(void);
 
 /* ------------------------------------------------------------------------

@@ -13,6 +13,8 @@ import ctypes
 import numpy as np
 import pytest
 
+from conftest import ENV_PLAIN
+
 pytestmark = pytest.mark.gpu
 
 ATOL, RTOL = 1e-4, 1e-5
@@ -33,11 +35,12 @@ def _result(raw, A):
     return int(raw[:8].view(np.int64)[0]), float(raw[8:16].view(np.float64)[0]), raw[16:16 + 8 * A].view(np.float64)
 
 
-def _close(got, want, near=None, label=""):
+def _close(got, want, near=None, label="", env=ENV_PLAIN):
+    """The stated tolerance AND the achieved envelope ``env`` (conftest.envelope)."""
     assert np.array_equal(np.isnan(got), np.isnan(want))
     ok = ~np.isnan(want)
     d = np.abs(got[ok] - want[ok])
-    tol = ATOL + RTOL * np.abs(want[ok])
+    tol = np.minimum(ATOL + RTOL * np.abs(want[ok]), env)
     bad = d > tol
     if near is not None:
         bad &= ~(near[ok] & (np.abs(d - 10.0 * np.round(d / 10.0)) <= tol))

@@ -17,7 +17,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import Golden, golden_names
+from conftest import ENV_PLAIN, ENV_WIDE, Golden, envelope, golden_names
 
 pytestmark = pytest.mark.gpu
 
@@ -61,13 +61,15 @@ def _engine(g: Golden, K=None, H=None, cost="cheetah", kernel="auto"):
     return eng
 
 
-def assert_costs_close(got, want, near=None, label=""):
+def assert_costs_close(got, want, near=None, label="", env=ENV_PLAIN):
+    """The stated tolerance AND the achieved envelope ``env`` (conftest.envelope), except exact +-10
+    flips of near-threshold candidates."""
     assert got.shape == want.shape
     nan_g, nan_w = np.isnan(got), np.isnan(want)
     assert np.array_equal(nan_g, nan_w), f"{label}: NaN pattern differs"
     ok = ~nan_w
     diff = np.abs(got[ok] - want[ok])
-    tol = ATOL + RTOL * np.abs(want[ok])
+    tol = np.minimum(ATOL + RTOL * np.abs(want[ok]), env)
     bad = diff > tol
     if near is not None:
         nr = near[ok]
@@ -99,7 +101,8 @@ def test_engine_matches_reference_fixture(name, kernel):
     else:
         res = eng.get_action(g.state, g.actions(), return_costs=True)
         offset = 0
-    assert_costs_close(res.costs, g.costs, g.near, f"{name}/{kernel}")
+    assert_costs_close(res.costs, g.costs, g.near, f"{name}/{kernel}",
+                       env=envelope(g.meta["ln"], g.weights.n_layers, g.meta["hidden"], g.H))
     assert res.best_index - offset == int(np.argmin(res.costs))
     if argmin_is_decidable(g):
         assert res.best_index - offset == g.argmin
@@ -294,7 +297,8 @@ def test_large_hidden_vs_oracle(hidden, L, act, ln, kernel):
     eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), norm, 1)
     res = eng.get_action(state, acts, return_costs=True)
     want, states = orc.rollout(orc.NumpyDynamics(w, norm), state, acts)
-    assert_costs_close(res.costs, want, orc.near_threshold_mask(states), f"h{hidden}xL{L}/{kernel}")
+    assert_costs_close(res.costs, want, orc.near_threshold_mask(states), f"h{hidden}xL{L}/{kernel}",
+                       env=envelope(ln, L, hidden, H))
     assert res.best_index == int(np.argmin(res.costs))
 
 
@@ -349,7 +353,8 @@ def test_policy_engine_matches_reference_fixture(name, kernel):
     rs = np.random.RandomState(g.meta["seed"])
     expl = rs.uniform(g.low, g.high, size=[g.H, g.K, g.A])
     res = eng.get_action(g.state, expl, return_costs=True)
-    assert_costs_close(res.costs, g.costs, g.near, f"{name}/{kernel}")
+    assert_costs_close(res.costs, g.costs, g.near, f"{name}/{kernel}",
+                       env=envelope(w.layer_norm, w.n_layers, w.hidden, g.H))
     fa = eng.first_actions()
     err = np.abs(fa - g.z["first_actions"])
     print(f"[{name}] max|dfirst_action|={err.max():.3e}")

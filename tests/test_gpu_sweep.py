@@ -8,6 +8,7 @@ of the same draws (oracle.device_rng_actions)."""
 import numpy as np
 import pytest
 
+from conftest import ENV_PLAIN, envelope
 from oracle import mpc_oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -21,9 +22,10 @@ DELTA = [  # (K, H, hidden, L, kernel)
 ]
 
 
-def _check(costs, want, near, best_index, first, actions_h0, label):
+def _check(costs, want, near, best_index, first, actions_h0, label, env=ENV_PLAIN):
+    """The stated tolerance AND the achieved envelope ``env`` (conftest.envelope)."""
     d = np.abs(costs - want)
-    tol = ATOL + RTOL * np.abs(want)
+    tol = np.minimum(ATOL + RTOL * np.abs(want), env)
     bad = d > tol
     bad &= ~(near & (np.abs(d - 10.0 * np.round(d / 10.0)) <= tol))
     print(f"[{label}] max|dcost|={np.nanmax(d) if d.size else 0:.2e}")
@@ -51,7 +53,8 @@ def test_split_delta_shapes(K, H, hidden, L, kernel):
     dyn = orc.NumpyDynamics(w, norm)
     want, paths = orc.rollout(dyn, state, ap)
     near = orc.near_threshold_mask(paths)
-    _check(res.costs, want, near, res.best_index - 5, res.first_action, ap[0], f"{kernel} K{K} H{H} {L}x{hidden}")
+    _check(res.costs, want, near, res.best_index - 5, res.first_action, ap[0], f"{kernel} K{K} H{H} {L}x{hidden}",
+           env=envelope(False, L, hidden, H))
     eng.close()
 
 
@@ -102,5 +105,5 @@ def test_split_relu_layernorm_shapes(K, H, hidden, L, act, ln, kernel):
     want, paths = orc.rollout(orc.NumpyDynamics(w, norm), state, ap)
     near = orc.near_threshold_mask(paths)
     _check(res.costs, want, near, res.best_index - 3, res.first_action, ap[0],
-           f"{kernel} {act}{'+LN' if ln else ''} K{K} H{H} {L}x{hidden}")
+           f"{kernel} {act}{'+LN' if ln else ''} K{K} H{H} {L}x{hidden}", env=envelope(ln, L, hidden, H))
     eng.close()

@@ -18,6 +18,7 @@ import ctypes
 import numpy as np
 import pytest
 
+from conftest import ENV_WIDE
 from test_gpu_parity import assert_costs_close
 
 pytestmark = pytest.mark.gpu
@@ -127,7 +128,7 @@ def test_cfg5_cem_full_size_pinned_to_oracle():
         costs = d_costs.cpu().numpy()
         acts = orc.cem_actions(seed, it, 0, K, H, mu_in, sd_in, low, high, index=sample)
         want, states = orc.rollout(dyn, state, acts)
-        assert_costs_close(costs[sample], want, orc.near_threshold_mask(states), f"cfg5 it{it}")
+        assert_costs_close(costs[sample], want, orc.near_threshold_mask(states), f"cfg5 it{it}", env=ENV_WIDE)
         all_costs.append(costs)
         eng.select_async(None, d_costs.data_ptr(), K, 0, E, d_el.data_ptr(), d_cnt.data_ptr(), st)
         rec = d_el.cpu().numpy().view(ELITE)
