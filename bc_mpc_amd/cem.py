@@ -26,6 +26,8 @@ from __future__ import annotations
 import ctypes
 from typing import Optional
 
+import math
+
 import numpy as np
 
 from . import _lib
@@ -130,7 +132,7 @@ class CEMcontroller(Controller):
         return self._engine
 
     def get_action(self, state):
-        S = int(np.prod(self.env.observation_space.shape))
+        S = int(math.prod(self.env.observation_space.shape))
         A = len(self.env.action_space.high)
         K = int(self.num_simulated_paths)
         if self.horizon < 1:

@@ -36,6 +36,7 @@ The siblings run on the same engine:
 from __future__ import annotations
 
 import copy
+import math
 import os
 from typing import Optional
 
@@ -120,6 +121,8 @@ def _minloc(ctrl, eng, valid, cost, index, first, A):
     """The ranks' agreement on (cost, index, first action): already made inside the library when the
     engine that ran THIS step (``eng``: None when this rank launched nothing) has a communicator, else
     one torch all-gather of the records."""
+    if valid and _dist.world(ctrl._group)[1] == 1:      # one rank: nothing to agree on
+        return float(cost), int(index), np.array(first, dtype=np.float64)
     if eng is not None and getattr(eng, "comm", None) is not None:
         return float(cost), int(index), np.asarray(first, dtype=np.float64).copy()
     return _dist.allgather_minloc(valid, cost, index, first, A, ctrl._group, device=_comm_device(ctrl))
@@ -171,7 +174,7 @@ class MPCcontroller(Controller):
 
     # ------------------------------------------------------------------ engine
     def _dims(self):
-        S = int(np.prod(self.env.observation_space.shape))
+        S = int(math.prod(self.env.observation_space.shape))
         A = len(self.env.action_space.high)
         return S, A
 
@@ -359,7 +362,7 @@ class MPCcontrollerPolicyNet(Controller):
 
     # controllers.py:189-237
     def get_action(self, state):
-        S = int(np.prod(self.env.observation_space.shape))
+        S = int(math.prod(self.env.observation_space.shape))
         A = len(self.env.action_space.high)
         K = int(self.num_simulated_paths)
         if self.horizon < 1:
@@ -494,7 +497,7 @@ class MPCcontrollerReward(Controller):
 
     # controllers.py:121-158
     def get_action(self, state):
-        S = int(np.prod(self.env.observation_space.shape))
+        S = int(math.prod(self.env.observation_space.shape))
         A = len(self.env.action_space.high)
         K = int(self.num_simulated_paths)
         if self.horizon < 1:
@@ -639,7 +642,7 @@ class MCTScontrollerPolicyNetReward(Controller):
     # controllers.py:397-457
     def get_action(self, state):
         import torch
-        S = int(np.prod(self.env.observation_space.shape))
+        S = int(math.prod(self.env.observation_space.shape))
         A = len(self.env.action_space.high)
         N, R = int(self.num_first_stage_actions), int(self.random_path_per_action)
         state = np.asarray(state, dtype=np.float64).reshape(-1)

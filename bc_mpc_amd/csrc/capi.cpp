@@ -7,8 +7,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -167,8 +169,25 @@ struct bcmpc_engine {
     double* d_state = nullptr;
     double* d_actions = nullptr; size_t actions_cap = 0;
     double* h_stage = nullptr; size_t stage_cap = 0;   // pinned [H, K, A] staging (bcmpc_get_action_mt19937)
-    double* h_zc = nullptr; size_t zc_cap = 0;   // small NumPy-stream draws: fine-grained (coherent) pinned rows
-    double* d_zc = nullptr;             // ... and their device address (the kernel reads them over the bus)
+    // small NumPy-stream draws: two fine-grained (coherent) pinned row buffers and their device addresses
+    // (the kernel reads them over the bus); a call uses one while the pre-draw worker fills the other
+    double* h_zc[2] = {nullptr, nullptr}; size_t zc_cap = 0;
+    double* d_zc[2] = {nullptr, nullptr};
+    int zc_last = 0;                    // the buffer the last successful call read
+    // pre-draw (BCMPC_MT_PREDRAW, default on): after a successful small draw, a worker thread draws the
+    // rows the NEXT call would draw -- from NumPy's advanced state, same bounds / shard -- into the other
+    // buffer; the next call uses them only if NumPy's state is still exactly that state
+    struct PreDraw {
+        std::thread th;
+        std::mutex mu;
+        std::condition_variable cv;
+        bool quit = false, pending = false, busy = false, ready = false;
+        Mt19937 from, to;               // the state the rows were drawn from / leave behind
+        std::vector<double> low, high;
+        int64_t kg = 0, off = 0;
+        int buf = 0;
+        uint64_t hits = 0, misses = 0;
+    } pre;
     double* d_costs = nullptr;
     bcmpc_result* d_result = nullptr;
     double* d_amin_c = nullptr;         // argmin scratch: per-block best
@@ -563,7 +582,16 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (e->h_team_err) (void)hipHostFree(e->h_team_err);
     if (e->h_done) (void)hipHostFree(e->h_done);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
-    if (e->h_zc) (void)hipHostFree(e->h_zc);
+    if (e->pre.th.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(e->pre.mu);
+            e->pre.quit = true;
+        }
+        e->pre.cv.notify_all();
+        e->pre.th.join();
+    }
+    for (double* p : e->h_zc)
+        if (p) (void)hipHostFree(p);
     if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1439,6 +1467,67 @@ static int mt_splits(int cj) {
 // 227 words per LDS-synchronised step) and copies cost more than the host's ~0.5 ns per word.  2^16:
 // the reference's K = 400 steps (33.6k words at H = 7); a K = 1000 x 15 draw (180k) is faster on the
 // device with 2^14-word chunks (0.223 vs 0.250 ms per drop-in get_action)
+// ---- pre-draw worker (small NumPy-stream draws) ----
+static bool mt_predraw_enabled() {
+    static const bool on = [] {
+        const char* v = std::getenv("BCMPC_MT_PREDRAW");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
+// wait until the worker is idle (its buffer complete); returns the buffer index it last filled
+static int predraw_wait(bcmpc_engine* e) {
+    std::unique_lock<std::mutex> lk(e->pre.mu);
+    e->pre.cv.wait(lk, [&] { return !e->pre.pending && !e->pre.busy; });
+    return e->pre.buf;
+}
+
+// rows [H][shard] of the draw that starts at NumPy state `from`, into the buffer the last call did not read
+static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low, const double* high, int A,
+                         int64_t k_global, int64_t cand_offset) {
+    auto& p = e->pre;
+    {
+        std::lock_guard<std::mutex> lk(p.mu);
+        p.from = from;
+        p.low.assign(low, low + A);
+        p.high.assign(high, high + A);
+        p.kg = k_global;
+        p.off = cand_offset;
+        p.buf = e->zc_last ^ 1;
+        p.ready = false;
+        p.pending = true;
+    }
+    if (!p.th.joinable()) {
+        p.th = std::thread([e] {
+            auto& q = e->pre;
+            const bcmpc_config& c = e->cfg;
+            std::unique_lock<std::mutex> lk(q.mu);
+            for (;;) {
+                q.cv.wait(lk, [&] { return q.quit || q.pending; });
+                if (q.quit) return;
+                q.pending = false;
+                q.busy = true;
+                Mt19937 g = q.from;
+                const std::vector<double> lo = q.low, hi = q.high;
+                const int64_t kg = q.kg, off = q.off;
+                double* dst = e->h_zc[q.buf];
+                lk.unlock();
+                const int64_t K = c.num_paths;
+                const size_t row = (size_t)K * c.action_dim;
+                for (int h = 0; h < c.horizon; ++h)
+                    mt_uniform_rows(g, lo.data(), hi.data(), c.action_dim, kg, off, off + K, dst + h * row);
+                lk.lock();
+                q.to = g;
+                q.ready = true;
+                q.busy = false;
+                q.cv.notify_all();
+            }
+        });
+    }
+    p.cv.notify_all();
+}
+
 static int64_t mt_zero_copy_words() {
     const char* v = std::getenv("BCMPC_MT_ZC_WORDS");
     return (v && *v) ? std::max<int64_t>(0, std::atoll(v)) : int64_t(1) << 16;
@@ -1580,26 +1669,47 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         const int64_t K = c.num_paths;
         const int A = c.action_dim, H = c.horizon;
         const size_t row = (size_t)K * A, n = (size_t)H * row;
+        // (no pre-draw is running past this point: the worker finishes its job before the buffers change)
+        const bool predraw = mt_predraw_enabled();
+        int b = predraw_wait(e);
         if (n > e->zc_cap) {
             // fine-grained host memory: no GPU cache keeps an earlier call's rows (the rows change every call)
-            if (e->h_zc) (void)hipHostFree(e->h_zc);
-            e->h_zc = nullptr;
-            e->d_zc = nullptr;
+            for (int i = 0; i < 2; ++i) {
+                if (e->h_zc[i]) (void)hipHostFree(e->h_zc[i]);
+                e->h_zc[i] = nullptr;
+                e->d_zc[i] = nullptr;
+            }
             e->zc_cap = 0;
-            HIP_TRY(hipHostMalloc(&e->h_zc, n * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
-            HIP_TRY(hipHostGetDevicePointer((void**)&e->d_zc, e->h_zc, 0));
+            e->pre.ready = false;
+            for (int i = 0; i < 2; ++i) {
+                HIP_TRY(hipHostMalloc(&e->h_zc[i], n * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+                HIP_TRY(hipHostGetDevicePointer((void**)&e->d_zc[i], e->h_zc[i], 0));
+            }
             e->zc_cap = n;
         }
         Mt19937 g;
         std::memcpy(g.key, mt_key, sizeof(g.key));
         g.pos = *mt_pos;
-        for (int h = 0; h < H; ++h)
-            mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_zc + h * row);
+        const bool hit = predraw && e->pre.ready && e->pre.kg == k_global && e->pre.off == cand_offset &&
+                         g.pos == e->pre.from.pos && std::memcmp(g.key, e->pre.from.key, sizeof(g.key)) == 0 &&
+                         std::memcmp(low, e->pre.low.data(), sizeof(double) * A) == 0 &&
+                         std::memcmp(high, e->pre.high.data(), sizeof(double) * A) == 0;
+        e->pre.ready = false;
+        if (hit) {                                    // NumPy's stream is exactly where the worker drew from
+            b = e->pre.buf;
+            g = e->pre.to;
+            ++e->pre.hits;
+        } else {
+            b = e->zc_last ^ 1;
+            if (predraw) ++e->pre.misses;
+            for (int h = 0; h < H; ++h)
+                mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_zc[b] + h * row);
+        }
         const bool lean = e->comm == nullptr;
         if (!lean)
             HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
         e->want_done = lean && !costs_out;
-        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_zc, seed, cand_offset, e->d_costs, nullptr,
+        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_zc[b], seed, cand_offset, e->d_costs, nullptr,
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
         const bool spin = e->want_done && rc == BCMPC_OK;
@@ -1625,6 +1735,8 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         std::memcpy(mt_key, g.key, sizeof(g.key));
         *mt_pos = g.pos;
         *out = lean ? *e->h_result_map : *e->h_result;
+        e->zc_last = b;
+        if (predraw) predraw_post(e, g, low, high, A, k_global, cand_offset);   // the next call's rows
         return BCMPC_OK;
     }
     if (mt_device_path()) {

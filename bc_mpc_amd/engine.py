@@ -319,12 +319,22 @@ class RolloutEngine:
                           np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
 
     def _numpy_bounds(self, low, high):
-        """Per-action f64 bounds with a finite range (np.random.uniform would not raise), else None."""
+        """Per-action f64 bounds with a finite range (np.random.uniform would not raise), else None
+        (checked once per bounds content: every env step passes the same action_space arrays)."""
+        key = None
+        if isinstance(low, np.ndarray) and isinstance(high, np.ndarray):
+            key = (low.dtype.str, low.tobytes(), high.dtype.str, high.tobytes())
+            hit = getattr(self, "_bounds_cache", None)
+            if hit is not None and hit[0] == key:
+                return hit[1]
         lo = np.asarray(low, dtype=np.float64)
         hi = np.asarray(high, dtype=np.float64)
         if lo.shape != (self.action_dim,) or hi.shape != (self.action_dim,) or not np.all(np.isfinite(hi - lo)):
             return None
-        return np.ascontiguousarray(lo), np.ascontiguousarray(hi)
+        out = (np.ascontiguousarray(lo), np.ascontiguousarray(hi))
+        if key is not None:
+            self._bounds_cache = (key, out)
+        return out
 
     def numpy_stream_available(self, low, high) -> bool:
         """The global generator is NumPy's legacy MT19937 and the bounds are per-action vectors

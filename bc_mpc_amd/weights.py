@@ -35,11 +35,25 @@ _NORM_ATTRS = ("mean_obs", "std_obs", "mean_action", "std_action", "mean_reward"
                "mean_nxt_state", "std_nxt_state", "mean_deltas", "std_deltas")
 
 
+_NORM_CACHE: dict = {}      # id(model) -> (the attribute objects, their f64 arrays)
+
+
 def normalization_of(dyn_model) -> List[np.ndarray]:
-    out = []
-    for name in _NORM_ATTRS:
-        v = getattr(dyn_model, name, None)
-        out.append(np.zeros(1) if v is None else np.asarray(v, dtype=np.float64))
+    """The 10-tuple of normalisation vectors (utils.py:143-158 order) as f64 arrays; converted once per
+    set of attribute objects (get_action asks every env step; the reference fixes them at construction,
+    dynamics.py:41)."""
+    objs = [getattr(dyn_model, name, None) for name in _NORM_ATTRS]
+    hit = _NORM_CACHE.get(id(dyn_model))
+    if hit is not None:
+        for a, b in zip(hit[0], objs):
+            if a is not b:
+                break
+        else:
+            return hit[1]
+    out = [np.zeros(1) if v is None else np.asarray(v, dtype=np.float64) for v in objs]
+    if len(_NORM_CACHE) > 64:
+        _NORM_CACHE.clear()
+    _NORM_CACHE[id(dyn_model)] = (objs, out)
     return out
 
 

@@ -145,3 +145,48 @@ def test_zero_copy_shard_continues_the_stream(monkeypatch):
         assert np.array_equal(res.first_action, ref.first_action)
         assert np.array_equal(st[1], st_want[1]) and st[2] == st_want[2]
     eng.close()
+
+
+@pytest.mark.parametrize("predraw", ["1", "0"])
+def test_predraw_sequence_bitexact_with_interleaved_draws(predraw, monkeypatch):
+    """The drop-in at train_mpc_ppo.py's K = 400, H = 7 (the zero-copy draw, with the pre-draw worker
+    on or off): a sequence of MPCcontroller.get_action calls, some separated by foreign draws from the
+    global stream (the worker's rows must then be discarded), each returning the reference's action for
+    the array np.random.uniform would return at that point, and leaving NumPy's state exactly where the
+    reference leaves it (controllers.py:53, :82-85)."""
+    monkeypatch.setenv("BCMPC_MT_PREDRAW", predraw)
+    from bc_mpc_amd import MPCcontroller, cheetah_cost_fn
+    from oracle import mpc_oracle as orc
+    S, A, K, H = 20, 6, 400, 7
+    w = orc.synthetic_weights(S, A, 256, 2, "relu", True, seed_base=5)
+    norm = orc.synthetic_normalization(S, A)
+    dyn = orc.NumpyDynamics(w, norm)
+
+    class Box:
+        low, high = -np.ones(A, np.float32), np.ones(A, np.float32)
+        shape = (A,)
+
+    class Env:
+        action_space = Box()
+
+        class observation_space:
+            shape = (S,)
+
+    ctrl = MPCcontroller(Env(), dyn, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K)
+    np.random.seed(123)
+    state = orc.synthetic_state(norm)
+    for i in range(8):
+        if i in (3, 4, 6):
+            np.random.random(1 + i)                     # another consumer of the global stream
+        ref = np.random.RandomState()
+        ref.set_state(np.random.get_state())
+        paths = ref.uniform(Box.low, Box.high, [H, K, A])
+        costs, _ = orc.rollout(dyn, state, paths)
+        a = ctrl.get_action(state)
+        st_got, st_ref = np.random.get_state(), ref.get_state()
+        assert st_got[2] == st_ref[2] and np.array_equal(st_got[1], st_ref[1]), f"call {i}: stream position"
+        best = int(np.argmin(costs))
+        srt = np.sort(costs)
+        if srt[1] - srt[0] > 2e-4:
+            assert np.array_equal(a, paths[0, best]), f"call {i}"
+        state = state + 0.01 * np.sin(np.arange(S) + i)   # the next control step's state
