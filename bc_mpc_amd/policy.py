@@ -16,7 +16,10 @@ Supported containers:
    with the reference's variable names (tests/test_tf_readers.py).
 
 The policy changes every PPO update, and there is no hook for it, so the
-version stamp is a content digest (the 20->128->128->6 stack is ~80 KB).
+version stamp is a content digest (the 20->128->128->6 stack is ~80 KB), taken
+every control step: xxh3-64 over the arrays in place (~10 GB/s; blake2b, ~1 GB/s,
+when xxhash is not importable).  A container with an integer ``version``
+attribute is trusted instead (no digest).
 """
 from __future__ import annotations
 
@@ -28,10 +31,21 @@ import numpy as np
 from .engine import PolicySpec
 
 
+try:
+    import xxhash as _xxhash
+except Exception:  # pragma: no cover - installed in this image
+    _xxhash = None
+
+
 def _digest(spec: PolicySpec) -> int:
-    d = hashlib.blake2b(digest_size=8)
+    d = _xxhash.xxh3_64() if _xxhash is not None else hashlib.blake2b(digest_size=8)
+    shapes = []
     for a in list(spec.kernels) + list(spec.biases) + [spec.ob_mean, spec.ob_std, spec.logstd]:
-        d.update(np.ascontiguousarray(a, dtype=np.float32).tobytes())
+        if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous):
+            a = np.ascontiguousarray(a, dtype=np.float32)
+        d.update(a)                                                # (the buffer in place, no copy)
+        shapes.append(a.shape)
+    d.update(repr(shapes).encode())
     return int.from_bytes(d.digest(), "little") & (2**63 - 1)
 
 
@@ -84,4 +98,7 @@ def extract(policy_net) -> Tuple[PolicySpec, int]:
         spec = _tf_policy(policy_net)
     else:
         raise TypeError(f"cannot read policy weights from {type(policy_net).__name__}")
+    v = getattr(policy_net, "version", None)
+    if isinstance(v, int) and not isinstance(v, bool):
+        return spec, v
     return spec, _digest(spec)
