@@ -1207,8 +1207,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.team_buf = e->d_team;
         a.team_ctl = e->d_team_ctl;
         a.team_err = e->d_team_err;
-        // BCMPC_TEAM_SPINS (tests): exchange polls before a member gives up; -1: give up at the first
-        // exchange (forces the fallback path)
+        // BCMPC_TEAM_SPINS (tests): exchange polls before a member gives up; -1: the launch is skipped and
+        // reported as a team that gave up (forces the fallback path deterministically)
         const char* sv = std::getenv("BCMPC_TEAM_SPINS");
         a.team_spins = sv && *sv ? std::max(-1, std::atoi(sv)) : 0;
         if (const int rc = team_order_before(c.device, st)) return rc;
@@ -1227,7 +1227,10 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             HIP_TRY(hipMemsetAsync(d_tst, 0, tst_n * sizeof(uint64_t), st));
             a.stamps = d_tst;
         }
-        HIP_TRY(launch_rollout_team(a, e->HP, st));
+        if (a.team_spins < 0)
+            __atomic_store_n(e->h_team_err, 1u, __ATOMIC_RELEASE);
+        else
+            HIP_TRY(launch_rollout_team(a, e->HP, st));
         if (!e->sync_call)
             if (const int rc = team_order_after(c.device, st)) return rc;
         if (stamps) {

@@ -93,8 +93,7 @@ struct RolloutArgs {
     unsigned long long* team_buf;
     unsigned* team_ctl;
     unsigned* team_err;
-    int32_t team_spins;                      // exchange polls before a member gives up (0: the default, ~1 s;
-                                             // -1: at the first exchange -- tests of the fallback path)
+    int32_t team_spins;                      // exchange polls before a member gives up (0: the default, ~1 s)
     // (team kernel, the reward net with LayerNorm heads) [8 members][32 rows]: sum over member t's head
     // rows of the gamma-folded, scaled output weights (the centring correction, rollout_team.hip)
     const float* head_rs;

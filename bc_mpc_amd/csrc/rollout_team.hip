@@ -523,7 +523,7 @@ void rollout_team(const RolloutArgs a) {
         const int qc = RW ? (S - 16) >> 2 : 0;           // lane row holding the cost: dim 17 / reward row S
         gu64* const gb = (gu64*)a.team_buf;           // (global address space: never flat)
         bool dead = false;                                // the team cannot meet: finish without waiting
-        const int spin_limit = a.team_spins != 0 ? a.team_spins : kTeamSpins;   // (-1: give up at once)
+        const int spin_limit = a.team_spins > 0 ? a.team_spins : kTeamSpins;
         f4 ot[2];                                         // the step's summed output layer (rows 16 v + 4 q + r)
         double gp = 0.0;                                  // (reward net) gamma**(h-1) for this step's tail
 
@@ -952,7 +952,7 @@ void rollout_team(const RolloutArgs a) {
                     const gu64* const src = gb + (slot + t) * 512;
                     f4 got[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
                     for (int spins = 0; !dead; ++spins) {
-                        bool ok = true, gone = false;
+                        bool ok = true;
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
                             if (xrow(16 * (k >> 2) + 4 * q + (k & 3))) {
@@ -960,9 +960,13 @@ void rollout_team(const RolloutArgs a) {
                                     __hip_atomic_load(src + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 got[k >> 2][k & 3] = __uint_as_float((unsigned)xv);
                                 ok &= (unsigned)(xv >> 32) == ep;
-                                gone |= (unsigned)(xv >> 32) == dep;
                             }
-                        if (__all(ok) && spin_limit >= 0) break;
+                        if (__all(ok)) break;
+                        // (off the success path: every 32nd failed poll looks for a dead tag in row 0)
+                        bool gone = false;
+                        if ((spins & 31) == 31)
+                            gone = (unsigned)(__hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
+                                              32) == dep;
                         if (__any(gone) || spins >= spin_limit) {
                             // give up: raise the mapped error word (the host reruns the call on its fallback
                             // engine), tell this member's other waves (LDS) and the team (dead tags)
@@ -972,14 +976,12 @@ void rollout_team(const RolloutArgs a) {
                                 if (a.team_err)
                                     __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                             }
-#pragma unroll
-                            for (int par = 0; par < 2; ++par) {
-                                gu64* const mine = gb + (((size_t)col * 2 + par) * T + tm) * 512;
-#pragma unroll
-                                for (int k = 0; k < 8; ++k)
-                                    __hip_atomic_store(mine + k * 64 + lane, (unsigned long long)dep << 32,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            }
+                            // (granule row k = 0 of both parities: every poller reads it, rows 4q < R)
+                            gu64* const mine = gb + ((size_t)col * 2 * T + tm) * 512 + lane;
+                            __hip_atomic_store(mine, (unsigned long long)dep << 32, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(mine + (size_t)T * 512, (unsigned long long)dep << 32,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             break;
                         }
                         __builtin_amdgcn_s_sleep(1);

@@ -68,6 +68,9 @@ WORKLOADS = {
     # MPCcontrollerPolicyNet over the 2x256 relu + LayerNorm NNDynamicsModel with the 2x128 tanh MlpPolicy,
     # self_exp=False, explore=0.5, 400 paths, horizon 7
     "ppo_mpc_default": dict(K=400, H=7, hidden=256, L=2, act="relu", ln=True, policy=(128, 2), explore=0.5),
+    # diagnostic: the run.sh recipe's net without its LayerNorms (round 2's "runsh_recipe" line)
+    "runsh_noln": dict(K=400, H=30, hidden=500, L=2, act="tanh", reward=True, policy=(128, 2), explore=0.5,
+                       policy_mode="stochastic"),
 }
 S_DIM, A_DIM = 20, 6
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix, v_mfma_f32_16x16x4_f32
@@ -202,6 +205,73 @@ def dropin_parity_p50(K_global, H, hidden, L, act, ln, kernels, biases, ln_g, ln
     return out
 
 
+class _BenchPolicy:
+    """A policy container for the drop-in policy controllers (bc_mpc_amd.policy.extract: policy_spec() and
+    an integer version -- the weights are fixed during a control loop; the reference's TF MlpPolicy is read
+    through its session instead)."""
+
+    def __init__(self, arrays):
+        from bc_mpc_amd.engine import PolicySpec
+        self._spec = PolicySpec(*arrays)
+        self.version = 1
+
+    def policy_spec(self):
+        return self._spec
+
+
+def dropin_small_k(name, wl, prob, device, calls=200, gap_us=50.0):
+    """The reference's controller for a small-K workload, driven exactly as utils.py:193-213 drives it
+    (one get_action per env step; NumPy's global stream seeded, train_mpc_ppo.py:499): MPCcontroller
+    (plain nets), MPCcontrollerPolicyNet (a fused policy, explore / self_exp from the workload) or
+    MPCcontrollerPolicyNetReward (the reward net).  p50 back to back, and with ``gap_us`` of host work
+    between calls (an env.step stand-in: the call's pre-draw of the next rows overlaps it)."""
+    import torch
+    from bc_mpc_amd import MPCcontroller, MPCcontrollerPolicyNet, MPCcontrollerPolicyNetReward, cheetah_cost_fn
+    from bc_mpc_amd.dynamics import NNDynamicsModel, NNDynamicsRewardModel
+    K, H = wl["K"], wl["H"]
+    if prob["reward"]:
+        dyn = NNDynamicsRewardModel(_Env(), prob["norm"], 512, 1, 1e-3, layer_norm=prob["ln"], size=wl["hidden"],
+                                    device=device)
+        dyn.load_weights(prob["kernels"], prob["biases"], prob["ln_g"], prob["ln_b"])
+    else:
+        dyn = NNDynamicsModel(_Env(), wl["L"], wl["hidden"], wl["act"], None, prob["norm"], 512, 1, 1e-3,
+                              layer_norm=prob["ln"], device=device)
+        dyn.load_weights(prob["kernels"], prob["biases"], prob["ln_g"], prob["ln_b"])
+    stochastic = wl.get("policy_mode") == "stochastic"
+    if prob["policy"] and prob["reward"]:
+        ctrl = MPCcontrollerPolicyNetReward(_Env(), dyn, _BenchPolicy(prob["pol_arrays"]), explore=wl["explore"],
+                                            self_exp=stochastic, horizon=H, num_simulated_paths=K, device=device)
+        kind = "MPCcontrollerPolicyNetReward"
+    elif prob["policy"]:
+        ctrl = MPCcontrollerPolicyNet(_Env(), dyn, _BenchPolicy(prob["pol_arrays"]), explore=wl["explore"],
+                                      self_exp=stochastic, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K,
+                                      device=device)
+        kind = "MPCcontrollerPolicyNet"
+    else:
+        ctrl = MPCcontroller(_Env(), dyn, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K, device=device)
+        kind = "MPCcontroller"
+    np.random.seed(0)                                  # train_mpc_ppo.py:499
+    for _ in range(10):
+        ctrl.get_action(prob["state"])
+    ts, tg = [], []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        ctrl.get_action(prob["state"])
+        ts.append(time.perf_counter() - t0)
+    for _ in range(calls):
+        t1 = time.perf_counter()
+        while time.perf_counter() - t1 < gap_us * 1e-6:
+            pass
+        t0 = time.perf_counter()
+        ctrl.get_action(prob["state"])
+        tg.append(time.perf_counter() - t0)
+    torch.cuda.synchronize(device)
+    out = {"controller": kind, "kernel": ctrl._engine.info()["kernel"], "precision": ctrl._engine.precision,
+           "p50_ms": float(np.median(ts) * 1e3), f"p50_gap{int(gap_us)}us_ms": float(np.median(tg) * 1e3)}
+    ctrl._engine.close()
+    return out
+
+
 def synthetic_problem(wl):
     """Synthetic inputs of a workload: glorot kernels, 0.1 N biases, synthetic stats /
     state, the policy's normc kernels (random init: no checkpoints)."""
@@ -319,11 +389,11 @@ def small_k_lines(device, calls=200, warmup=20):
             row[tag + "kernel_ms"] = float(np.mean(ks))
             eng.close()
         row["speedup_p50"] = row["slab_p50_ms"] / row["p50_ms"]
-        if not prob["policy"] and not prob["reward"]:
-            # the drop-in MPCcontroller.get_action in parity mode (NumPy's stream, controllers.py:53)
-            row["dropin_parity_p50_ms"] = dropin_parity_p50(
-                wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"], prob["ln"], prob["kernels"], prob["biases"],
-                prob["ln_g"], prob["ln_b"], prob["norm"], prob["state"], device, 100, 1)["p50_ms"]
+        # the drop-in controller in parity mode (NumPy's stream, controllers.py:53 / :191 / :310)
+        d = dropin_small_k(name, wl, prob, device)
+        row["dropin_controller"] = d["controller"]
+        row["dropin_parity_p50_ms"] = d["p50_ms"]
+        row["dropin_parity_p50_gap50us_ms"] = d["p50_gap50us_ms"]
         out[name] = row
     return out
 
