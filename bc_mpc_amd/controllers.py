@@ -81,6 +81,13 @@ def _stock_sampler(obj) -> bool:
             and getattr(type(obj).sample_random_actions, "_bcmpc_stock_sampler", False))
 
 
+def _legacy_stream_unverified(eng) -> bool:
+    """True when get_action_numpy_stream may return None (the global generator is not NumPy's verified
+    legacy MT19937): the caller then keeps its own seed stream's state to restore."""
+    from .engine import _legacy_mt_state
+    return _legacy_mt_state() is None
+
+
 def _default_device() -> int:
     if "LOCAL_RANK" in os.environ:
         return int(os.environ["LOCAL_RANK"])
@@ -381,12 +388,15 @@ class MPCcontrollerPolicyNet(Controller):
             # the exploration draw (controllers.py:191) made by the library into pinned memory,
             # same values and stream advance as sample_random_actions
             eng = self._engine_for(spec, pspec, S, A, hi - lo)
-            if eng.numpy_stream_available(self.env.action_space.low, self.env.action_space.high):
-                eng.set_weights(spec, norm, version)
-                eng.set_policy(pspec, float(self.explore), pversion)
-                seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
-                res = eng.get_action_numpy_stream(state, self.env.action_space.low, self.env.action_space.high, K,
-                                                  lo, return_costs=self.keep_costs, seed=seed)
+            eng.set_weights(spec, norm, version)
+            eng.set_policy(pspec, float(self.explore), pversion)
+            seed_state = self._seed_rng.get_state() if _legacy_stream_unverified(eng) else None
+            seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+            res = eng.get_action_numpy_stream(state, self.env.action_space.low, self.env.action_space.high, K,
+                                              lo, return_costs=self.keep_costs, seed=seed)
+            if res is None and seed_state is not None:
+                self._seed_rng.set_state(seed_state)         # (nothing drawn: the host path draws the seed)
+            if res is not None:
                 self.last_costs = res.costs
                 cost, index, first_g = _minloc(self, eng, True, sign * res.best_cost, res.best_index,
                                                res.first_action, A)

@@ -182,6 +182,7 @@ struct bcmpc_engine {
         std::mutex mu;
         std::condition_variable cv;
         bool quit = false, pending = false, busy = false, ready = false;
+        bool rows = true;               // false: only NumPy's state is needed (the stochastic policy)
         Mt19937 from, to;               // the state the rows were drawn from / leave behind
         std::vector<double> low, high;
         int64_t kg = 0, off = 0;
@@ -1488,10 +1489,11 @@ static int predraw_wait(bcmpc_engine* e) {
 
 // rows [H][shard] of the draw that starts at NumPy state `from`, into the buffer the last call did not read
 static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low, const double* high, int A,
-                         int64_t k_global, int64_t cand_offset) {
+                         int64_t k_global, int64_t cand_offset, bool rows) {
     auto& p = e->pre;
     {
         std::lock_guard<std::mutex> lk(p.mu);
+        p.rows = rows;
         p.from = from;
         p.low.assign(low, low + A);
         p.high.assign(high, high + A);
@@ -1514,12 +1516,16 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
                 Mt19937 g = q.from;
                 const std::vector<double> lo = q.low, hi = q.high;
                 const int64_t kg = q.kg, off = q.off;
+                const bool rows = q.rows;
                 double* dst = e->h_zc[q.buf];
                 lk.unlock();
                 const int64_t K = c.num_paths;
                 const size_t row = (size_t)K * c.action_dim;
-                for (int h = 0; h < c.horizon; ++h)
-                    mt_uniform_rows(g, lo.data(), hi.data(), c.action_dim, kg, off, off + K, dst + h * row);
+                if (rows)
+                    for (int h = 0; h < c.horizon; ++h)
+                        mt_uniform_rows(g, lo.data(), hi.data(), c.action_dim, kg, off, off + K, dst + h * row);
+                else
+                    g.advance(2 * (int64_t)c.action_dim * c.horizon * kg);
                 lk.lock();
                 q.to = g;
                 q.ready = true;
@@ -1531,6 +1537,9 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
     p.cv.notify_all();
 }
 
+// (2^18 with the pre-draw worker measured worse at cfg1's 180k words back to back: the kernel's own reads of
+// 720 KB of rows over the bus, +30 us -- profiles/r03_dropin_zc_bound_ab.txt; draws whose rows are not read,
+// the stochastic policy's, take the host path at any size: only NumPy's state advances)
 static int64_t mt_zero_copy_words() {
     const char* v = std::getenv("BCMPC_MT_ZC_WORDS");
     return (v && *v) ? std::max<int64_t>(0, std::atoll(v)) : int64_t(1) << 16;
@@ -1665,7 +1674,10 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     HIP_TRY(hipSetDevice(c.device));
     const SyncCall sync_guard(e);
     const int64_t draw_words = 2 * (int64_t)c.action_dim * c.horizon * k_global;
-    if (draw_words <= mt_zero_copy_words() && mt_device_path()) {
+    // MPCcontrollerPolicyNet with self_exp=True draws its exploration array (controllers.py:191) but rolls out
+    // the policy's own samples (:202-203): only NumPy's state has to advance, no row is read
+    const bool rows_needed = !(e->PL > 0 && c.policy_mode == BCMPC_POLICY_STOCHASTIC);
+    if ((draw_words <= mt_zero_copy_words() || !rows_needed) && mt_device_path()) {
         // small draw: the host generates the shard's rows of every step into pinned memory (the
         // reference's own draw order), the kernel reads them in place; state in the kernel
         // arguments, result into mapped memory, one spin -- no copy either way
@@ -1693,7 +1705,8 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         Mt19937 g;
         std::memcpy(g.key, mt_key, sizeof(g.key));
         g.pos = *mt_pos;
-        const bool hit = predraw && e->pre.ready && e->pre.kg == k_global && e->pre.off == cand_offset &&
+        const bool hit = predraw && e->pre.ready && e->pre.rows == rows_needed && e->pre.kg == k_global &&
+                         e->pre.off == cand_offset &&
                          g.pos == e->pre.from.pos && std::memcmp(g.key, e->pre.from.key, sizeof(g.key)) == 0 &&
                          std::memcmp(low, e->pre.low.data(), sizeof(double) * A) == 0 &&
                          std::memcmp(high, e->pre.high.data(), sizeof(double) * A) == 0;
@@ -1705,14 +1718,18 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         } else {
             b = e->zc_last ^ 1;
             if (predraw) ++e->pre.misses;
-            for (int h = 0; h < H; ++h)
-                mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_zc[b] + h * row);
+            if (rows_needed)
+                for (int h = 0; h < H; ++h)
+                    mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_zc[b] + h * row);
+            else
+                g.advance(draw_words);
         }
         const bool lean = e->comm == nullptr;
         if (!lean)
             HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
         e->want_done = lean && !costs_out;
-        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_zc[b], seed, cand_offset, e->d_costs, nullptr,
+        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, rows_needed ? e->d_zc[b] : nullptr, seed, cand_offset,
+                              e->d_costs, nullptr,
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
         const bool spin = e->want_done && rc == BCMPC_OK;
@@ -1739,7 +1756,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         *mt_pos = g.pos;
         *out = lean ? *e->h_result_map : *e->h_result;
         e->zc_last = b;
-        if (predraw) predraw_post(e, g, low, high, A, k_global, cand_offset);   // the next call's rows
+        if (predraw) predraw_post(e, g, low, high, A, k_global, cand_offset, rows_needed);   // the next call's rows
         return BCMPC_OK;
     }
     if (mt_device_path()) {

@@ -44,6 +44,15 @@ struct Mt19937 {
         y ^= y >> 18;
         return y;
     }
+    // skip n raw words: the state n next32() calls leave behind (no tempering, nothing stored)
+    void advance(int64_t n) {
+        while (n > 0) {
+            if (pos >= 624) twist();
+            const int64_t take = n < 624 - pos ? n : 624 - pos;
+            pos += (int32_t)take;
+            n -= take;
+        }
+    }
     double next_double() {
         const int32_t a = (int32_t)(next32() >> 5), b = (int32_t)(next32() >> 6);
         return (a * 67108864.0 + b) / 9007199254740992.0;
