@@ -426,6 +426,9 @@ __device__ __forceinline__ void epi_colx(f4 (&acc)[TW][NC], const float (&f)[NC]
 #ifndef X3_NW512                // waves per workgroup at hidden 512 (8: one 64-candidate group per CU;
 #define X3_NW512 8               // 4: two 32-candidate groups per CU, out of phase)
 #endif
+#ifndef X3_NW1024               // waves per workgroup at hidden 1024 (8, or 16: four per SIMD)
+#define X3_NW1024 8
+#endif
 #ifndef X3_ONLY_NC
 #define X3_ONLY_NC 4
 #endif
@@ -436,7 +439,10 @@ __device__ __forceinline__ void epi_colx(f4 (&acc)[TW][NC], const float (&f)[NC]
 #define X3_STAGGER 0
 #endif
 // tiles per streamed operand unit: a whole k-step up to 4 tiles per wave, else half
-__host__ __device__ constexpr int x3_group(int TW) { return TW <= 4 ? TW : TW / 2; }
+#ifndef X3_GMAX
+#define X3_GMAX 4
+#endif
+__host__ __device__ constexpr int x3_group(int TW) { return TW <= X3_GMAX ? TW : TW / 2; }
 
 #ifndef X3_OWN                   // hidden layers start with the k-steps the wave produced itself
 #define X3_OWN 1
@@ -1260,7 +1266,8 @@ int x3_waves(int hidden_padded) {
         case 128: return 4;
         case 256: return X3_NW256;
         case 512: return X3_NW512;
-        default: return 8;          // 768, 1024
+        case 1024: return X3_NW1024;
+        default: return 8;          // 768
     }
 }
 
@@ -1304,7 +1311,7 @@ static hipError_t launch_x3_plain_nc(const RolloutArgs& a, int hidden_padded, hi
             if constexpr (NC <= 2) return launch_x3_t<768, NC, 8>(a, st);
             return hipErrorInvalidValue;
         case 1024:
-            if constexpr (NC <= 2) return launch_x3_t<1024, NC, 8>(a, st);
+            if constexpr (NC <= 2) return launch_x3_t<1024, NC, X3_NW1024>(a, st);
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
@@ -1353,7 +1360,7 @@ static hipError_t launch_x3_nc(const RolloutArgs& a, int hidden_padded, hipStrea
             if constexpr (X3_NW512 == 8 && X3_ONLY >= 512) return launch_x3_t<X3_ONLY, X3_ONLY_NC, 8, 128>(a, st);
             return hipErrorInvalidValue;
         }
-        return launch_x3_t<X3_ONLY, X3_ONLY_NC, X3_NW512>(a, st);
+        return launch_x3_t<X3_ONLY, X3_ONLY_NC, X3_ONLY == 1024 ? X3_NW1024 : X3_NW512>(a, st);
     }
     return hipErrorInvalidValue;
 #else

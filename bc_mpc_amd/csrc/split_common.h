@@ -58,8 +58,11 @@ __device__ __forceinline__ int partner_row16(int v) {    // the value of row (r 
     return (int)r[0] == v ? (int)r[1] : (int)r[0];          // (equal values: either is right)
 }
 
+#ifndef BCMPC_FLOAD_AUX           // cache-policy bits of the weight-fragment loads (variant builds)
+#define BCMPC_FLOAD_AUX 0
+#endif
 __device__ __forceinline__ h8 fload(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, BCMPC_FLOAD_AUX));
 }
 
 __device__ __forceinline__ h8 sread(const f4* p) { return __builtin_bit_cast(h8, *p); }
