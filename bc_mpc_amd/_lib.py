@@ -31,8 +31,9 @@ OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
 ACT_TANH, ACT_RELU = 0, 1
 COST_CHEETAH, COST_NONE, COST_REWARD = 0, 1, 2
 MODEL_DELTA, MODEL_REWARD = 0, 1
-PREC_FP32, PREC_SPLIT_F16 = 0, 1
-PRECISIONS = {"fp32": PREC_FP32, "split": PREC_SPLIT_F16}
+PREC_FP32, PREC_SPLIT_F16, PREC_F16 = 0, 1, 2
+# "f16": single-pass f16 MFMA (BASELINE cfg3's bf16-class GEMM), not the fp32 tolerance
+PRECISIONS = {"fp32": PREC_FP32, "split": PREC_SPLIT_F16, "f16": PREC_F16}
 KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3, "group8": 4, "split1": 5, "split2": 6, "split4": 7, "splitr": 8, "team": 9}
 
 

@@ -152,7 +152,8 @@ struct bcmpc_engine {
     int kernel = BCMPC_KERNEL_SOLO;    // resolved kernel layout
     int nw = 1;                        // waves per group (group kernels)
     int pack_tb = 4;                   // output tiles per packed block of layers 0..L-1
-    bool split = false;                // BCMPC_PREC_SPLIT_F16 (rollout_x3)
+    bool split = false;                // BCMPC_PREC_SPLIT_F16 or F16 (rollout_x3)
+    bool f16 = false;                  // BCMPC_PREC_F16: single MFMA pass
     int nc = 0;                        // split kernel: 16-candidate columns per workgroup
     int nwl = 0;                       // packed weight layers (RolloutArgs.w entries)
     float winv[BCMPC_MAX_LAYERS + 1]{};  // split kernel: 1 / operand scales per layer
@@ -295,9 +296,15 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (c.state_dim > 31) return fail(BCMPC_ERR_UNSUPPORTED, "reward model: state_dim must be <= 31");
     }
     if (c.cost == BCMPC_COST_CHEETAH && c.state_dim < 18) return fail(BCMPC_ERR_UNSUPPORTED, "cheetah cost needs state_dim >= 18");
-    if (c.precision != BCMPC_PREC_FP32 && c.precision != BCMPC_PREC_SPLIT_F16)
-        return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32 or SPLIT_F16");
-    const bool split = c.precision == BCMPC_PREC_SPLIT_F16;
+    if (c.precision != BCMPC_PREC_FP32 && c.precision != BCMPC_PREC_SPLIT_F16 && c.precision != BCMPC_PREC_F16)
+        return fail(BCMPC_ERR_UNSUPPORTED, "precision must be FP32, SPLIT_F16 or F16");
+    // single-pass f16 (BASELINE cfg3's bf16-class GEMM): the split slab kernels' plain tanh delta net only
+    const bool f16 = c.precision == BCMPC_PREC_F16;
+    if (f16 && (reward || c.policy_hidden > 0 || c.activation != BCMPC_ACT_TANH || c.layer_norm))
+        return fail(BCMPC_ERR_UNSUPPORTED, "F16 precision: the tanh NNDynamicsModel without LayerNorm / policy only");
+    if (f16 && c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_SPLIT4))
+        return fail(BCMPC_ERR_ARG, "F16 precision runs on the split1/split2/split4 kernels");
+    const bool split = c.precision != BCMPC_PREC_FP32;
     // relu / LayerNorm hidden layers (per-column scales or statistics exchanged across the workgroup)
     // on the split slab kernels: the plain delta net without a policy, hidden <= 512; beyond that only
     // the small-K team kernel takes them (checked once the kernel is chosen, below)
@@ -319,6 +326,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     bcmpc_engine* e = new bcmpc_engine();
     e->cfg = c;
     e->reward = reward;
+    e->f16 = f16;
     e->HP = reward ? std::max(128, padded_hidden(c.hidden)) : padded_hidden(c.hidden);
     e->T = e->HP / 16;
     // small K: one wave per block spreads candidates over more CUs
@@ -355,7 +363,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     // resident-column split kernel (rollout_rr.hip): the 2-layer tanh delta net at hidden <= 512.
     // Opt-in (kernel = splitr, or BCMPC_SPLITR=1 under auto): measured 2.03 ms at cfg3 against the
     // slab kernel's 1.90 ms -- LDS-read-bound at one column per wave
-    const bool rr_ok = split && !reward && e->PL == 0 && c.activation == BCMPC_ACT_TANH && !c.layer_norm &&
+    const bool rr_ok = split && !f16 && !reward && e->PL == 0 && c.activation == BCMPC_ACT_TANH && !c.layer_norm &&
                        c.n_layers == 2 && e->HP <= 512 && c.state_dim + c.action_dim <= 32;
     bool use_rr = c.kernel == BCMPC_KERNEL_SPLITR;
     if (use_rr && !rr_ok) {
@@ -377,7 +385,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     const int tmem = team_members(e->HP, tkind);
     // (a LayerNorm over a layer split across members: only the reward net's heads, whose statistics
     //  ride along with the output partials in the exchange -- rows 24..27, so S + 1 <= 24)
-    const bool team_shape = split && c.n_layers == 2 && e->HP <= 512 && c.state_dim + c.action_dim <= 32 &&
+    const bool team_shape = split && !f16 && c.n_layers == 2 && e->HP <= 512 && c.state_dim + c.action_dim <= 32 &&
                             c.action_dim <= 15 && c.horizon <= 1022 && tmem > 0 &&
                             !(c.layer_norm && tmem > 1 && tkind != 2) &&
                             (tkind == 0 || (c.state_dim >= 16 && e->PL <= 2 &&
@@ -1135,6 +1143,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             a.lnb[l] = e->d_ln + (size_t)(c.n_layers + l) * e->HP;
         }
     }
+    a.f16_single = e->f16 ? 1 : 0;
     a.consts = e->d_consts;
     a.state = d_state; a.state_stride = stride;
     if (state_inline) {                       // the tiled state by value in the kernel arguments

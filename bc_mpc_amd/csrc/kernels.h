@@ -81,6 +81,7 @@ struct RolloutArgs {
     float winv[BCMPC_MAX_LAYERS + 1];
     float pwinv[BCMPC_MAX_LAYERS + 1];       // the same for the fused policy's layers
     float hsc[BCMPC_MAX_LAYERS];             // split LN nets: power-of-two scale of hidden layer l's output
+    int32_t f16_single;                      // BCMPC_PREC_F16: one f16 MFMA pass (hi x hi), no lo operands
     uint64_t* stamps;                        // diagnostics (X3_STAMP builds): [blocks][NW][10] phase cycles
     // split kernel: np.argmin fused into the launch's tail (fused_argmin != 0): every workgroup
     // leaves its best (cost, index) in amin.scratch_c/i[blockIdx.x], the last to finish (ticket)

@@ -19,8 +19,8 @@ inline uint32_t temper(uint32_t y) {
 }  // namespace
 
 // the next m random_sample doubles of the stream (mt19937_next_double, two words each);
-// AVX2 clone where the host has it (same integer ops and exactly rounded conversions)
-__attribute__((target_clones("avx2", "default")))
+// AVX-512 / AVX2 clones where the host has them (same integer ops and exactly rounded conversions)
+__attribute__((target_clones("avx512f", "avx2", "default")))
 void mt_next_doubles(Mt19937& g, double* dbl, int64_t m) {
     int64_t i = 0;
     while (i < m) {

@@ -123,14 +123,15 @@ __device__ __forceinline__ int sidx(int p, int c, int part, int lane) {
 // One operand unit: acc[g*G + j][c] += W[tile g*G + j] * X[c] for j < G (the G
 // tiles' A fragments, hi / lo, in registers) and the k-step's B fragments (bh/bl,
 // all NC columns, read by the caller).
-template <int TW, int NC, int G>
+// F1 (BCMPC_PREC_F16): the hi x hi pass only.
+template <int TW, int NC, int G, bool F1 = false>
 __device__ __forceinline__ void unit_x3(const h8 (&ah)[G], const h8 (&al)[G], const h8 (&bh)[NC],
                                         const h8 (&bl)[NC], int g, f4 (&acc)[TW][NC]) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
 #pragma unroll
         for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bh[c], acc[g * G + j][c]);
-        if constexpr (X3_DIAG_ONEPASS) continue;       // timing only: the hi x hi pass alone
+        if constexpr (X3_DIAG_ONEPASS || F1) continue;  // (ONEPASS: timing only)
 #pragma unroll
         for (int j = 0; j < G; ++j) acc[g * G + j][c] = mfma16(ah[j], bl[c], acc[g * G + j][c]);
 #pragma unroll
@@ -166,16 +167,17 @@ __device__ __forceinline__ void unit_x3s(const h8 (&ah)[G], const h8 (&al)[G], c
 #ifndef X3_BSTREAM
 #define X3_BSTREAM 0
 #endif
-template <int NC>
+// (F1: the hi parts only; the lo operands are never read)
+template <int NC, bool F1 = false>
 __device__ __forceinline__ void bread_x3(const f4* slab, int p, int lane, h8 (&bh)[NC], h8 (&bl)[NC]) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         bh[c] = sread(slab + sidx<NC>(p, c, 0, lane));
-        bl[c] = sread(slab + sidx<NC>(p, c, 1, lane));
+        bl[c] = F1 ? bh[c] : sread(slab + sidx<NC>(p, c, 1, lane));
     }
 }
 
-template <int G>
+template <int G, bool F1 = false>
 __device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, int base, h8 (&ah)[G], h8 (&al)[G],
                                          bool diag = false) {
 #pragma unroll
@@ -187,7 +189,8 @@ __device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, in
             continue;
         }
         ah[j] = fload(rs, voff, o);
-        al[j] = (diag && X3_DIAG_LOADS == 1) ? ah[j] + (h8)(_Float16)1.0f : fload(rs, voff, o + 1024);
+        if constexpr (F1) al[j] = ah[j];
+        else al[j] = (diag && X3_DIAG_LOADS == 1) ? ah[j] + (h8)(_Float16)1.0f : fload(rs, voff, o + 1024);
     }
 }
 
@@ -203,7 +206,7 @@ __device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, in
 // other wave: bar() (the "layer input complete" barrier) runs after their MFMAs are
 // issued, overlapping them with the slower waves' epilogues.  (A wave reads its own
 // LDS writes in program order: no barrier.)
-template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, typename Bar = void (*)()>
+template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, bool F1 = false, typename Bar = void (*)()>
 __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
                                       int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr) {
     constexpr int NG = TW / G;
@@ -227,14 +230,14 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     if constexpr (OWN) {
 #pragma unroll
         for (int u = 0; u < NOWN; u += 2) {
-            aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
+            aload_x3<G, F1>(rs, voff, uoff(u + 1), s1h, s1l, true);
             __builtin_amdgcn_sched_barrier(0);
-            bread_x3<NC>(slab, kstep(u), lane, bh, bl);
-            unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-            aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
+            bread_x3<NC, F1>(slab, kstep(u), lane, bh, bl);
+            unit_x3<TW, NC, G, F1>(s0h, s0l, bh, bl, 0, acc);
+            aload_x3<G, F1>(rs, voff, uoff(u + 2), s0h, s0l, true);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (NG == 1) bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
-            unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
+            if constexpr (NG == 1) bread_x3<NC, F1>(slab, kstep(u + 1), lane, bh, bl);
+            unit_x3<TW, NC, G, F1>(s1h, s1l, bh, bl, G1, acc);
         }
         bar();
     }
@@ -242,14 +245,14 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     // conditional load would make the compiler drain vmcnt to 0 at the merge)
     if constexpr (NG == 1 && X3_BSTREAM && !OWN) {
         for (int u = 0; u < NU - 2; u += 2) {
-            aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
+            aload_x3<G, F1>(rs, voff, uoff(u + 1), s1h, s1l, true);
             __builtin_amdgcn_sched_barrier(0);      // keep the loads ahead of the MFMAs they overlap
             unit_x3s<TW, NC, G>(s0h, s0l, slab, u, lane, acc);
-            aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
+            aload_x3<G, F1>(rs, voff, uoff(u + 2), s0h, s0l, true);
             __builtin_amdgcn_sched_barrier(0);
             unit_x3s<TW, NC, G>(s1h, s1l, slab, u + 1, lane, acc);
         }
-        aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
+        aload_x3<G, F1>(rs, voff, uoff(NU - 1), s1h, s1l, true);
         __builtin_amdgcn_sched_barrier(0);
         unit_x3s<TW, NC, G>(s0h, s0l, slab, NU - 2, lane, acc);
         unit_x3s<TW, NC, G>(s1h, s1l, slab, NU - 1, lane, acc);
@@ -257,21 +260,21 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
         return;
     }
     for (int u = NOWN; u < NU - 2; u += 2) {
-        aload_x3<G>(rs, voff, uoff(u + 1), s1h, s1l, true);
+        aload_x3<G, F1>(rs, voff, uoff(u + 1), s1h, s1l, true);
         __builtin_amdgcn_sched_barrier(0);          // keep the loads ahead of the MFMAs they overlap
-        bread_x3<NC>(slab, kstep(u), lane, bh, bl);
-        unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-        aload_x3<G>(rs, voff, uoff(u + 2), s0h, s0l, true);
+        bread_x3<NC, F1>(slab, kstep(u), lane, bh, bl);
+        unit_x3<TW, NC, G, F1>(s0h, s0l, bh, bl, 0, acc);
+        aload_x3<G, F1>(rs, voff, uoff(u + 2), s0h, s0l, true);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NG == 1) bread_x3<NC>(slab, kstep(u + 1), lane, bh, bl);
-        unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
+        if constexpr (NG == 1) bread_x3<NC, F1>(slab, kstep(u + 1), lane, bh, bl);
+        unit_x3<TW, NC, G, F1>(s1h, s1l, bh, bl, G1, acc);
     }
-    aload_x3<G>(rs, voff, uoff(NU - 1), s1h, s1l, true);
+    aload_x3<G, F1>(rs, voff, uoff(NU - 1), s1h, s1l, true);
     __builtin_amdgcn_sched_barrier(0);
-    bread_x3<NC>(slab, kstep(NU - 2), lane, bh, bl);
-    unit_x3<TW, NC, G>(s0h, s0l, bh, bl, 0, acc);
-    if constexpr (NG == 1) bread_x3<NC>(slab, kstep(NU - 1), lane, bh, bl);
-    unit_x3<TW, NC, G>(s1h, s1l, bh, bl, G1, acc);
+    bread_x3<NC, F1>(slab, kstep(NU - 2), lane, bh, bl);
+    unit_x3<TW, NC, G, F1>(s0h, s0l, bh, bl, 0, acc);
+    if constexpr (NG == 1) bread_x3<NC, F1>(slab, kstep(NU - 1), lane, bh, bl);
+    unit_x3<TW, NC, G, F1>(s1h, s1l, bh, bl, G1, acc);
 }
 
 // Epilogue of one tile pair (k-step) for one column: BiasAdd (f32, after undoing
@@ -468,7 +471,7 @@ __host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, 
            NC * 2048 + (HP / 32) * NC * 2048 + (AK != 0 ? NW * NC * 16 * 8 : 0) + ((AK & 2) ? 2 * L * HP * 4 : 0);
 }
 
-template <int HP, int NC, int NW, int PHP, bool RW, int AK>
+template <int HP, int NC, int NW, int PHP, bool RW, int AK, bool F1 = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(x3_waves_per_eu(HP, NC, NW), 8)))
 void rollout_x3(const RolloutArgs a) {
     // AK: hidden activation kind, 0 tanh (activations tanh x 2^12: static scales); bit 0 relu,
@@ -476,6 +479,9 @@ void rollout_x3(const RolloutArgs a) {
     constexpr bool RELU = (AK & 1) != 0, LNK = (AK & 2) != 0, DYN = RELU && !LNK;
     constexpr float kAct = RELU ? 1.0f : kTanhK;        // folded into the epilogue factors / biases
     static_assert(AK == 0 || (PHP == 0 && !RW), "relu / LayerNorm: the plain delta net only");
+    // F1 (BCMPC_PREC_F16, BASELINE cfg3's "bf16 MFMA GEMM + fp32 cost accumulate" with f16's 11-bit
+    // significand): every operand is its hi part alone, one MFMA pass, no lo loads / slab writes
+    static_assert(!F1 || (PHP == 0 && !RW && AK == 0), "single-pass f16: the plain tanh delta net only");
     constexpr int T = HP / 16;          // hidden tiles
     constexpr int P = T / 2;            // hidden k-steps (32 wide)
     constexpr int TW = T / NW;          // output tiles per wave
@@ -628,7 +634,7 @@ void rollout_x3(const RolloutArgs a) {
 #endif
     constexpr int OP = PW < X3_OP ? PW : X3_OP;
     h8 a0h[TW], a0l[TW], uh[G], ul[G], oh[2 * OP], ol[2 * OP];
-    if constexpr (PHP == 0) aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);
+    if constexpr (PHP == 0) aload_x3<TW, F1>(rs0, voff, w * TW * 2048, a0h, a0l);
     // (the slot is a compile-time constant at every call: a runtime index into oh/ol would
     // demote the arrays to scratch memory)
     auto load_out = [&](int pp, auto SLOTc) __attribute__((always_inline)) {
@@ -637,12 +643,12 @@ void rollout_x3(const RolloutArgs a) {
         for (int v = 0; v < 2; ++v) {
             const int o = (((w * PW + pp) * 2 + v) * 2) * 1024;
             oh[2 * slot + v] = fload(rso, voff, o);
-            ol[2 * slot + v] = fload(rso, voff, o + 1024);
+            ol[2 * slot + v] = F1 ? oh[2 * slot + v] : fload(rso, voff, o + 1024);
         }
     };
     auto load_next = [&](int l_next) __attribute__((always_inline)) {
         if (l_next < L) {
-            aload_x3<G>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, w * P * TW * 2048 + kown * TW * 2048, uh, ul);
+            aload_x3<G, F1>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, w * P * TW * 2048 + kown * TW * 2048, uh, ul);
         } else {
             load_out(0, std::integral_constant<int, 0>{});
             if constexpr (OP > 1) load_out(1, std::integral_constant<int, OP - 1>{});
@@ -870,13 +876,13 @@ void rollout_x3(const RolloutArgs a) {
                 }
                 // this half's 4 slots are bytes [8*hv0, 8*hv0+8) of the lane's 16-byte B fragment
                 reinterpret_cast<h4*>(slab0 + (cw * 2 + 0) * 64 + lane)[hv0] = xh;
-                reinterpret_cast<h4*>(slab0 + (cw * 2 + 1) * 64 + lane)[hv0] = xl;
+                if constexpr (!F1) reinterpret_cast<h4*>(slab0 + (cw * 2 + 1) * 64 + lane)[hv0] = xl;
                 if (hv0 == 0 && q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kAct;
             } else {
                 h8 xh, xl;
                 split8(xin, xh, xl);
                 swrite(slab0 + (cw * 2 + 0) * 64 + lane, xh);
-                swrite(slab0 + (cw * 2 + 1) * 64 + lane, xl);
+                if constexpr (!F1) swrite(slab0 + (cw * 2 + 1) * 64 + lane, xl);
                 if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kAct;
             }
         }
@@ -895,12 +901,13 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 bh[c] = sread(slab0 + (c * 2 + 0) * 64 + lane);
-                bl[c] = sread(slab0 + (c * 2 + 1) * 64 + lane);
+                bl[c] = F1 ? bh[c] : sread(slab0 + (c * 2 + 1) * 64 + lane);
             }
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
 #pragma unroll
                 for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0h[j], bh[c], acc[j][c]);
+                if constexpr (F1) continue;
 #pragma unroll
                 for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0h[j], bl[c], acc[j][c]);
 #pragma unroll
@@ -999,7 +1006,7 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
-                    swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
+                    if constexpr (!F1) swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
             auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // layer input complete
             X3_ST(4);
@@ -1009,8 +1016,8 @@ void rollout_x3(const RolloutArgs a) {
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
             const float f = a.winv[l] * kAct;
             // own k-steps first: this wave's slab writes need no barrier
-            mm_x3<TW, NC, P, G, X3_OWN != 0, PW>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc, lane,
-                                                 uh, ul, kown, ready);
+            mm_x3<TW, NC, P, G, X3_OWN != 0, PW, F1>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc,
+                                                     lane, uh, ul, kown, ready);
             if constexpr (!X3_OWN) ready();
             X3_ST(5);
             load_next(l + 1);
@@ -1045,6 +1052,7 @@ void rollout_x3(const RolloutArgs a) {
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
                     po[v][c] = mfma16(oh[2 * slot + v], xh[pp][c], po[v][c]);
+                    if constexpr (F1) continue;
                     po[v][c] = mfma16(oh[2 * slot + v], xl[pp][c], po[v][c]);
                     po[v][c] = mfma16(ol[2 * slot + v], xh[pp][c], po[v][c]);
                 }
@@ -1054,7 +1062,7 @@ void rollout_x3(const RolloutArgs a) {
             }
         }
         __builtin_amdgcn_sched_barrier(0);              // (not hoisted above the MFMAs' operand waits)
-        if constexpr (PHP == 0) aload_x3<TW>(rs0, voff, w * TW * 2048, a0h, a0l);   // next step's layer 0
+        if constexpr (PHP == 0) aload_x3<TW, F1>(rs0, voff, w * TW * 2048, a0h, a0l);   // next step's layer 0
         // the owners reach this point first (the older waves win the MFMA arbitration):
         // they stage the next chunk's action inputs while the others finish
         if constexpr (PHP == 0)
@@ -1235,7 +1243,7 @@ void rollout_x3(const RolloutArgs a) {
 #endif
 hipError_t launch_rollout_x3_plain(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
 
-template <int HP, int NC, int NW, int PHP = 0, bool RW = false, int AK = 0>
+template <int HP, int NC, int NW, int PHP = 0, bool RW = false, int AK = 0, bool F1 = false>
 static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
     if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1, 0, 0, AK, NW) > 160 * 1024) {
         (void)a; (void)st;
@@ -1244,17 +1252,18 @@ static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
         if (PHP > 0 && (a.pL < 1 || a.phidden_padded != PHP)) return hipErrorInvalidValue;
         static bool attr_set = false;
         if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW, PHP, RW, AK>,
+            hipError_t e = hipFuncSetAttribute((const void*)rollout_x3<HP, NC, NW, PHP, RW, AK, F1>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
             attr_set = true;
         }
         if (RW != (a.model == BCMPC_MODEL_REWARD) || (RW && (a.L != 2 || a.S < 16))) return hipErrorInvalidValue;
         if (AK != ((a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0))) return hipErrorInvalidValue;
+        if (F1 != (a.f16_single != 0)) return hipErrorInvalidValue;
         const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, RW ? 3 : a.L, a.A, PHP > 0 ? a.pL : 0, PHP, AK, NW);
         if (lds > 160 * 1024) return hipErrorInvalidValue;
         const int64_t blocks = (a.K + 16 * NC - 1) / (16 * NC);
-        hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP, RW, AK>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
+        hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP, RW, AK, F1>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
         return hipGetLastError();
     }
 }
@@ -1299,23 +1308,44 @@ size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int polic
 
 #endif  // X3_PART != 1
 
-// the plain tanh delta net without a policy (X3_PART 1)
-template <int NC>
-static hipError_t launch_x3_plain_nc(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+// the plain tanh delta net without a policy (X3_PART 1); F1: single-pass f16 (BCMPC_PREC_F16)
+template <int NC, bool F1>
+static hipError_t launch_x3_plain_ncf(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
     switch (hidden_padded) {
-        case 64: return launch_x3_t<64, NC, 2>(a, st);
-        case 128: return launch_x3_t<128, NC, 4>(a, st);
-        case 256: return launch_x3_t<256, NC, X3_NW256>(a, st);
-        case 512: return launch_x3_t<512, NC, X3_NW512>(a, st);
+        case 64: return launch_x3_t<64, NC, 2, 0, false, 0, F1>(a, st);
+        case 128: return launch_x3_t<128, NC, 4, 0, false, 0, F1>(a, st);
+        case 256: return launch_x3_t<256, NC, X3_NW256, 0, false, 0, F1>(a, st);
+        case 512: return launch_x3_t<512, NC, X3_NW512, 0, false, 0, F1>(a, st);
         case 768:
-            if constexpr (NC <= 2) return launch_x3_t<768, NC, 8>(a, st);
+            if constexpr (NC <= 2) return launch_x3_t<768, NC, 8, 0, false, 0, F1>(a, st);
             return hipErrorInvalidValue;
         case 1024:
-            if constexpr (NC <= 2) return launch_x3_t<1024, NC, X3_NW1024>(a, st);
+            if constexpr (NC <= 2) return launch_x3_t<1024, NC, X3_NW1024, 0, false, 0, F1>(a, st);
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }
+// (the single-pass instantiations live in X3_PART 2: iterative-ILP crashes the compiler on them)
+hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
+template <int NC>
+static hipError_t launch_x3_plain_nc(const RolloutArgs& a, int hidden_padded, hipStream_t st) {
+#ifdef X3_ONLY
+    if (a.f16_single) return hipErrorInvalidValue;
+#else
+    if (a.f16_single) return launch_rollout_x3_f16(a, hidden_padded, NC, st);
+#endif
+    return launch_x3_plain_ncf<NC, false>(a, hidden_padded, st);
+}
+#if X3_PART != 1 && !defined(X3_ONLY)
+hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st) {
+    switch (nc) {
+        case 1: return launch_x3_plain_ncf<1, true>(a, hidden_padded, st);
+        case 2: return launch_x3_plain_ncf<2, true>(a, hidden_padded, st);
+        case 4: return launch_x3_plain_ncf<4, true>(a, hidden_padded, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+#endif
 
 #if X3_PART == 1 && !defined(X3_ONLY)
 hipError_t launch_rollout_x3_plain(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st) {

@@ -130,8 +130,9 @@ class RolloutEngine:
         """``precision``: "fp32" (v_mfma_f32_16x16x4_f32), "split" (f32-accurate hi/lo f16
         operands on v_mfma_f32_16x16x32_f16, rollout_x3.hip; relu / LayerNorm only for the plain delta net
         with hidden <= 512; a fused policy needs a tanh net of hidden 449..1024, 449..512 with the reward
-        net) or "auto" (split where it
-        applies, else fp32).
+        net), "f16" (one f16 MFMA pass on the split slab kernels: BASELINE cfg3's "bf16 MFMA GEMM + fp32
+        cost accumulate", the tanh delta net only; NOT the fp32 tolerance) or "auto" (split
+        where it applies, else fp32).
         Default: "split" for the split* kernels, else $BCMPC_PRECISION or "auto"."""
         self._lib = _lib.load()
         if activation not in _ACT:

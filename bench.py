@@ -398,6 +398,33 @@ def small_k_lines(device, calls=200, warmup=20):
     return out
 
 
+def f16_line(wl, prob, device, steps=50, warmup=5):
+    """BASELINE configs[2] as it is worded ("bf16 MFMA GEMM + fp32 cost accumulate"): the same complete
+    get_action with the single-pass f16 engine (precision "f16"; f16's 11-bit significand,
+    f32 accumulate, f64 state and cost).  Not `value`: its costs meet the f16 bar of tests/test_gpu_f16.py,
+    not the fp32 tolerance.  Roofline against the f16 dense MFMA peak (one pass per product)."""
+    K, H = wl["K"], wl["H"]
+    eng = make_engine(wl, prob, device, "f16")
+    eng.set_timing(True)
+    for i in range(warmup):
+        eng.get_action(prob["state"], None, seed=0xF16 + i)
+    ts, ks = [], []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        eng.get_action(prob["state"], None, seed=0xF16 + warmup + i)
+        ts.append(time.perf_counter() - t0)
+        ks.append(eng.last_kernel_ms()[0])
+    kern = eng.info()["kernel"]
+    eng.close()
+    fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
+    tf = K * H * fpcs / (float(np.mean(ks)) / 1e3) / 1e12
+    return {"precision": "f16 (one v_mfma_f32_16x16x32_f16 pass, f32 accumulate; f64 state / cost)",
+            "kernel": kern, "value": K * H / float(np.mean(ts)), "unit": "candidate-steps/s",
+            "p50_ms": float(np.percentile(ts, 50) * 1e3), "kernel_ms_avg": float(np.mean(ks)),
+            "roofline": {"bound": "mfma", "achieved": tf, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": tf / F16_MFMA_PEAK_TFLOPS}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -410,10 +437,12 @@ def main():
     ap.add_argument("--dropin-calls", type=int, default=20,
                     help="MPCcontroller.get_action calls (rng='numpy', the reference's draw) timed for "
                          "dropin_parity_p50_ms (0: skip)")
-    ap.add_argument("--precision", default=os.environ.get("BCMPC_PRECISION", "auto"), choices=["auto", "fp32", "split"],
+    ap.add_argument("--precision", default=os.environ.get("BCMPC_PRECISION", "auto"), choices=["auto", "fp32", "split", "f16"],
                     help="fp32: f32 MFMA (rollout_grp); split: f32-accurate hi/lo f16 MFMA (rollout_x3, tanh "
                          "NNDynamicsModel without LayerNorm; with a fused policy: hidden 449..1024); auto: split "
                          "where it applies, else fp32")
+    ap.add_argument("--no-f16", action="store_true",
+                    help="skip the f16_single_pass line (BASELINE cfg3's bf16-class GEMM on the f16 engine)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-small-k", action="store_true",
@@ -554,7 +583,7 @@ def main():
     if cem and world > 1:                              # per-launch device time: the wall-clock share
         kern_ms = [t * 1e3 for t in step_s]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
-    peak = FP32_MFMA_PEAK_TFLOPS if eng.precision == "fp32" else SPLIT_PEAK_TFLOPS
+    peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16": F16_MFMA_PEAK_TFLOPS}.get(eng.precision, SPLIT_PEAK_TFLOPS)
     achieved_tflops = K * H * iters * fpcs / kern_avg_s / 1e12
     out = {
         "metric": "candidate-steps/sec (K x H per get_action), HalfCheetah dims",
@@ -568,7 +597,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if eng.precision == "fp32" else "f32 (hi/lo f16 split operands, 3 MFMA passes, f32 accumulate)",
+        "dtype": {"fp32": "f32", "f16": "f16 (one MFMA pass, f32 accumulate; not the fp32 tolerance)"}.get(
+            eng.precision, "f32 (hi/lo f16 split operands, 3 MFMA passes, f32 accumulate)"),
         "data": f"synthetic (HalfCheetah dims s=20,a=6; random-init {'two-head reward net' if reward else 'dynamics MLP'}; "
                 f"actions {'resident in HBM as [H,K,6] f64, rollout only' if args.actions == 'hbm' else 'drawn in-kernel (Philox); step = complete get_action, host state in, host result out'})",
         "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
@@ -577,7 +607,8 @@ def main():
                                + (f" + fused policy {policy[1]}x{policy[0]} tanh "
                                   f"({wl.get('policy_mode', 'explore')})" if policy else "")
                                + (f" + CEM {iters} iterations, {n_elite} elites, alpha {cem['alpha']}" if cem else "")
-                               + (", fp32 MFMA" if eng.precision == "fp32" else ", split-f16 MFMA (f32-accurate)")
+                               + {"fp32": ", fp32 MFMA", "f16": ", single-pass f16 MFMA"}.get(
+                                   eng.precision, ", split-f16 MFMA (f32-accurate)")
                                + (f", {world} ranks: 1 all-gather min-loc per step"
                                   + (" (+1 all-gather of the local top-E per CEM iteration)" if cem else "")
                                   if world > 1 else ", 1 GPU (no collective)"),
@@ -595,8 +626,10 @@ def main():
         "kernel_ms_avg": kern_avg_s * 1e3,
         "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved_tflops / peak, "traffic": None,
-                     "peak_note": "fp32 matrix peak (v_mfma_f32_16x16x4_f32)" if eng.precision == "fp32" else
-                                  "f16 dense MFMA peak 2516.6 / 3 passes per f32 product (f32-equivalent)",
+                     "peak_note": {"fp32": "fp32 matrix peak (v_mfma_f32_16x16x4_f32)",
+                                   "f16": "f16 dense MFMA peak (one pass per product)"}.get(
+                                       eng.precision, "f16 dense MFMA peak 2516.6 / 3 passes per f32 product "
+                                                      "(f32-equivalent)"),
                      "kernel": kernel_name + (" x CEM iterations + select/refit (HIP events around the "
                                               "whole device-side CEM call)" if cem else ""),
                      "flop_per_launch": K * H * fpcs,
@@ -608,7 +641,7 @@ def main():
     if os.path.exists(prof):
         try:
             # PMC traffic of this kernel in this action mode (device: Philox actions in-kernel, hbm: read)
-            key = args.workload + ("" if eng.precision == "fp32" else ":split") + \
+            key = args.workload + {"fp32": "", "f16": ":f16"}.get(eng.precision, ":split") + \
                 (":device" if args.actions == "device" else "")
             tr = json.load(open(prof)).get(key)
             if tr:
@@ -626,6 +659,9 @@ def main():
                                            pol_arrays, wl.get("explore", 0.5), gamma, cem)
     if rank == 0 and world == 1 and not args.no_small_k:
         out["small_k"] = small_k_lines(local)
+    if (rank == 0 and world == 1 and not args.no_f16 and not (cem or policy or reward or ln) and act == "tanh"
+            and eng.precision != "f16"):
+        out["f16_single_pass"] = f16_line(wl, prob, local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if lib_comm is not None:

@@ -64,10 +64,14 @@ typedef enum bcmpc_model {      /* which dynamics net (dynamics.py)             
 
 typedef enum bcmpc_precision {
     BCMPC_PREC_FP32 = 0,        /* f32 MLP on v_mfma_f32_16x16x4_f32 (exact f32 fma chain) */
-    BCMPC_PREC_SPLIT_F16 = 1    /* f32-accurate MLP on the f16 matrix cores: every operand as
+    BCMPC_PREC_SPLIT_F16 = 1,   /* f32-accurate MLP on the f16 matrix cores: every operand as
                                    hi + lo f16 halves (22 bits), three v_mfma_f32_16x16x32_f16
                                    passes hi*hi + hi*lo + lo*hi, f32 accumulate (DESIGN.md
                                    "split kernel"); tanh, no LayerNorm, NNDynamicsModel only */
+    BCMPC_PREC_F16 = 2          /* BASELINE cfg3's "bf16 MFMA GEMM + fp32 cost": one f16 pass
+                                   (11-bit operands, f32 accumulate, f64 state / cost) on the
+                                   split slab kernels; the tanh NNDynamicsModel only.  NOT the
+                                   fp32 tolerance: DESIGN.md "single-pass f16"               */
 } bcmpc_precision;
 
 typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")              */
