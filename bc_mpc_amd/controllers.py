@@ -164,6 +164,7 @@ class MPCcontroller(Controller):
         self._group = process_group
         self._engine: Optional[RolloutEngine] = None
         self._engine_key = None
+        self._fast = None                       # get_action's repeat-call fast path (see there)
         self._traj_buf = None
         # diagnostics of the last call (not part of the reference API)
         self.last_cost = None
@@ -207,6 +208,21 @@ class MPCcontroller(Controller):
 
     # controllers.py:57-88
     def get_action(self, state):
+        fp = getattr(self, "_fast", None)
+        if fp is not None:
+            # the per-env-step repeat (utils.py:202): same env / model / cost / shape as the last call, the
+            # model's weights version and normalisation objects unchanged, one rank -- the checks below
+            # were all made by that call, so only the NumPy-stream launch remains
+            if (fp[0] == (self.env, self.dyn_model, self.cost_fn, self.horizon, self.num_simulated_paths, self.rng,
+                          self.keep_costs) and _weights.same_token(self.dyn_model, fp[1])
+                    and "sample_random_actions" not in self.__dict__ and _dist.world(self._group)[1] == 1):
+                space = self.env.action_space
+                res = fp[2].get_action_numpy_stream(state, space.low, space.high, fp[3])
+                if res is not None:
+                    self.last_costs = None
+                    self.last_cost, self.last_index = res.best_cost, res.best_index
+                    return res.first_action
+            self._fast = None
         S, A = self._dims()
         K = int(self.num_simulated_paths)
         if self.horizon < 1:
@@ -239,6 +255,10 @@ class MPCcontroller(Controller):
                 self.last_costs = res.costs
                 cost, index, first_g = _minloc(self, eng, True, res.best_cost, res.best_index, res.first_action, A)
                 self.last_cost, self.last_index = cost, index
+                tok = _weights.weight_token(self.dyn_model)
+                if ws == 1 and not self.keep_costs and tok is not None and eng.comm is None:
+                    self._fast = ((self.env, self.dyn_model, self.cost_fn, self.horizon, self.num_simulated_paths,
+                                   self.rng, self.keep_costs), tok, eng, K)
                 return first_g                               # = action_paths[0, index] (controllers.py:84-85)
 
         action_paths = None

@@ -198,6 +198,7 @@ class RolloutEngine:
         self._wver = None
         self._pol = None
         self.comm = None
+        self._mt_fast = None        # get_action_numpy_stream's prepared ctypes arguments
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, spec: MLPSpec, normalization: Sequence, version: int) -> None:
@@ -362,19 +363,42 @@ class RolloutEngine:
             bounds = self._numpy_bounds(low, high)
             if bounds is None:
                 return None
-            s = _f64(state).reshape(-1)
-            if s.shape[0] != self.state_dim:
-                raise ValueError(f"state has {s.shape[0]} dims, expected {self.state_dim}")
             bg, key_p, pos_p = mt
-            res = _lib.Result()
-            costs = np.empty(self.num_paths, dtype=np.float64) if return_costs else None
+            if return_costs:
+                s = _f64(state).reshape(-1)
+                if s.shape[0] != self.state_dim:
+                    raise ValueError(f"state has {s.shape[0]} dims, expected {self.state_dim}")
+                res = _lib.Result()
+                costs = np.empty(self.num_paths, dtype=np.float64)
+                with bg.lock:
+                    _lib.check(self._lib.bcmpc_get_action_mt19937(
+                        self._h, _dp(s), key_p, pos_p, _dp(bounds[0]), _dp(bounds[1]), ctypes.c_int64(k_global),
+                        ctypes.c_int64(cand_offset), ctypes.c_uint64(seed & (2**64 - 1)), ctypes.byref(res),
+                        _dp(costs)))
+                return StepResult(int(res.best_index), float(res.best_cost),
+                                  np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
+            # the per-env-step call (no cost vector): ctypes arguments built once per (generator, bounds,
+            # shard, seed) and reused -- the state goes into an engine-owned buffer, the first action is
+            # copied out of a NumPy view on the result record (~6 us of Python per call less)
+            key = (k_global, cand_offset, seed)
+            fa = self._mt_fast
+            if fa is None or fa[0] != key or fa[5] is not bg or fa[6] is not bounds:
+                sbuf = np.zeros(self.state_dim, dtype=np.float64)
+                res = _lib.Result()
+                first = np.ctypeslib.as_array(res.first_action)[: self.action_dim]
+                args = (self._h, _dp(sbuf), key_p, pos_p, _dp(bounds[0]), _dp(bounds[1]), ctypes.c_int64(k_global),
+                        ctypes.c_int64(cand_offset), ctypes.c_uint64(seed & (2**64 - 1)), ctypes.byref(res), None)
+                fa = self._mt_fast = (key, sbuf, res, first, args, bg, bounds)
+            _, sbuf, res, first, args = fa[:5]
+            s = state if type(state) is np.ndarray else _f64(state)
+            if s.size != self.state_dim:
+                raise ValueError(f"state has {s.size} dims, expected {self.state_dim}")
+            np.copyto(sbuf, s.reshape(-1), casting="unsafe")
             with bg.lock:
-                _lib.check(self._lib.bcmpc_get_action_mt19937(
-                    self._h, _dp(s), key_p, pos_p, _dp(bounds[0]), _dp(bounds[1]), ctypes.c_int64(k_global),
-                    ctypes.c_int64(cand_offset), ctypes.c_uint64(seed & (2**64 - 1)), ctypes.byref(res),
-                    _dp(costs) if costs is not None else None))
-            return StepResult(int(res.best_index), float(res.best_cost),
-                              np.array(res.first_action[: self.action_dim], dtype=np.float64), costs)
+                rc = self._lib.bcmpc_get_action_mt19937(*args)
+            if rc:
+                _lib.check(rc)
+            return StepResult(res.best_index, res.best_cost, first.copy(), None)
         if not self.numpy_stream_available(low, high):
             return None
         st = np.random.get_state()

@@ -35,26 +35,43 @@ _NORM_ATTRS = ("mean_obs", "std_obs", "mean_action", "std_action", "mean_reward"
                "mean_nxt_state", "std_nxt_state", "mean_deltas", "std_deltas")
 
 
-_NORM_CACHE: dict = {}      # id(model) -> (the attribute objects, their f64 arrays)
+_NORM_CACHE: dict = {}      # id(model) -> (the attribute objects, their f64 arrays, generation): slotted models
 
 
-def normalization_of(dyn_model) -> List[np.ndarray]:
-    """The 10-tuple of normalisation vectors (utils.py:143-158 order) as f64 arrays; converted once per
-    set of attribute objects (get_action asks every env step; the reference fixes them at construction,
-    dynamics.py:41)."""
+def _norm_entry(dyn_model):
+    """(attribute objects, f64 arrays, generation) of the model's normalisation: converted once per set
+    of attribute objects (get_action asks every env step; the reference fixes them at construction,
+    dynamics.py:41); the generation counts the sets seen, kept on the model object itself."""
     objs = [getattr(dyn_model, name, None) for name in _NORM_ATTRS]
-    hit = _NORM_CACHE.get(id(dyn_model))
+    hit = getattr(dyn_model, "_bcmpc_norm_cache", None)
+    if hit is None:
+        hit = _NORM_CACHE.get(id(dyn_model))
     if hit is not None:
         for a, b in zip(hit[0], objs):
             if a is not b:
                 break
         else:
-            return hit[1]
+            return hit
     out = [np.zeros(1) if v is None else np.asarray(v, dtype=np.float64) for v in objs]
-    if len(_NORM_CACHE) > 64:
-        _NORM_CACHE.clear()
-    _NORM_CACHE[id(dyn_model)] = (objs, out)
-    return out
+    entry = (objs, out, 0 if hit is None else hit[2] + 1)
+    try:
+        dyn_model._bcmpc_norm_cache = entry
+    except AttributeError:                                  # (a slotted object)
+        if len(_NORM_CACHE) > 64:
+            _NORM_CACHE.clear()
+        _NORM_CACHE[id(dyn_model)] = entry
+    return entry
+
+
+def normalization_of(dyn_model) -> List[np.ndarray]:
+    """The 10-tuple of normalisation vectors (utils.py:143-158 order) as f64 arrays."""
+    return _norm_entry(dyn_model)[1]
+
+
+def _with_norm(version: int, gen: int) -> int:
+    """The engine's weights version: the model's own stamp with the normalisation generation folded in,
+    so replacing a normalisation attribute re-uploads it (set_weights is idempotent on the version)."""
+    return ((int(version) & (2**47 - 1)) << 16) | (gen & 0xFFFF)
 
 
 def _act_name(act) -> str:
@@ -137,12 +154,34 @@ def _cached(dyn_model, version: int, make):
     return spec
 
 
+def weight_token(dyn_model):
+    """A cheap token that changes whenever extract(dyn_model) could return different weights or
+    normalisation: the model's version stamp (ours, or the fit hook's on the reference's TF model) and
+    the identities of its normalisation attribute objects.  None when the model has no stamp (the
+    weights are digested by content each call)."""
+    if hasattr(dyn_model, "mlp_spec"):
+        v = int(dyn_model.version)
+    elif hasattr(dyn_model, "sess") and getattr(dyn_model, "_bcmpc_fit_hooked", False):
+        v = int(dyn_model._bcmpc_version)
+    else:
+        return None
+    return (v,) + tuple(getattr(dyn_model, name, None) for name in _NORM_ATTRS)
+
+
+def same_token(dyn_model, token) -> bool:
+    """weight_token(dyn_model) would equal ``token`` (the version, then the normalisation objects by
+    identity -- the token holds them, so their ids cannot be reused)."""
+    t = weight_token(dyn_model)
+    return t is not None and t[0] == token[0] and all(a is b for a, b in zip(t[1:], token[1:]))
+
+
 def extract(dyn_model) -> Tuple[MLPSpec, List[np.ndarray], int]:
-    """Return ``(spec, normalization10, version)`` for the engine."""
-    norm = normalization_of(dyn_model)
+    """Return ``(spec, normalization10, version)`` for the engine (``version``: the weights' stamp with
+    the normalisation generation folded in, _with_norm)."""
+    _, norm, gen = _norm_entry(dyn_model)
     if hasattr(dyn_model, "mlp_spec"):                      # bc_mpc_amd.dynamics.NNDynamicsModel
         v = int(dyn_model.version)
-        return _cached(dyn_model, v, dyn_model.mlp_spec), norm, v
+        return _cached(dyn_model, v, dyn_model.mlp_spec), norm, _with_norm(v, gen)
     w = getattr(dyn_model, "weights", None)
     if w is not None and hasattr(w, "kernels"):             # NumPy stand-ins
         kernels = [np.asarray(k) for k in w.kernels]
@@ -157,9 +196,9 @@ def extract(dyn_model) -> Tuple[MLPSpec, List[np.ndarray], int]:
                     + list(getattr(w, "ln_beta", None) or []):
                 d.update(np.ascontiguousarray(a, dtype=np.float32).tobytes())
             version = int.from_bytes(d.digest(), "little") & (2**63 - 1)
-        return spec, norm, int(version)
+        return spec, norm, _with_norm(int(version), gen)
     if hasattr(dyn_model, "sess"):                          # reference TF1 NNDynamicsModel
         _install_fit_hook(dyn_model)
         v = int(dyn_model._bcmpc_version)                   # (variables read once per refit)
-        return _cached(dyn_model, v, lambda: _tf_weights(dyn_model)), norm, v
+        return _cached(dyn_model, v, lambda: _tf_weights(dyn_model)), norm, _with_norm(v, gen)
     raise TypeError(f"cannot read dynamics weights from {type(dyn_model).__name__}")

@@ -663,3 +663,66 @@ def test_numpy_stream_shards_equal_whole_draw():
     assert np.array_equal(np.concatenate(costs[1:]), costs[0])
     for st in states:
         assert np.array_equal(st[1], st_want[1]) and st[2] == st_want[2]
+
+
+def test_dropin_repeat_fast_path_tracks_changes():
+    """MPCcontroller.get_action's repeat-call fast path (controllers.py fast path: the checks of the last
+    call reused): consecutive calls, a weight reload (version bump), a replaced normalisation object and a
+    changed horizon each return exactly what a fresh controller returns from the same NumPy state, and
+    leave NumPy's stream where it leaves it."""
+    from bc_mpc_amd import MPCcontroller, cheetah_cost_fn
+    from bc_mpc_amd.dynamics import NNDynamicsModel
+    from oracle import mpc_oracle as orc
+    S, A, K, H = 20, 6, 400, 7
+
+    class Box:
+        low, high = -np.ones(A), np.ones(A)
+        shape = (A,)
+
+    class Env:
+        action_space = Box()
+
+        class observation_space:
+            shape = (S,)
+
+    norm = orc.synthetic_normalization(S, A)
+    w = orc.synthetic_weights(S, A, 256, 2, "relu", True)
+    w2 = orc.synthetic_weights(S, A, 256, 2, "relu", True, seed_base=5)
+
+    def model(wt):
+        m = NNDynamicsModel(Env(), 2, 256, "relu", None, list(norm), 512, 1, 1e-3, layer_norm=True, device=0)
+        m.load_weights(wt.kernels, wt.biases, wt.ln_gamma, wt.ln_beta)
+        return m
+
+    state = orc.synthetic_state(norm)
+    dm = model(w)
+    ctrl = MPCcontroller(Env(), dm, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K)
+
+    def fresh(wt, h, nrm=None):
+        m = model(wt)
+        if nrm is not None:
+            m.std_obs = nrm
+        return MPCcontroller(Env(), m, horizon=h, cost_fn=cheetah_cost_fn, num_simulated_paths=K)
+
+    def same(step, ref_ctrl):
+        st = np.random.get_state()
+        want = ref_ctrl.get_action(state)
+        want_next = np.random.get_state()
+        np.random.set_state(st)
+        got = ctrl.get_action(state)
+        got_next = np.random.get_state()
+        assert np.array_equal(got, want), step
+        assert np.array_equal(got_next[1], want_next[1]) and got_next[2] == want_next[2], step
+        ref_ctrl._engine.close()
+
+    np.random.seed(11)
+    for i in range(3):
+        same(f"repeat {i}", fresh(w, H))
+    assert ctrl._fast is not None                      # the repeat path is the one under test
+    dm.load_weights(w2.kernels, w2.biases, w2.ln_gamma, w2.ln_beta)
+    same("weights reloaded", fresh(w2, H))
+    dm.std_obs = np.asarray(norm[1]) * 1.5
+    same("normalisation replaced", fresh(w2, H, dm.std_obs))
+    ctrl.horizon = 5
+    same("horizon changed", fresh(w2, 5, dm.std_obs))
+    ctrl._engine.close()

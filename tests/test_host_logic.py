@@ -188,3 +188,33 @@ def test_legacy_mt_state_pointers_are_numpys_own_state():
     pos_p[0] = want[2]
     assert np.array_equal(np.random.random(4), np.random.RandomState(5).random_sample(4))
     assert engine._legacy_mt_state() is mt                      # cached per generator object
+
+
+def test_replaced_normalisation_changes_the_engine_version():
+    """A normalisation attribute replaced on the model (same weights) gives a new engine version, so the
+    engine re-uploads it; the same objects keep the version (weights.extract / weight_token)."""
+    from oracle import mpc_oracle as orc
+    w = orc.synthetic_weights(20, 6, 64, 2, "relu", True)
+    dyn = orc.NumpyDynamics(w, orc.synthetic_normalization())
+    _, norm1, v1 = ww.extract(dyn)
+    assert ww.extract(dyn)[2] == v1
+    dyn.std_obs = np.asarray(dyn.std_obs) * 2.0
+    _, norm2, v2 = ww.extract(dyn)
+    assert v2 != v1 and np.array_equal(norm2[1], norm1[1] * 2.0)
+    assert ww.extract(dyn)[2] == v2
+
+    class Stamped:                                      # a model with its own version stamp (ours / TF hook)
+        version = 3
+
+        def mlp_spec(self):
+            return None
+    m = Stamped()
+    for n, a in zip(ww._NORM_ATTRS, orc.synthetic_normalization()):
+        setattr(m, n, a)
+    t1 = ww.weight_token(m)
+    assert ww.same_token(m, t1)
+    m.mean_obs = np.array(m.mean_obs)
+    assert not ww.same_token(m, t1)
+    t2 = ww.weight_token(m)
+    m.version = 4
+    assert not ww.same_token(m, t2) and ww.same_token(m, ww.weight_token(m))

@@ -82,6 +82,23 @@ def main():
     ctrl = MPCcontroller(bench._Env(), dyn, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K, device=0)
     np.random.seed(0)
     out["ctrl_ms"] = p50(lambda: ctrl.get_action(p["state"]), calls)
+
+    def slow():                                  # the repeat-call fast path off (every check redone)
+        ctrl._fast = None
+        ctrl.get_action(p["state"])
+    out["ctrl_slowpath_ms"] = p50(slow, calls)
+
+    def gap_p50(fn):
+        ts = []
+        for i in range(calls + 20):
+            with_gap()
+            t0 = time.perf_counter()
+            fn()
+            if i >= 20:
+                ts.append(time.perf_counter() - t0)
+        return float(np.median(ts) * 1e3)
+    out["ctrl_gap50us_ms"] = gap_p50(lambda: ctrl.get_action(p["state"]))
+    out["ctrl_slowpath_gap50us_ms"] = gap_p50(slow)
     out["np_draw_ms"] = p50(lambda: np.random.uniform(low, high, [H, K, A]), calls)
     print(json.dumps(out), flush=True)
 
