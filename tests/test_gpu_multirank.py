@@ -1,0 +1,130 @@
+"""The N > 1 path with the REAL engines (the CPU gloo tests substitute an oracle-backed
+shard engine): two ranks, one process each, both on this box's one GPU, torch.distributed over gloo for
+the exchange (RCCL refuses two ranks on one card; the library's RCCL communicator is covered by
+test_gpu_comm.py and the device select by bcmpc_select_results_async there).
+
+Each rank runs the drop-in controllers on its contiguous candidate shard (distributed.shard_range) with the
+HIP kernels, agrees on the argmin through the one all-gather per control step, and must return exactly
+what ONE rank holding all K candidates returns (a size-1 process group in the same process): per-candidate
+costs are shard invariant bitwise (test_gpu_parity), so the argmin, the first action, NumPy's stream
+position afterwards (parity mode: every rank draws the whole [H, K, A]) and the CEM iterations' elite sets
+and refits are identical.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Box:
+    def __init__(self, n, lo, hi):
+        self.low = np.full(n, lo, dtype=np.float32)
+        self.high = np.full(n, hi, dtype=np.float32)
+        self.shape = (n,)
+
+
+class _Env:
+    action_space = _Box(6, -1, 1)
+    observation_space = _Box(20, -np.inf, np.inf)
+
+
+CASES = {
+    # (controller, hidden, layers, act, ln, K, H, rng)
+    # (K large enough that a rank's shard and the whole K pick the same kernel layout: the team kernel
+    #  at one workgroup per column, or the split slab kernel with 64-candidate workgroups)
+    "mpc_ppo_net_numpy": ("mpc", 256, 2, "relu", True, 800, 7, "numpy"),        # team kernel, 400 per rank
+    "mpc_2x500_numpy": ("mpc", 500, 2, "tanh", False, 131072, 5, "numpy"),      # split4 slab kernel
+    "mpc_2x500_device": ("mpc", 500, 2, "tanh", False, 131072, 5, "device"),
+    "cem_2x500": ("cem", 500, 2, "tanh", False, 131072, 4, "device"),
+}
+
+
+def _run(ctrl_kind, hidden, L, act, ln, K, H, rng, group, steps=3):
+    import torch.distributed as dist  # noqa: F401
+    from bc_mpc_amd import MPCcontroller, cheetah_cost_fn
+    from bc_mpc_amd.cem import CEMcontroller
+    from bc_mpc_amd.dynamics import NNDynamicsModel
+    from oracle import mpc_oracle as orc
+    norm = orc.synthetic_normalization()
+    w = orc.synthetic_weights(20, 6, hidden, L, act, ln)
+    dm = NNDynamicsModel(_Env(), L, hidden, act, None, list(norm), 512, 1, 1e-3, layer_norm=ln, device=0)
+    dm.load_weights(w.kernels, w.biases, w.ln_gamma, w.ln_beta)
+    if ctrl_kind == "cem":
+        ctrl = CEMcontroller(_Env(), dm, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K, iterations=3,
+                             elite_frac=0.02, seed=7, device=0, process_group=group)
+    else:
+        ctrl = MPCcontroller(_Env(), dm, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K, rng=rng,
+                             seed=5 if rng == "device" else None, device=0, process_group=group)
+    state = orc.synthetic_state(norm)
+    np.random.seed(123)
+    acts = []
+    for _ in range(steps):
+        acts.append(np.asarray(ctrl.get_action(state), dtype=np.float64).tolist())
+        state = state + 0.01                        # a new state each control step
+    extra = float(np.random.random())               # the stream position the calls left behind
+    if ctrl._engine is not None:
+        ctrl._engine.close()
+    return acts, extra, getattr(ctrl, "last_mu", None)
+
+
+def _worker(rank, world, port, q, case):
+    import sys
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
+    solo = [dist.new_group([r]) for r in range(world)]          # (collective: every rank makes every group)
+    try:
+        acts, extra, mu = _run(*CASES[case], group=None)         # the world: K sharded over the ranks
+        ref = _run(*CASES[case], group=solo[rank])               # one rank holding all K candidates
+        q.put((rank, acts, extra, None if mu is None else mu.tolist(), ref[0], ref[1],
+               None if ref[2] is None else ref[2].tolist(), ""))
+    except Exception as exc:                                     # report, do not hang the parent
+        q.put((rank, None, None, None, None, None, None, repr(exc)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_two_ranks_real_engines_match_one_rank(case):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, case)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(2):
+            r, *rest = q.get(timeout=150)
+            out[r] = rest
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in (0, 1):
+        assert out[r][-1] == "", f"rank {r}: {out[r][-1]}"
+    acts0, extra0, mu0, ref_acts, ref_extra, ref_mu, _ = out[0]
+    acts1, extra1, mu1 = out[1][:3]
+    print(f"[{case}] 2-rank actions {np.round(np.asarray(acts0)[:, :3], 4).tolist()} ... "
+          f"1-rank identical: {acts0 == ref_acts}")
+    assert acts0 == acts1, "ranks disagree"
+    assert acts0 == ref_acts, "sharded result differs from one rank holding all candidates"
+    assert extra0 == extra1 == ref_extra, "NumPy's stream advanced differently"
+    if mu0 is not None:
+        assert mu0 == mu1 == ref_mu, "CEM refit differs"
