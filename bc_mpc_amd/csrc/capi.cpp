@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -183,6 +184,8 @@ struct bcmpc_engine {
         std::mutex mu;
         std::condition_variable cv;
         bool quit = false, pending = false, busy = false, ready = false;
+        // lock-free mirrors for the spinning handshake: a job posted and not yet finished / shutting down
+        std::atomic<bool> inflight{false}, quit_a{false};
         bool rows = true;               // false: only NumPy's state is needed (the stochastic policy)
         Mt19937 from, to;               // the state the rows were drawn from / leave behind
         std::vector<double> low, high;
@@ -595,6 +598,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
         {
             std::lock_guard<std::mutex> lk(e->pre.mu);
             e->pre.quit = true;
+            e->pre.quit_a.store(true, std::memory_order_release);
         }
         e->pre.cv.notify_all();
         e->pre.th.join();
@@ -1489,8 +1493,36 @@ static bool mt_predraw_enabled() {
     return on;
 }
 
+// The worker and the control thread hand jobs over by spinning first (BCMPC_MT_PREDRAW_SPIN_US, default
+// 200 us) and only then blocking on the condition variable: a futex wake of either side costs several
+// microseconds on a loaded host, the same order as the K = 400 draw itself
+static int64_t predraw_spin_ns() {
+    static const int64_t ns = [] {
+        const char* v = std::getenv("BCMPC_MT_PREDRAW_SPIN_US");
+        return (v && *v) ? std::max<int64_t>(0, std::atoll(v)) * 1000 : int64_t(200000);
+    }();
+    return ns;
+}
+
+// spin until *a == want or (b and *b), at most predraw_spin_ns()
+static void spin_until(const std::atomic<bool>* a, bool want, const std::atomic<bool>* b = nullptr) {
+    const int64_t lim = predraw_spin_ns();
+    if (lim <= 0) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto done = [&] {
+        return a->load(std::memory_order_acquire) == want || (b && b->load(std::memory_order_acquire));
+    };
+    for (uint32_t i = 1; !done(); ++i) {
+        if ((i & 255) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                  std::chrono::steady_clock::now() - t0).count() > lim)
+            return;
+        __builtin_ia32_pause();
+    }
+}
+
 // wait until the worker is idle (its buffer complete); returns the buffer index it last filled
 static int predraw_wait(bcmpc_engine* e) {
+    spin_until(&e->pre.inflight, false);
     std::unique_lock<std::mutex> lk(e->pre.mu);
     e->pre.cv.wait(lk, [&] { return !e->pre.pending && !e->pre.busy; });
     return e->pre.buf;
@@ -1511,6 +1543,7 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
         p.buf = e->zc_last ^ 1;
         p.ready = false;
         p.pending = true;
+        p.inflight.store(true, std::memory_order_release);
     }
     if (!p.th.joinable()) {
         p.th = std::thread([e] {
@@ -1518,6 +1551,11 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
             const bcmpc_config& c = e->cfg;
             std::unique_lock<std::mutex> lk(q.mu);
             for (;;) {
+                if (!q.quit && !q.pending) {              // spin for the next job before sleeping
+                    lk.unlock();
+                    spin_until(&q.inflight, true, &q.quit_a);
+                    lk.lock();
+                }
                 q.cv.wait(lk, [&] { return q.quit || q.pending; });
                 if (q.quit) return;
                 q.pending = false;
@@ -1539,6 +1577,7 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
                 q.to = g;
                 q.ready = true;
                 q.busy = false;
+                q.inflight.store(false, std::memory_order_release);
                 q.cv.notify_all();
             }
         });
