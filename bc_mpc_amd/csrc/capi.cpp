@@ -1568,7 +1568,10 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
                 lk.unlock();
                 const int64_t K = c.num_paths;
                 const size_t row = (size_t)K * c.action_dim;
-                if (rows)
+                if (rows && off == 0 && K == kg)          // the whole draw: one pass over [H * K] rows
+                    mt_uniform_rows(g, lo.data(), hi.data(), c.action_dim, (int64_t)c.horizon * kg, 0,
+                                    (int64_t)c.horizon * kg, dst);
+                else if (rows)
                     for (int h = 0; h < c.horizon; ++h)
                         mt_uniform_rows(g, lo.data(), hi.data(), c.action_dim, kg, off, off + K, dst + h * row);
                 else
@@ -1766,7 +1769,9 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         } else {
             b = e->zc_last ^ 1;
             if (predraw) ++e->pre.misses;
-            if (rows_needed)
+            if (rows_needed && cand_offset == 0 && K == k_global)   // the whole draw: one pass
+                mt_uniform_rows(g, low, high, A, (int64_t)H * k_global, 0, (int64_t)H * k_global, e->h_zc[b]);
+            else if (rows_needed)
                 for (int h = 0; h < H; ++h)
                     mt_uniform_rows(g, low, high, A, k_global, cand_offset, cand_offset + K, e->h_zc[b] + h * row);
             else

@@ -38,6 +38,26 @@ def test_uniform_matches_numpy_stream(seed, pre_words):
     assert np.array_equal(np.random.random(3), after)
 
 
+@pytest.mark.parametrize("A", [1, 3, 5, 8, 11, 16])
+@pytest.mark.parametrize("pre_words", [0, 1, 623, 1249])
+def test_uniform_any_action_dim(A, pre_words):
+    """The one-pass draw (every row kept) for action dims whose bound pattern spans 8..128 doubles."""
+    from bc_mpc_amd import _lib
+    lib = _lib.load()
+    rs = np.random.RandomState(A)
+    low = rs.uniform(-3, 0, A).astype(np.float32)
+    high = (low + rs.uniform(0.1, 4, A)).astype(np.float32)
+    np.random.seed(11)
+    np.random.randint(0, 2**31 - 1, size=pre_words, dtype=np.int64)
+    st = np.random.get_state()
+    want = np.random.uniform(low=low, high=high, size=[7, 97, A])
+    after = np.random.random(3)
+    np.random.set_state(st)
+    got = _draw(lib, low.astype(np.float64), high.astype(np.float64), 7 * 97).reshape(7, 97, A)
+    assert np.array_equal(got, want)
+    assert np.array_equal(np.random.random(3), after)
+
+
 def _draw_par(lib, low, high, n_rows, period, keep_lo, keep_hi, threads, min_words):
     st = np.random.get_state()
     key = np.array(st[1], dtype=np.uint32)
