@@ -175,6 +175,13 @@ struct bcmpc_engine {
     // (the kernel reads them over the bus); a call uses one while the pre-draw worker fills the other
     double* h_zc[2] = {nullptr, nullptr}; size_t zc_cap = 0;
     double* d_zc[2] = {nullptr, nullptr};
+    // the pre-draw worker also copies its rows into device memory (copy stream + event per buffer) while the
+    // caller's env step runs; a call whose copy has completed reads HBM instead of the bus (zero-copy rows
+    // cost the K = 400 kernel 3.7 us; BCMPC_MT_PREDRAW_DEV=0 turns the copy off)
+    double* d_rows[2] = {nullptr, nullptr};
+    hipStream_t copy_st = nullptr;
+    hipEvent_t copy_ev[2] = {nullptr, nullptr};
+    bool copy_valid[2] = {false, false};
     int zc_last = 0;                    // the buffer the last successful call read
     // pre-draw (BCMPC_MT_PREDRAW, default on): after a successful small draw, a worker thread draws the
     // rows the NEXT call would draw -- from NumPy's advanced state, same bounds / shard -- into the other
@@ -605,6 +612,12 @@ int bcmpc_destroy(bcmpc_engine* e) {
     }
     for (double* p : e->h_zc)
         if (p) (void)hipHostFree(p);
+    if (e->copy_st) (void)hipStreamSynchronize(e->copy_st);
+    for (int i = 0; i < 2; ++i) {
+        if (e->d_rows[i]) (void)hipFree(e->d_rows[i]);
+        if (e->copy_ev[i]) (void)hipEventDestroy(e->copy_ev[i]);
+    }
+    if (e->copy_st) (void)hipStreamDestroy(e->copy_st);
     if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1493,6 +1506,14 @@ static bool mt_predraw_enabled() {
     return on;
 }
 
+static bool mt_predraw_dev() {
+    static const bool on = [] {
+        const char* v = std::getenv("BCMPC_MT_PREDRAW_DEV");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 // The worker and the control thread hand jobs over by spinning first (BCMPC_MT_PREDRAW_SPIN_US, default
 // 200 us) and only then blocking on the condition variable: a futex wake of either side costs several
 // microseconds on a loaded host, the same order as the K = 400 draw itself
@@ -1576,7 +1597,16 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
                         mt_uniform_rows(g, lo.data(), hi.data(), c.action_dim, kg, off, off + K, dst + h * row);
                 else
                     g.advance(2 * (int64_t)c.action_dim * c.horizon * kg);
+                bool copied = false;
+                const int qb = (int)(dst == e->h_zc[0] ? 0 : 1);
+                if (rows && e->copy_st && e->d_rows[qb]) {   // the rows into HBM while the caller's env step runs
+                    (void)hipSetDevice(c.device);
+                    copied = hipMemcpyAsync(e->d_rows[qb], dst, (size_t)c.horizon * row * sizeof(double),
+                                            hipMemcpyHostToDevice, e->copy_st) == hipSuccess &&
+                             hipEventRecord(e->copy_ev[qb], e->copy_st) == hipSuccess;
+                }
                 lk.lock();
+                e->copy_valid[qb] = copied;
                 q.to = g;
                 q.ready = true;
                 q.busy = false;
@@ -1751,6 +1781,18 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
                 HIP_TRY(hipHostMalloc(&e->h_zc[i], n * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
                 HIP_TRY(hipHostGetDevicePointer((void**)&e->d_zc[i], e->h_zc[i], 0));
             }
+            if (mt_predraw_dev()) {
+                if (!e->copy_st) {
+                    HIP_TRY(hipStreamCreateWithFlags(&e->copy_st, hipStreamNonBlocking));
+                    for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&e->copy_ev[i], hipEventDisableTiming));
+                }
+                for (int i = 0; i < 2; ++i) {
+                    if (e->d_rows[i]) (void)hipFree(e->d_rows[i]);
+                    e->d_rows[i] = nullptr;
+                    e->copy_valid[i] = false;
+                    HIP_TRY(hipMalloc(&e->d_rows[i], n * sizeof(double)));
+                }
+            }
             e->zc_cap = n;
         }
         Mt19937 g;
@@ -1762,10 +1804,16 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
                          std::memcmp(low, e->pre.low.data(), sizeof(double) * A) == 0 &&
                          std::memcmp(high, e->pre.high.data(), sizeof(double) * A) == 0;
         e->pre.ready = false;
+        const double* rows_ptr = nullptr;
         if (hit) {                                    // NumPy's stream is exactly where the worker drew from
             b = e->pre.buf;
             g = e->pre.to;
             ++e->pre.hits;
+            // (its device copy, when it has landed: the kernel then reads HBM instead of the bus)
+            // (the stream wait orders and publishes the copy for the kernel; it has already completed)
+            if (rows_needed && e->copy_valid[b] && hipEventQuery(e->copy_ev[b]) == hipSuccess &&
+                hipStreamWaitEvent(e->stream, e->copy_ev[b], 0) == hipSuccess)
+                rows_ptr = e->d_rows[b];
         } else {
             b = e->zc_last ^ 1;
             if (predraw) ++e->pre.misses;
@@ -1781,7 +1829,9 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         if (!lean)
             HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
         e->want_done = lean && !costs_out;
-        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, rows_needed ? e->d_zc[b] : nullptr, seed, cand_offset,
+        if (!rows_ptr && rows_needed) rows_ptr = e->d_zc[b];
+        e->copy_valid[b] = false;                     // (the next fill of this buffer replaces it)
+        int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, rows_ptr, seed, cand_offset,
                               e->d_costs, nullptr,
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
