@@ -1219,9 +1219,16 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     // BCMPC_FUSED_ARGMIN=1: the split kernel reduces np.argmin in its own tail (one launch per
     // get_action).  Off by default: the tail's ticket + acquire cost ~6 us in-kernel, as much as the
     // two argmin launches it replaces, and p50 did not move (cfg1/cfg2/run.sh recipe)
+    // The team kernel (small K: a few dozen workgroups) reduces it in its tail by default (round 3; one
+    // launch per control step instead of two; BCMPC_TEAM_FUSED_ARGMIN=0 restores the argmin launch)
     const char* fa = std::getenv("BCMPC_FUSED_ARGMIN");
-    const bool fused = e->split && e->kernel != BCMPC_KERNEL_SPLITR && e->kernel != BCMPC_KERNEL_TEAM && d_result &&
-                       fa && fa[0] == '1';
+    static const bool team_fused = [] {
+        const char* v = std::getenv("BCMPC_TEAM_FUSED_ARGMIN");
+        return !(v && v[0] == '0');
+    }();
+    const bool fused = d_result && !cem &&
+                       (e->kernel == BCMPC_KERNEL_TEAM ? team_fused
+                                                       : e->split && e->kernel != BCMPC_KERNEL_SPLITR && fa && fa[0] == '1');
     if (fused) {
         a.fused_argmin = 1;
         a.amin = m;
@@ -1230,6 +1237,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     record_events = record_events && e->timing;
     e->timed = false;
     if (record_events) HIP_TRY(hipEventRecord(e->ev[0], st));
+    bool team_skipped = false;
     if (e->kernel == BCMPC_KERNEL_TEAM) {
         a.team_buf = e->d_team;
         a.team_ctl = e->d_team_ctl;
@@ -1254,10 +1262,12 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             HIP_TRY(hipMemsetAsync(d_tst, 0, tst_n * sizeof(uint64_t), st));
             a.stamps = d_tst;
         }
-        if (a.team_spins < 0)
+        if (a.team_spins < 0) {
             __atomic_store_n(e->h_team_err, 1u, __ATOMIC_RELEASE);
-        else
+            team_skipped = true;                      // (no tail ran: the argmin launch raises the done word)
+        } else {
             HIP_TRY(launch_rollout_team(a, e->HP, st));
+        }
         if (!e->sync_call)
             if (const int rc = team_order_after(c.device, st)) return rc;
         if (stamps) {
@@ -1351,7 +1361,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         HIP_TRY(launch_rollout_grp(a, e->HP, kern_waves(e->kernel), st));
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[1], st));
-    if (d_result && !fused) HIP_TRY(launch_argmin(m, st));
+    if (d_result && (!fused || team_skipped)) HIP_TRY(launch_argmin(m, st));
     if (d_result && e->comm && !cem) {
         // the one collective of a sharded control step: every rank's record, then np.argmin's rule
         std::string err;

@@ -46,6 +46,7 @@
 #include "device_common.h"
 #include "kernels.h"
 #include "split_common.h"
+#include "argmin_common.h"
 
 namespace bcmpc {
 
@@ -306,6 +307,7 @@ void rollout_team(const RolloutArgs a) {
     unsigned gen = 0;
     if constexpr (T > 1) gen = __hip_atomic_load(a.team_ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
+    Best mybest{__builtin_inf(), INT64_MAX};              // (fused argmin) this workgroup's candidate
     if (col < ncol) {
         char* const base = reinterpret_cast<char*>(lds);
         double* C = reinterpret_cast<double*>(base);
@@ -1045,9 +1047,72 @@ void rollout_team(const RolloutArgs a) {
             stamp(8);
         }
         if (writer && a.costs && valid && q == qc) a.costs[cand] = cost;
+        if (writer && valid && q == qc) mybest = Best{a.amin.maximize ? -cost : cost, cand};
         if constexpr (TEAM_STAMP) {
             if (a.stamps && lane == 0)
                 for (int k = 0; k < 10; ++k) a.stamps[((size_t)blockIdx.x * NWV + w) * 10 + k] = ph_[k];
+        }
+    }
+    if (a.fused_argmin && w == 0) {
+        // ---- np.argmin / argmax (controllers.py:82,152) in the launch's tail: every workgroup's best (wave 0
+        //      holds the costs: member 0's writer lanes) into the scratch records, the last workgroup to
+        //      arrive (ticket) reduces them and writes the result record + the done word -- no argmin launch
+        //      (the split kernel's recipe, wave-level: cdna_hip_programming.md "In-launch split-K reduction") ----
+        const ArgminArgs& am = a.amin;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const Best o{__shfl_xor(mybest.c, off), __shfl_xor(mybest.i, off)};
+            if (better(o, mybest)) mybest = o;
+        }
+        unsigned last = 0;
+        if (lane == 0) {
+            __hip_atomic_store(&am.scratch_c[blockIdx.x], mybest.c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&am.scratch_i[blockIdx.x], mybest.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the act_out rows and the record before the ticket)
+            const unsigned t = __hip_atomic_fetch_add(a.amin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = t == gridDim.x - 1 ? 1u : 0u;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        last = __shfl(last, 0);
+        if (last) {
+            Best best{__builtin_inf(), INT64_MAX};
+            for (unsigned b = lane; b < gridDim.x; b += 64) {
+                const Best o{__hip_atomic_load(&am.scratch_c[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                             __hip_atomic_load(&am.scratch_i[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+                if (better(o, best)) best = o;
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const Best o{__shfl_xor(best.c, off), __shfl_xor(best.i, off)};
+                if (better(o, best)) best = o;
+            }
+            // the record: index, cost, first action (lanes j < BCMPC_MAX_ACTION in parallel, as argmin_write_block)
+            bcmpc_result* out = am.out;
+            const int64_t bi = best.i;
+            if (lane == 0) {
+                out->best_index = am.cand_offset + bi;
+                out->best_cost = am.maximize ? -best.c : best.c;
+            }
+            if (lane < BCMPC_MAX_ACTION) {
+                double v = 0.0;
+                if (bi < am.K && lane < am.A) {
+                    const uint64_t g = (uint64_t)(am.cand_offset + bi);
+                    v = am.act_out ? am.act_out[bi * am.A + lane]
+                        : am.actions ? am.actions[bi * am.A + lane]
+                                     : rng_action(am.seed, g, 0, lane, am.consts[6 * 32 + lane], am.consts[7 * 32 + lane]);
+                }
+                out->first_action[lane] = v;
+            }
+            if (lane == 0) {
+                __hip_atomic_store(a.amin_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+                if (am.done) {
+                    __threadfence_system();
+                    __hip_atomic_store(am.done, am.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
         }
     }
     if constexpr (T > 1) {
