@@ -353,6 +353,7 @@ class MPCcontrollerPolicyNet(Controller):
         self._group = process_group
         self._engine = None
         self._engine_key = None
+        self._fast = None                       # get_action's repeat-call fast path
         self.last_cost = None
         self.last_index = None
         self.last_costs = None
@@ -387,8 +388,29 @@ class MPCcontrollerPolicyNet(Controller):
 
     _MODEL = "delta"     # NNDynamicsModel + cheetah cost, argmin
 
+    def _fast_key(self):
+        return (self.env, self.dyn_model, self.policy_net, self.cost_fn, self.horizon, self.num_simulated_paths,
+                self.explore, self.self_exp, self.keep_costs)
+
     # controllers.py:189-237
     def get_action(self, state):
+        fp = getattr(self, "_fast", None)
+        if fp is not None:
+            # the per-env-step repeat (as MPCcontroller.get_action): same env / models / cost / shape /
+            # exploration as the last call, the dynamics weights version and normalisation objects and the
+            # policy's integer version unchanged, one rank, NumPy's verified legacy stream
+            from .engine import _legacy_mt_state
+            if (fp[0] == self._fast_key() and _weights.same_token(self.dyn_model, fp[1])
+                    and _policy.int_version(self.policy_net) == fp[2] and "sample_random_actions" not in self.__dict__
+                    and _dist.world(self._group)[1] == 1 and _legacy_mt_state() is not None):
+                space = self.env.action_space
+                seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+                res = fp[3].get_action_numpy_stream(state, space.low, space.high, fp[4], 0, seed=seed)
+                if res is not None:
+                    self.last_costs = None
+                    self.last_cost, self.last_index = res.best_cost, res.best_index
+                    return res.first_action
+            self._fast = None
         S = int(math.prod(self.env.observation_space.shape))
         A = len(self.env.action_space.high)
         K = int(self.num_simulated_paths)
@@ -421,6 +443,9 @@ class MPCcontrollerPolicyNet(Controller):
                 cost, index, first_g = _minloc(self, eng, True, sign * res.best_cost, res.best_index,
                                                res.first_action, A)
                 self.last_cost, self.last_index = sign * cost, index
+                tok, pv = _weights.weight_token(self.dyn_model), _policy.int_version(self.policy_net)
+                if ws == 1 and not self.keep_costs and tok is not None and pv is not None and eng.comm is None:
+                    self._fast = (self._fast_key(), tok, pv, eng, K)
                 return first_g
         exploration = self.sample_random_actions()           # every rank draws the full [H, K, A]
         seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))

@@ -380,16 +380,18 @@ class RolloutEngine:
             # the per-env-step call (no cost vector): ctypes arguments built once per (generator, bounds,
             # shard, seed) and reused -- the state goes into an engine-owned buffer, the first action is
             # copied out of a NumPy view on the result record (~6 us of Python per call less)
-            key = (k_global, cand_offset, seed)
+            key = (k_global, cand_offset)
             fa = self._mt_fast
             if fa is None or fa[0] != key or fa[5] is not bg or fa[6] is not bounds:
                 sbuf = np.zeros(self.state_dim, dtype=np.float64)
                 res = _lib.Result()
                 first = np.ctypeslib.as_array(res.first_action)[: self.action_dim]
+                cseed = ctypes.c_uint64(0)
                 args = (self._h, _dp(sbuf), key_p, pos_p, _dp(bounds[0]), _dp(bounds[1]), ctypes.c_int64(k_global),
-                        ctypes.c_int64(cand_offset), ctypes.c_uint64(seed & (2**64 - 1)), ctypes.byref(res), None)
-                fa = self._mt_fast = (key, sbuf, res, first, args, bg, bounds)
+                        ctypes.c_int64(cand_offset), cseed, ctypes.byref(res), None)
+                fa = self._mt_fast = (key, sbuf, res, first, args, bg, bounds, cseed)
             _, sbuf, res, first, args = fa[:5]
+            fa[7].value = seed & (2**64 - 1)           # (the policy controllers' per-call Philox seed)
             s = state if type(state) is np.ndarray else _f64(state)
             if s.size != self.state_dim:
                 raise ValueError(f"state has {s.size} dims, expected {self.state_dim}")

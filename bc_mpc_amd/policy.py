@@ -87,6 +87,12 @@ def _tf_policy(policy_net, tf=None) -> PolicySpec:
     return PolicySpec(ks, bs, mean, std.astype(np.float32), logstd.astype(np.float32))
 
 
+def int_version(policy_net):
+    """The policy container's own integer ``version`` (trusted, as by extract), else None."""
+    v = getattr(policy_net, "version", None)
+    return v if isinstance(v, int) and not isinstance(v, bool) else None
+
+
 def extract(policy_net) -> Tuple[PolicySpec, int]:
     if hasattr(policy_net, "policy_spec"):
         spec = policy_net.policy_spec()

@@ -726,3 +726,73 @@ def test_dropin_repeat_fast_path_tracks_changes():
     ctrl.horizon = 5
     same("horizon changed", fresh(w2, 5, dm.std_obs))
     ctrl._engine.close()
+
+
+def test_policy_dropin_repeat_fast_path_tracks_changes():
+    """MPCcontrollerPolicyNet's repeat-call fast path (train_mpc_ppo's default MPC-aug controller: explore 0.5
+    over the 2x256 relu + LN net): repeated calls, a new policy (integer version bumped), a changed explore
+    and a reloaded dynamics net each return exactly what a fresh controller returns from the same NumPy state
+    (and the same private seed stream), and leave NumPy's stream where it leaves it."""
+    from bc_mpc_amd import MPCcontrollerPolicyNet, cheetah_cost_fn
+    from bc_mpc_amd.dynamics import NNDynamicsModel
+    from bc_mpc_amd.engine import PolicySpec
+    from oracle import mpc_oracle as orc
+    S, A, K, H = 20, 6, 400, 7
+
+    class Box:
+        low, high = -np.ones(A), np.ones(A)
+        shape = (A,)
+
+    class Env:
+        action_space = Box()
+
+        class observation_space:
+            shape = (S,)
+
+    class Pol:                                          # a versioned policy container (policy.extract)
+        def __init__(self, p, version):
+            self._spec = PolicySpec(p.kernels, p.biases, p.ob_mean, p.ob_std, p.logstd)
+            self.version = version
+
+        def policy_spec(self):
+            return self._spec
+
+    norm = orc.synthetic_normalization(S, A)
+    w, w2 = orc.synthetic_weights(S, A, 256, 2, "relu", True), orc.synthetic_weights(S, A, 256, 2, "relu", True, seed_base=9)
+    p1, p2 = orc.synthetic_policy(S, A), orc.synthetic_policy(S, A, seed=77)
+
+    def model(wt):
+        m = NNDynamicsModel(Env(), 2, 256, "relu", None, list(norm), 512, 1, 1e-3, layer_norm=True, device=0)
+        m.load_weights(wt.kernels, wt.biases, wt.ln_gamma, wt.ln_beta)
+        return m
+
+    state = orc.synthetic_state(norm)
+    dm, pol = model(w), Pol(p1, 1)
+    ctrl = MPCcontrollerPolicyNet(Env(), dm, pol, explore=0.5, self_exp=False, horizon=H, cost_fn=cheetah_cost_fn,
+                                  num_simulated_paths=K, seed=3)
+
+    def same(step, wt, pp, explore):
+        ref = MPCcontrollerPolicyNet(Env(), model(wt), Pol(pp, 1), explore=explore, self_exp=False, horizon=H,
+                                     cost_fn=cheetah_cost_fn, num_simulated_paths=K, seed=3)
+        ref._seed_rng.set_state(ctrl._seed_rng.get_state())
+        st = np.random.get_state()
+        want = ref.get_action(state)
+        want_next = np.random.get_state()
+        np.random.set_state(st)
+        got = ctrl.get_action(state)
+        got_next = np.random.get_state()
+        assert np.array_equal(got, want), step
+        assert np.array_equal(got_next[1], want_next[1]) and got_next[2] == want_next[2], step
+        ref._engine.close()
+
+    np.random.seed(5)
+    for i in range(3):
+        same(f"repeat {i}", w, p1, 0.5)
+    assert ctrl._fast is not None                      # the repeat path is the one under test
+    ctrl.policy_net = Pol(p2, 2)
+    same("new policy", w, p2, 0.5)
+    ctrl.explore = 0.3
+    same("explore changed", w, p2, 0.3)
+    dm.load_weights(w2.kernels, w2.biases, w2.ln_gamma, w2.ln_beta)
+    same("dynamics reloaded", w2, p2, 0.3)
+    ctrl._engine.close()
