@@ -141,6 +141,7 @@ SIGNATURES = [
     ("bcmpc_destroy", ctypes.c_int, [ctypes.c_void_p]),
     ("bcmpc_set_weights", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Weights), ctypes.c_uint64]),
     ("bcmpc_weights_version", ctypes.c_uint64, [ctypes.c_void_p]),
+    ("bcmpc_predraw_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     ("bcmpc_set_policy", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Policy), ctypes.c_uint64]),
     ("bcmpc_first_actions", ctypes.c_int, [ctypes.c_void_p, _DP]),
     ("bcmpc_set_discount", ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),

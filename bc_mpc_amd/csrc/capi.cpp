@@ -175,6 +175,12 @@ struct bcmpc_engine {
     // (the kernel reads them over the bus); a call uses one while the pre-draw worker fills the other
     double* h_zc[2] = {nullptr, nullptr}; size_t zc_cap = 0;
     double* d_zc[2] = {nullptr, nullptr};
+    // late pre-draw hit (team kernel): the worker publishes each job's sequence number into this mapped
+    // host word after its last row; a call that finds its rows still being drawn launches at once and the
+    // kernel waits for the word (BCMPC_MT_PREDRAW_LATE=0: the call waits on the host instead)
+    uint32_t* h_rows_seq = nullptr;
+    uint32_t* d_rows_seq = nullptr;
+    uint32_t rows_wait_seq = 0;         // (the next team launch waits for this sequence number; 0: none)
     // the pre-draw worker also copies its rows into device memory (copy stream + event per buffer) while the
     // caller's env step runs; a call whose copy has completed reads HBM instead of the bus (zero-copy rows
     // cost the K = 400 kernel 3.7 us; BCMPC_MT_PREDRAW_DEV=0 turns the copy off)
@@ -193,12 +199,14 @@ struct bcmpc_engine {
         bool quit = false, pending = false, busy = false, ready = false;
         // lock-free mirrors for the spinning handshake: a job posted and not yet finished / shutting down
         std::atomic<bool> inflight{false}, quit_a{false};
+        std::atomic<bool> claimed{false};   // a call already reads this job's pinned rows: no device copy
+        uint32_t job = 0;                   // the posted job's sequence number (published to h_rows_seq)
         bool rows = true;               // false: only NumPy's state is needed (the stochastic policy)
         Mt19937 from, to;               // the state the rows were drawn from / leave behind
         std::vector<double> low, high;
         int64_t kg = 0, off = 0;
         int buf = 0;
-        uint64_t hits = 0, misses = 0;
+        uint64_t hits = 0, late = 0, misses = 0;   // hits include the late ones
     } pre;
     double* d_costs = nullptr;
     bcmpc_result* d_result = nullptr;
@@ -612,6 +620,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
     }
     for (double* p : e->h_zc)
         if (p) (void)hipHostFree(p);
+    if (e->h_rows_seq) (void)hipHostFree(e->h_rows_seq);
     if (e->copy_st) (void)hipStreamSynchronize(e->copy_st);
     for (int i = 0; i < 2; ++i) {
         if (e->d_rows[i]) (void)hipFree(e->d_rows[i]);
@@ -627,6 +636,14 @@ int bcmpc_destroy(bcmpc_engine* e) {
 }
 
 uint64_t bcmpc_weights_version(const bcmpc_engine* e) { return e ? e->version : 0; }
+
+int bcmpc_predraw_stats(const bcmpc_engine* e, uint64_t* out3) {
+    if (!e || !out3) return fail(BCMPC_ERR_ARG, "null argument");
+    out3[0] = e->pre.hits;
+    out3[1] = e->pre.late;
+    out3[2] = e->pre.misses;
+    return BCMPC_OK;
+}
 
 int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version) {
     if (!e || !w || !w->kernels || !w->biases) return fail(BCMPC_ERR_ARG, "null argument");
@@ -1242,6 +1259,9 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         a.team_buf = e->d_team;
         a.team_ctl = e->d_team_ctl;
         a.team_err = e->d_team_err;
+        a.rows_flag = e->rows_wait_seq ? e->d_rows_seq : nullptr;
+        a.rows_seq = e->rows_wait_seq;
+        e->rows_wait_seq = 0;
         // BCMPC_TEAM_SPINS (tests): exchange polls before a member gives up; -1: the launch is skipped and
         // reported as a team that gave up (forces the fallback path deterministically)
         const char* sv = std::getenv("BCMPC_TEAM_SPINS");
@@ -1516,6 +1536,14 @@ static bool mt_predraw_enabled() {
     return on;
 }
 
+static bool mt_predraw_late() {
+    static const bool on = [] {
+        const char* v = std::getenv("BCMPC_MT_PREDRAW_LATE");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 static bool mt_predraw_dev() {
     static const bool on = [] {
         const char* v = std::getenv("BCMPC_MT_PREDRAW_DEV");
@@ -1574,6 +1602,8 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
         p.buf = e->zc_last ^ 1;
         p.ready = false;
         p.pending = true;
+        p.job = p.job + 1 == 0 ? 1 : p.job + 1;       // (0 is "no wait")
+        p.claimed.store(false, std::memory_order_relaxed);
         p.inflight.store(true, std::memory_order_release);
     }
     if (!p.th.joinable()) {
@@ -1595,8 +1625,12 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
                 const std::vector<double> lo = q.low, hi = q.high;
                 const int64_t kg = q.kg, off = q.off;
                 const bool rows = q.rows;
+                const uint32_t job = q.job;
                 double* dst = e->h_zc[q.buf];
                 lk.unlock();
+                // (tests: BCMPC_MT_PREDRAW_DELAY_US holds every job back, so calls find it in flight)
+                if (const char* dv = std::getenv("BCMPC_MT_PREDRAW_DELAY_US"))
+                    std::this_thread::sleep_for(std::chrono::microseconds(std::atoll(dv)));
                 const int64_t K = c.num_paths;
                 const size_t row = (size_t)K * c.action_dim;
                 if (rows && off == 0 && K == kg)          // the whole draw: one pass over [H * K] rows
@@ -1607,9 +1641,13 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
                         mt_uniform_rows(g, lo.data(), hi.data(), c.action_dim, kg, off, off + K, dst + h * row);
                 else
                     g.advance(2 * (int64_t)c.action_dim * c.horizon * kg);
+                if (rows && e->h_rows_seq)                // (x86 stores are ordered: the rows before the word)
+                    __atomic_store_n(e->h_rows_seq, job, __ATOMIC_RELEASE);
                 bool copied = false;
                 const int qb = (int)(dst == e->h_zc[0] ? 0 : 1);
-                if (rows && e->copy_st && e->d_rows[qb]) {   // the rows into HBM while the caller's env step runs
+                // the rows into HBM while the caller's env step runs (not when a call already reads them
+                // from the pinned buffer: the copy would only share the bus with that kernel)
+                if (rows && e->copy_st && e->d_rows[qb] && !q.claimed.load(std::memory_order_acquire)) {
                     (void)hipSetDevice(c.device);
                     copied = hipMemcpyAsync(e->d_rows[qb], dst, (size_t)c.horizon * row * sizeof(double),
                                             hipMemcpyHostToDevice, e->copy_st) == hipSuccess &&
@@ -1775,10 +1813,27 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         const int64_t K = c.num_paths;
         const int A = c.action_dim, H = c.horizon;
         const size_t row = (size_t)K * A, n = (size_t)H * row;
-        // (no pre-draw is running past this point: the worker finishes its job before the buffers change)
         const bool predraw = mt_predraw_enabled();
-        int b = predraw_wait(e);
-        if (n > e->zc_cap) {
+        Mt19937 g;
+        std::memcpy(g.key, mt_key, sizeof(g.key));
+        g.pos = *mt_pos;
+        auto same_job = [&] {                         // the posted job draws exactly this call's rows
+            const auto& p = e->pre;
+            return p.rows == rows_needed && p.kg == k_global && p.off == cand_offset && g.pos == p.from.pos &&
+                   std::memcmp(g.key, p.from.key, sizeof(g.key)) == 0 &&
+                   std::memcmp(low, p.low.data(), sizeof(double) * A) == 0 &&
+                   std::memcmp(high, p.high.data(), sizeof(double) * A) == 0;
+        };
+        // late hit (team kernel): the worker is still drawing this call's rows (a caller with no host work
+        // between calls) -- launch now, the kernel waits for the rows' sequence word instead of the host
+        // waiting for the worker (the job's parameters are written only by this thread, in predraw_post)
+        const bool late = predraw && mt_predraw_late() && e->kernel == BCMPC_KERNEL_TEAM && e->h_rows_seq &&
+                          n <= e->zc_cap && e->pre.inflight.load(std::memory_order_acquire) && same_job();
+        if (late) e->pre.claimed.store(true, std::memory_order_release);
+        // (otherwise no pre-draw is running past this point: the worker finishes its job before the buffers
+        //  change)
+        int b = late ? e->pre.buf : predraw_wait(e);
+        if (!late && n > e->zc_cap) {
             // fine-grained host memory: no GPU cache keeps an earlier call's rows (the rows change every call)
             for (int i = 0; i < 2; ++i) {
                 if (e->h_zc[i]) (void)hipHostFree(e->h_zc[i]);
@@ -1803,19 +1858,24 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
                     HIP_TRY(hipMalloc(&e->d_rows[i], n * sizeof(double)));
                 }
             }
+            if (!e->h_rows_seq) {
+                HIP_TRY(hipHostMalloc(&e->h_rows_seq, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+                HIP_TRY(hipHostGetDevicePointer((void**)&e->d_rows_seq, e->h_rows_seq, 0));
+                __atomic_store_n(e->h_rows_seq, 0u, __ATOMIC_RELEASE);
+            }
             e->zc_cap = n;
         }
-        Mt19937 g;
-        std::memcpy(g.key, mt_key, sizeof(g.key));
-        g.pos = *mt_pos;
-        const bool hit = predraw && e->pre.ready && e->pre.rows == rows_needed && e->pre.kg == k_global &&
-                         e->pre.off == cand_offset &&
-                         g.pos == e->pre.from.pos && std::memcmp(g.key, e->pre.from.key, sizeof(g.key)) == 0 &&
-                         std::memcmp(low, e->pre.low.data(), sizeof(double) * A) == 0 &&
-                         std::memcmp(high, e->pre.high.data(), sizeof(double) * A) == 0;
-        e->pre.ready = false;
+        const bool hit = !late && predraw && e->pre.ready && same_job();
+        if (!late) e->pre.ready = false;
         const double* rows_ptr = nullptr;
-        if (hit) {                                    // NumPy's stream is exactly where the worker drew from
+        if (late) {                                   // the kernel reads the pinned rows once published
+            if (rows_needed) {
+                rows_ptr = e->d_zc[b];
+                e->rows_wait_seq = e->pre.job;
+            }
+            ++e->pre.hits;
+            ++e->pre.late;
+        } else if (hit) {                                    // NumPy's stream is exactly where the worker drew from
             b = e->pre.buf;
             g = e->pre.to;
             ++e->pre.hits;
@@ -1840,11 +1900,12 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
         e->want_done = lean && !costs_out;
         if (!rows_ptr && rows_needed) rows_ptr = e->d_zc[b];
-        e->copy_valid[b] = false;                     // (the next fill of this buffer replaces it)
+        if (!late) e->copy_valid[b] = false;          // (the next fill of this buffer replaces it)
         int rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, rows_ptr, seed, cand_offset,
                               e->d_costs, nullptr,
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
+        e->rows_wait_seq = 0;
         const bool spin = e->want_done && rc == BCMPC_OK;
         e->want_done = false;
         if (rc == BCMPC_OK && !lean &&
@@ -1859,6 +1920,11 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: the kernel reads h_zc)
             if (rc != BCMPC_OK) return rc;
             if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+        }
+        if (late) {                                   // (the job is finished: the kernel has read its rows)
+            predraw_wait(e);
+            g = e->pre.to;
+            e->pre.ready = false;
         }
         if (team_failed(e)) {                         // (NumPy's state not yet advanced)
             if (const int fr = team_fallback(e)) return fr;

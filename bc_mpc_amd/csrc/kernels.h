@@ -95,6 +95,11 @@ struct RolloutArgs {
     unsigned* team_ctl;
     unsigned* team_err;
     int32_t team_spins;                      // exchange polls before a member gives up (0: the default, ~1 s)
+    // (team kernel, the drop-in's late pre-draw hit) the actions are host rows that the pre-draw worker is
+    // still writing: every workgroup waits until this mapped host word equals rows_seq before its first
+    // read of them (nullptr: the rows are complete at launch)
+    const uint32_t* rows_flag;
+    uint32_t rows_seq;
     // (team kernel, the reward net with LayerNorm heads) [8 members][32 rows]: sum over member t's head
     // rows of the gamma-folded, scaled output weights (the centring correction, rollout_team.hip)
     const float* head_rs;

@@ -67,6 +67,7 @@ namespace {
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 constexpr int kTeamSpins = 1 << 20;      // exchange polls before a team gives up (~1 s)
+constexpr uint64_t kRowsWaitTicks = 20000000;   // late pre-draw rows: give up after 0.2 s (100-MHz clock)
 constexpr int kTeamNch = 16;             // steps of action inputs staged in LDS per fill
 constexpr int kPolNch = 8;               // steps of the policy's draws (f64) staged per fill
 
@@ -375,7 +376,23 @@ void rollout_team(const RolloutArgs a) {
         if constexpr (PHP == 0)
             for (int i = threadIdx.x; i < kTeamNch * 16 * 16; i += blockDim.x)
                 if ((i & 15) >= A) xas[i] = 0.f;            // action slots past A stay zero (fill writes j < A)
-        __syncthreads();                                  // parameters in LDS
+        if (a.rows_flag && threadIdx.x == 0) {
+            // late pre-draw hit (capi.cpp): the host worker publishes the rows' sequence number after its
+            // last row; its stores are ordered, so a system-scope acquire of the word makes every row visible
+            // (fine-grained host memory: no GPU cache holds an older copy).  A worker that never publishes
+            // gives up after ~0.2 s (100-MHz real-time clock): the team's error word makes the host rerun
+            // the call on its fallback engine with a fresh draw
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(a.rows_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != a.rows_seq) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kRowsWaitTicks) {
+                    if (a.team_err) __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        }
+        __syncthreads();                                  // parameters in LDS (and the rows published)
         pstamp(0);
         // ---- actions, normalised (dynamics.py:110) and cast to f32 (the TF feed), staged in LDS for
         //      kTeamNch steps at a time by the whole workgroup (one action per thread and pass, not per

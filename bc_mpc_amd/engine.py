@@ -294,6 +294,12 @@ class RolloutEngine:
     def weights_version(self) -> int:
         return int(self._lib.bcmpc_weights_version(self._h))
 
+    def predraw_stats(self) -> dict:
+        """The NumPy-stream pre-draw's counters (bcmpc_predraw_stats): hits (incl. late), late, misses."""
+        out = (ctypes.c_uint64 * 3)()
+        _lib.check(self._lib.bcmpc_predraw_stats(self._h, out))
+        return {"hits": int(out[0]), "late": int(out[1]), "misses": int(out[2])}
+
     def set_action_bounds(self, low, high) -> None:
         lo, hi = _f64(low), _f64(high)
         _lib.check(self._lib.bcmpc_set_action_bounds(self._h, _dp(lo), _dp(hi)))

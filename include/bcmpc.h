@@ -246,6 +246,14 @@ int bcmpc_get_action_mt19937(bcmpc_engine* eng, const double* state, uint32_t* m
                              const double* low, const double* high, int64_t k_global, int64_t cand_offset,
                              uint64_t seed, bcmpc_result* out, double* costs_out);
 
+/* Small draws (<= BCMPC_MT_ZC_WORDS generator words, the reference's K = 400 steps) of
+ * bcmpc_get_action_mt19937: after a call, a worker thread draws the NEXT call's rows from the advanced
+ * state; a call whose (key, pos, bounds, shard) equal that job's start uses them -- a hit (rows
+ * complete, copied into HBM when the copy has landed) or, on team-kernel engines, a late hit (the job
+ * still running: the kernel waits for the rows' sequence word in mapped memory) -- else it draws itself
+ * (a miss).  out3 = {hits incl. late, late hits, misses} since bcmpc_create. */
+int bcmpc_predraw_stats(const bcmpc_engine* eng, uint64_t* out3);
+
 /* The same draw as bcmpc_get_action_mt19937 on the device, alone: this engine's shard
  * [H, K, A] of np.random.uniform(low, high, [H, k_global, A]) (controllers.py:53) drawn on the GPU
  * from (mt_key, mt_pos), copied to `out` (host, H*K*A doubles); mt_key / mt_pos advance as the one

@@ -239,3 +239,55 @@ def test_stochastic_policy_dropin_advances_the_stream_only(K, H, monkeypatch):
         ctrl._engine.close()
     for a, b in zip(out["default"], out["host"]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("delay_us,expect", [(300, "late"), (400000, "rerun")])
+def test_late_predraw_hit_waits_for_the_rows(delay_us, expect, monkeypatch):
+    """Back-to-back NumPy-stream calls on a team-kernel engine (K = 400, H = 7, 2x256 relu + LN) while the
+    pre-draw worker is held back (BCMPC_MT_PREDRAW_DELAY_US): each call finds its rows still being drawn
+    and launches at once, the kernel waiting for the rows' sequence word (a late hit).  300 us: every late
+    call returns exactly the costs of the same engine on NumPy's own array; 0.4 s (past the kernel's 0.2-s
+    wait): the team gives up and the call is rerun on the fallback engine with a fresh draw.  NumPy's
+    stream ends where np.random.uniform leaves it either way (controllers.py:53)."""
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    monkeypatch.setenv("BCMPC_MT_PREDRAW", "1")
+    monkeypatch.setenv("BCMPC_MT_PREDRAW_DELAY_US", str(delay_us))
+    S, A, H, K = 20, 6, 7, 400
+    w = orc.synthetic_weights(S, A, 256, 2, "relu", True)
+    norm = orc.synthetic_normalization(S, A)
+    state = orc.synthetic_state(norm)
+    low, high = -np.ones(A), np.ones(A)
+    eng = RolloutEngine(S, A, 256, 2, "relu", True, H, K, device=0)
+    eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), norm, 1)
+    if eng.info()["kernel"] != "team":
+        eng.close()
+        pytest.skip("not a team-kernel engine")
+    np.random.seed(31)
+    calls = 6 if expect == "late" else 2
+    for i in range(calls):
+        st0 = np.random.get_state()
+        actions = np.random.uniform(low, high, [H, K, A])
+        st_want = np.random.get_state()
+        np.random.set_state(st0)
+        res = eng.get_action_numpy_stream(state, low, high, K)          # back to back: the job is in flight
+        st = np.random.get_state()
+        assert np.array_equal(st[1], st_want[1]) and st[2] == st_want[2], f"call {i}: stream position"
+        if expect == "late":
+            np.random.set_state(st0)
+            ref = eng.get_action(state, np.ascontiguousarray(actions), return_costs=True)
+            np.random.set_state(st_want)
+            assert res.best_index == ref.best_index and np.array_equal(res.first_action, ref.first_action), f"call {i}"
+        else:
+            costs, _ = orc.rollout(orc.NumpyDynamics(w, norm), state, actions)
+            srt = np.sort(costs)
+            assert costs[res.best_index] <= srt[0] + 2e-4, f"call {i}: not a near-optimal row"
+            assert np.array_equal(res.first_action, actions[0, res.best_index])
+        state = state + 0.01
+    stats = eng.predraw_stats()
+    print(f"[late predraw] delay {delay_us} us: {stats}, team reruns {eng.team_reruns}")
+    if expect == "late":
+        assert stats["late"] >= calls - 2
+    else:
+        assert stats["late"] >= 1 and eng.team_reruns >= 1
+    eng.close()
