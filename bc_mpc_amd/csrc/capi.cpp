@@ -263,6 +263,23 @@ struct bcmpc_engine {
     MtChunk* d_mt_chunks = nullptr;
     uint32_t* d_mt_part = nullptr;      // [Cj][S][624]
     uint32_t* h_mt_io = nullptr;        // pinned mirror of d_mt_io (+ bounds at word 1280)
+    // speculative device draw (BCMPC_MT_SPECULATE, default on): right behind a device-path call's argmin, the
+    // NEXT call's draw is enqueued from this draw's final state -- still on the device, no host round trip --
+    // into a slot of its own; the next call uses it when NumPy's state, bounds and shard equal its start
+    // (else it is discarded: two misses in a row pause speculation for kSpecPause calls)
+    struct Spec {
+        uint32_t* d_io = nullptr;       // [0, 625) final key + pos, then [2][A] bounds (f64) from word 640
+        uint32_t* h_io = nullptr;       // pinned mirror
+        double* d_act = nullptr;        // the shard's [H][K][A] rows
+    } spec[2];
+    size_t spec_cap = 0;
+    bool spec_armed = false;
+    int spec_slot = 0, spec_miss_run = 0, spec_pause = 0;
+    uint32_t spec_key[624];
+    int32_t spec_pos = 0;
+    int64_t spec_kg = 0, spec_off = 0;
+    double spec_low[BCMPC_MAX_ACTION], spec_high[BCMPC_MAX_ACTION];
+    uint64_t spec_hits = 0, spec_misses = 0;
     bcmpc_comm* comm = nullptr;         // attached communicator: results exchanged after every argmin
     // team kernel: a team that could not meet (its workgroups not all resident: another process or
     // kernel holding CUs for ~1 s) makes a synchronous call rerun on this fallback engine -- the same
@@ -628,6 +645,11 @@ int bcmpc_destroy(bcmpc_engine* e) {
     }
     if (e->copy_st) (void)hipStreamDestroy(e->copy_st);
     if (e->h_mt_io) (void)hipHostFree(e->h_mt_io);
+    for (auto& sp : e->spec) {
+        if (sp.d_io) (void)hipFree(sp.d_io);
+        if (sp.h_io) (void)hipHostFree(sp.h_io);
+        if (sp.d_act) (void)hipFree(sp.d_act);
+    }
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -637,11 +659,13 @@ int bcmpc_destroy(bcmpc_engine* e) {
 
 uint64_t bcmpc_weights_version(const bcmpc_engine* e) { return e ? e->version : 0; }
 
-int bcmpc_predraw_stats(const bcmpc_engine* e, uint64_t* out3) {
-    if (!e || !out3) return fail(BCMPC_ERR_ARG, "null argument");
-    out3[0] = e->pre.hits;
-    out3[1] = e->pre.late;
-    out3[2] = e->pre.misses;
+int bcmpc_predraw_stats(const bcmpc_engine* e, uint64_t* out5) {
+    if (!e || !out5) return fail(BCMPC_ERR_ARG, "null argument");
+    out5[0] = e->pre.hits;
+    out5[1] = e->pre.late;
+    out5[2] = e->pre.misses;
+    out5[3] = e->spec_hits;
+    out5[4] = e->spec_misses;
     return BCMPC_OK;
 }
 
@@ -1685,6 +1709,7 @@ static bool mt_device_path() {
 // the draw's last word also leaves NumPy's final state, else one extra chunk draws that word alone.
 static int mt_plan(bcmpc_engine* e, int64_t kg, int64_t off) {
     if (e->mt_kg == kg && e->mt_off == off) return BCMPC_OK;
+    HIP_TRY(hipStreamSynchronize(e->stream));         // (a queued speculative draw may still read the old plan)
     const int64_t K = e->cfg.num_paths, A = e->cfg.action_dim, H = e->cfg.horizon;
     const int64_t N = 2 * A * H * kg;
     struct Run { int64_t s, len, out0; };
@@ -1788,6 +1813,55 @@ static int mt_draw_enqueue(bcmpc_engine* e, const uint32_t* mt_key, int32_t pos,
     HIP_TRY(launch_mt_draw(a, e->stream));
     HIP_TRY(hipMemcpyAsync(e->h_mt_io + 640, e->d_mt_io + 640, (kMtN + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                            e->stream));
+    return BCMPC_OK;
+}
+
+static bool mt_speculate() {
+    static const bool on = [] {
+        const char* v = std::getenv("BCMPC_MT_SPECULATE");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+constexpr int kSpecPause = 32;
+
+// enqueue the speculative draw of the next call's rows into spec slot `slot`: from the device-resident
+// final state `in` of the draw just enqueued, same bounds and shard (mt_plan is the current one)
+static int mt_spec_enqueue(bcmpc_engine* e, const uint32_t* in, int slot, const double* low, const double* high) {
+    const bcmpc_config& c = e->cfg;
+    const int A = c.action_dim;
+    const size_t n = (size_t)c.horizon * (size_t)c.num_paths * (size_t)A;
+    if (n > e->spec_cap) {
+        for (auto& sp : e->spec) {
+            if (sp.d_act) (void)hipFree(sp.d_act);
+            sp.d_act = nullptr;
+        }
+        e->spec_cap = 0;
+        for (auto& sp : e->spec) HIP_TRY(hipMalloc(&sp.d_act, n * sizeof(double)));
+        e->spec_cap = n;
+    }
+    auto& sp = e->spec[slot];
+    const size_t io_bytes = 640 * sizeof(uint32_t) + 2 * BCMPC_MAX_ACTION * sizeof(double);
+    if (!sp.d_io) {
+        HIP_TRY(hipMalloc(&sp.d_io, io_bytes));
+        HIP_TRY(hipHostMalloc(&sp.h_io, io_bytes, hipHostMallocDefault));
+    }
+    // (the slot's staging is rewritten two calls later at the earliest: its copy has run by then)
+    double* hb = reinterpret_cast<double*>(sp.h_io + 640);
+    for (int j = 0; j < A; ++j) { hb[j] = low[j]; hb[A + j] = high[j]; }
+    HIP_TRY(hipMemcpyAsync(sp.d_io + 640, hb, 2 * A * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    MtDrawArgs a{};
+    a.in = in;
+    a.bounds = reinterpret_cast<const double*>(sp.d_io + 640);
+    a.xs = e->d_mt_xs;
+    a.polys = e->d_mt_polys;
+    a.chunks = e->d_mt_chunks;
+    a.part = e->d_mt_part;
+    a.final_state = sp.d_io;
+    a.out = sp.d_act;
+    a.nchunks = e->mt_nchunks; a.Cj = e->mt_cj; a.S = e->mt_s; a.A = A;
+    HIP_TRY(launch_mt_draw(a, e->stream));
+    HIP_TRY(hipMemcpyAsync(sp.h_io, sp.d_io, (kMtN + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     return BCMPC_OK;
 }
 
@@ -1944,15 +2018,52 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         const bool lean = e->comm == nullptr;         // (as bcmpc_get_action)
         if (!lean)
             HIP_TRY(hipMemcpyAsync(e->d_state, state, sizeof(double) * c.state_dim, hipMemcpyHostToDevice, e->stream));
-        int rc = mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
+        const int A = c.action_dim;
+        // the previous call's speculative draw, when it starts exactly where NumPy's stream is
+        const bool shit = e->spec_armed && e->spec_kg == k_global && e->spec_off == cand_offset &&
+                          e->spec_pos == *mt_pos && std::memcmp(e->spec_key, mt_key, sizeof(e->spec_key)) == 0 &&
+                          std::memcmp(e->spec_low, low, sizeof(double) * A) == 0 &&
+                          std::memcmp(e->spec_high, high, sizeof(double) * A) == 0;
+        if (e->spec_armed) {
+            if (shit) {
+                ++e->spec_hits;
+                e->spec_miss_run = 0;
+            } else {
+                ++e->spec_misses;
+                if (++e->spec_miss_run >= 2) {
+                    e->spec_pause = kSpecPause;
+                    e->spec_miss_run = 0;
+                }
+            }
+        }
+        e->spec_armed = false;
+        const int cur = e->spec_slot;
+        int rc = shit ? BCMPC_OK : mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
         // (the final-state copy was enqueued before the rollout: the argmin's done word implies it)
+        const uint32_t* fin_d = shit ? e->spec[cur].d_io : e->d_mt_io + 640;
+        const uint32_t* fin_h = shit ? e->spec[cur].h_io : e->h_mt_io + 640;
         e->want_done = lean && !costs_out;
         if (rc == BCMPC_OK)
-            rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, e->d_actions, seed, cand_offset, e->d_costs, nullptr,
+            rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, shit ? e->spec[cur].d_act : e->d_actions, seed,
+                              cand_offset, e->d_costs, nullptr,
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
         const bool spin = e->want_done && rc == BCMPC_OK;
         e->want_done = false;
+        // the next call's draw, behind this call's argmin (a spinning call returns at the done word, so the
+        // draw runs while the caller steps its env); not when the call synchronises the stream
+        int nslot = -1;
+        if (spin && mt_speculate()) {
+            if (e->spec_pause > 0) {
+                --e->spec_pause;
+            } else {
+                nslot = shit ? cur ^ 1 : 0;
+                // (a hit skipped mt_plan: another shard / size drawn in between may have replaced the plan)
+                if (mt_plan(e, k_global, cand_offset) != BCMPC_OK ||
+                    mt_spec_enqueue(e, fin_d, nslot, low, high) != BCMPC_OK)
+                    nslot = -1;
+            }
+        }
         if (rc == BCMPC_OK && !lean &&
             hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             rc = fail(BCMPC_ERR_HIP, "result copy failed");
@@ -1971,9 +2082,19 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
                                             out, costs_out);
         }
-        std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
-        *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];
+        std::memcpy(mt_key, fin_h, kMtN * sizeof(uint32_t));
+        *mt_pos = (int32_t)fin_h[kMtN];
         *out = lean ? *e->h_result_map : *e->h_result;
+        if (nslot >= 0) {                             // armed: it starts where this call leaves NumPy
+            e->spec_armed = true;
+            e->spec_slot = nslot;
+            std::memcpy(e->spec_key, mt_key, sizeof(e->spec_key));
+            e->spec_pos = *mt_pos;
+            e->spec_kg = k_global;
+            e->spec_off = cand_offset;
+            std::memcpy(e->spec_low, low, sizeof(double) * A);
+            std::memcpy(e->spec_high, high, sizeof(double) * A);
+        }
         return BCMPC_OK;
     }
     const int64_t K = c.num_paths;

@@ -295,10 +295,12 @@ class RolloutEngine:
         return int(self._lib.bcmpc_weights_version(self._h))
 
     def predraw_stats(self) -> dict:
-        """The NumPy-stream pre-draw's counters (bcmpc_predraw_stats): hits (incl. late), late, misses."""
-        out = (ctypes.c_uint64 * 3)()
+        """The NumPy-stream draw's counters (bcmpc_predraw_stats): the small draws' host pre-draw (hits incl.
+        late, late, misses) and the large draws' speculative device draw (spec_hits, spec_misses)."""
+        out = (ctypes.c_uint64 * 5)()
         _lib.check(self._lib.bcmpc_predraw_stats(self._h, out))
-        return {"hits": int(out[0]), "late": int(out[1]), "misses": int(out[2])}
+        return {"hits": int(out[0]), "late": int(out[1]), "misses": int(out[2]), "spec_hits": int(out[3]),
+                "spec_misses": int(out[4])}
 
     def set_action_bounds(self, low, high) -> None:
         lo, hi = _f64(low), _f64(high)

@@ -251,8 +251,12 @@ int bcmpc_get_action_mt19937(bcmpc_engine* eng, const double* state, uint32_t* m
  * state; a call whose (key, pos, bounds, shard) equal that job's start uses them -- a hit (rows
  * complete, copied into HBM when the copy has landed) or, on team-kernel engines, a late hit (the job
  * still running: the kernel waits for the rows' sequence word in mapped memory) -- else it draws itself
- * (a miss).  out3 = {hits incl. late, late hits, misses} since bcmpc_create. */
-int bcmpc_predraw_stats(const bcmpc_engine* eng, uint64_t* out3);
+ * (a miss).  Larger draws (the device path): right behind a synchronous call's argmin the NEXT call's
+ * draw is enqueued on the device from this draw's final state (BCMPC_MT_SPECULATE=0: off), used by the
+ * next call when NumPy's state, bounds and shard equal its start (two misses in a row pause it for 32
+ * calls).  out5 = {hits incl. late, late hits, misses, speculative hits, speculative misses} since
+ * bcmpc_create. */
+int bcmpc_predraw_stats(const bcmpc_engine* eng, uint64_t* out5);
 
 /* The same draw as bcmpc_get_action_mt19937 on the device, alone: this engine's shard
  * [H, K, A] of np.random.uniform(low, high, [H, k_global, A]) (controllers.py:53) drawn on the GPU

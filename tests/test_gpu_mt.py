@@ -291,3 +291,59 @@ def test_late_predraw_hit_waits_for_the_rows(delay_us, expect, monkeypatch):
     else:
         assert stats["late"] >= 1 and eng.team_reruns >= 1
     eng.close()
+
+
+@pytest.mark.parametrize("hidden,L,act,ln,K,H", [(500, 2, "tanh", False, 1000, 15),     # cfg1: team kernel
+                                                 (500, 2, "tanh", False, 8192, 10),     # split slab kernel
+                                                 (256, 2, "relu", True, 2000, 12)])
+def test_speculative_device_draw(hidden, L, act, ln, K, H, monkeypatch):
+    """Device-path draws (> 2^16 words): each synchronous call enqueues the NEXT call's draw on the device
+    from its own final state, right behind its argmin.  A call whose NumPy state is that start uses the rows
+    (a hit); a foreign draw from the global stream in between makes it a miss (fresh draw).  Every call must
+    pick exactly the candidate the same engine picks on np.random.uniform's own array and leave NumPy's stream
+    where that call leaves it (controllers.py:53, :82-85); two misses in a row pause the speculation."""
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    monkeypatch.setenv("BCMPC_MT_SPECULATE", "1")
+    S, A = 20, 6
+    w = orc.synthetic_weights(S, A, hidden, L, act, ln)
+    norm = orc.synthetic_normalization(S, A)
+    state = orc.synthetic_state(norm)
+    low, high = -np.ones(A), np.ones(A)
+    eng = RolloutEngine(S, A, hidden, L, act, ln, H, K, device=0)
+    eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation, w.ln_gamma, w.ln_beta), norm, 1)
+    np.random.seed(11)
+    foreign = {3, 6}
+    for i in range(8):
+        if i in foreign:
+            np.random.random(5)                          # another consumer of the global stream
+        st0 = np.random.get_state()
+        actions = np.random.uniform(low, high, [H, K, A])
+        st_want = np.random.get_state()
+        ref = eng.get_action(state, np.ascontiguousarray(actions))
+        np.random.set_state(st0)
+        res = eng.get_action_numpy_stream(state, low, high, K)
+        st = np.random.get_state()
+        assert np.array_equal(st[1], st_want[1]) and st[2] == st_want[2], f"call {i}: stream position"
+        assert res.best_index == ref.best_index and np.array_equal(res.first_action, ref.first_action), f"call {i}"
+        assert np.array_equal(res.first_action, actions[0, res.best_index])
+        state = state + 0.01
+    s1 = eng.predraw_stats()
+    # misses in a row: the speculation pauses (no further misses counted while paused)
+    for i in range(6):
+        np.random.random(3)
+        st0 = np.random.get_state()
+        actions = np.random.uniform(low, high, [H, K, A])
+        st_want = np.random.get_state()
+        ref = eng.get_action(state, np.ascontiguousarray(actions))
+        np.random.set_state(st0)
+        res = eng.get_action_numpy_stream(state, low, high, K)
+        st = np.random.get_state()
+        assert np.array_equal(st[1], st_want[1]) and st[2] == st_want[2], f"foreign call {i}: stream position"
+        assert res.best_index == ref.best_index, f"foreign call {i}"
+    s2 = eng.predraw_stats()
+    print(f"[speculative draw] {eng.info()['kernel']} K={K} H={H}: after the mixed run {s1}, after the "
+          f"foreign run {s2}")
+    assert s1["spec_hits"] == 5 and s1["spec_misses"] == 2
+    assert s2["spec_misses"] - s1["spec_misses"] == 2 and s2["spec_hits"] == s1["spec_hits"]
+    eng.close()
