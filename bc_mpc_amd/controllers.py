@@ -81,13 +81,6 @@ def _stock_sampler(obj) -> bool:
             and getattr(type(obj).sample_random_actions, "_bcmpc_stock_sampler", False))
 
 
-def _legacy_stream_unverified(eng) -> bool:
-    """True when get_action_numpy_stream may return None (the global generator is not NumPy's verified
-    legacy MT19937): the caller then keeps its own seed stream's state to restore."""
-    from .engine import _legacy_mt_state
-    return _legacy_mt_state() is None
-
-
 def _default_device() -> int:
     if "LOCAL_RANK" in os.environ:
         return int(os.environ["LOCAL_RANK"])
@@ -308,6 +301,31 @@ class MPCcontroller(Controller):
         return np.asarray(trajectory_cost_fn(self.cost_fn, traj[:-1], local_actions, traj[1:]), dtype=np.float64)
 
 
+class _SeedStream:
+    """A controller's per-call Philox seeds: ``RandomState(seed).randint(0, 2**62)``, one per call, drawn 64 at
+    a time (legacy randint fills a batch in call order, so the sequence is the one-at-a-time sequence) -- a call
+    pays a list pop instead of a ~3-us scalar randint.  ``get_state`` / ``set_state`` carry the unread seeds."""
+
+    def __init__(self, seed):
+        self._rs = np.random.RandomState(seed)
+        self._buf = []                          # unread seeds, next last
+
+    def next(self) -> int:
+        if not self._buf:
+            self._buf = self._rs.randint(0, 2**62, size=64, dtype=np.int64).tolist()[::-1]
+        return self._buf.pop()
+
+    def unread(self, seed: int) -> None:
+        self._buf.append(seed)
+
+    def get_state(self):
+        return self._rs.get_state(), tuple(self._buf)
+
+    def set_state(self, state) -> None:
+        self._rs.set_state(state[0])
+        self._buf = list(state[1])
+
+
 class MPCcontrollerPolicyNet(Controller):
     """Policy-guided MPC (controllers.py:160-237) on the MI355X rollout engine.
 
@@ -348,7 +366,7 @@ class MPCcontrollerPolicyNet(Controller):
         self.num_simulated_paths = num_simulated_paths
         self.self_exp = self_exp
         self.explore = explore
-        self._seed_rng = np.random.RandomState(0x5EEDF00D if seed is None else seed)
+        self._seed_rng = _SeedStream(0x5EEDF00D if seed is None else seed)
         self._device = device
         self._group = process_group
         self._engine = None
@@ -404,7 +422,7 @@ class MPCcontrollerPolicyNet(Controller):
                     and _policy.int_version(self.policy_net) == fp[2] and "sample_random_actions" not in self.__dict__
                     and _dist.world(self._group)[1] == 1 and _legacy_mt_state() is not None):
                 space = self.env.action_space
-                seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+                seed = self._seed_rng.next()
                 res = fp[3].get_action_numpy_stream(state, space.low, space.high, fp[4], 0, seed=seed)
                 if res is not None:
                     self.last_costs = None
@@ -432,12 +450,11 @@ class MPCcontrollerPolicyNet(Controller):
             eng = self._engine_for(spec, pspec, S, A, hi - lo)
             eng.set_weights(spec, norm, version)
             eng.set_policy(pspec, float(self.explore), pversion)
-            seed_state = self._seed_rng.get_state() if _legacy_stream_unverified(eng) else None
-            seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+            seed = self._seed_rng.next()
             res = eng.get_action_numpy_stream(state, self.env.action_space.low, self.env.action_space.high, K,
                                               lo, return_costs=self.keep_costs, seed=seed)
-            if res is None and seed_state is not None:
-                self._seed_rng.set_state(seed_state)         # (nothing drawn: the host path draws the seed)
+            if res is None:
+                self._seed_rng.unread(seed)                  # (nothing drawn: the host path draws the seed)
             if res is not None:
                 self.last_costs = res.costs
                 cost, index, first_g = _minloc(self, eng, True, sign * res.best_cost, res.best_index,
@@ -448,7 +465,7 @@ class MPCcontrollerPolicyNet(Controller):
                     self._fast = (self._fast_key(), tok, pv, eng, K)
                 return first_g
         exploration = self.sample_random_actions()           # every rank draws the full [H, K, A]
-        seed = int(self._seed_rng.randint(0, 2**62, dtype=np.int64))
+        seed = self._seed_rng.next()
         if K == 0:
             raise ValueError(f"attempt to get {'argmax' if reward else 'argmin'} of an empty sequence")
         valid, cost, index, first = False, float("inf"), -1, None

@@ -218,3 +218,26 @@ def test_replaced_normalisation_changes_the_engine_version():
     t2 = ww.weight_token(m)
     m.version = 4
     assert not ww.same_token(m, t2) and ww.same_token(m, ww.weight_token(m))
+
+
+def test_seed_stream_is_the_one_at_a_time_sequence():
+    """The policy controllers' per-call Philox seeds (_SeedStream, drawn 64 at a time) are exactly
+    RandomState(seed).randint(0, 2**62) called once per get_action; unread() puts a seed back, and
+    get_state / set_state carry the unread seeds."""
+    from bc_mpc_amd.controllers import _SeedStream
+    ref = np.random.RandomState(0x5EEDF00D)
+    want = [int(ref.randint(0, 2**62, dtype=np.int64)) for _ in range(150)]
+    s = _SeedStream(0x5EEDF00D)
+    got = []
+    for i in range(150):
+        v = s.next()
+        if i % 7 == 3:                      # a call that drew nothing: the host path takes the same seed
+            s.unread(v)
+            v = s.next()
+        got.append(v)
+        if i == 70:
+            st = s.get_state()
+    assert got == want
+    t = _SeedStream(1)
+    t.set_state(st)
+    assert [t.next() for _ in range(79)] == want[71:]
