@@ -280,6 +280,14 @@ struct bcmpc_engine {
     int64_t spec_kg = 0, spec_off = 0;
     double spec_low[BCMPC_MAX_ACTION], spec_high[BCMPC_MAX_ACTION];
     uint64_t spec_hits = 0, spec_misses = 0;
+    // slab-kernel engines draw beside the rollout: the speculative draw runs on spec_st, concurrently with
+    // this call's rollout (spec_in_ev: this call's draw has left its final state), with scratch of its own;
+    // spec_done_ev closes it and every later draw / rollout that touches its slots waits for it
+    hipStream_t spec_st = nullptr;
+    hipEvent_t spec_in_ev = nullptr, spec_done_ev = nullptr;
+    bool spec_side_pending = false;
+    uint32_t* d_spec_xs = nullptr;
+    uint32_t* d_spec_part = nullptr;
     bcmpc_comm* comm = nullptr;         // attached communicator: results exchanged after every argmin
     // team kernel: a team that could not meet (its workgroups not all resident: another process or
     // kernel holding CUs for ~1 s) makes a synchronous call rerun on this fallback engine -- the same
@@ -614,6 +622,14 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (!e) return BCMPC_OK;
     if (e->fb) (void)bcmpc_destroy(e->fb);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->spec_st) {
+        (void)hipStreamSynchronize(e->spec_st);
+        (void)hipStreamDestroy(e->spec_st);
+    }
+    for (hipEvent_t ev : {e->spec_in_ev, e->spec_done_ev})
+        if (ev) (void)hipEventDestroy(ev);
+    for (void* p : {(void*)e->d_spec_xs, (void*)e->d_spec_part})
+        if (p) (void)hipFree(p);
     for (void* p : {(void*)e->d_w, (void*)e->d_b, (void*)e->d_ln, (void*)e->d_consts, (void*)e->d_state,
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
                     (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
@@ -1710,6 +1726,9 @@ static bool mt_device_path() {
 static int mt_plan(bcmpc_engine* e, int64_t kg, int64_t off) {
     if (e->mt_kg == kg && e->mt_off == off) return BCMPC_OK;
     HIP_TRY(hipStreamSynchronize(e->stream));         // (a queued speculative draw may still read the old plan)
+    if (e->spec_st) HIP_TRY(hipStreamSynchronize(e->spec_st));
+    if (e->d_spec_part) (void)hipFree(e->d_spec_part);
+    e->d_spec_part = nullptr;
     const int64_t K = e->cfg.num_paths, A = e->cfg.action_dim, H = e->cfg.horizon;
     const int64_t N = 2 * A * H * kg;
     struct Run { int64_t s, len, out0; };
@@ -1763,6 +1782,7 @@ static int mt_plan(bcmpc_engine* e, int64_t kg, int64_t off) {
     HIP_TRY(hipMalloc(&e->d_mt_polys, polys.size() * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&e->d_mt_chunks, ch.size() * sizeof(MtChunk)));
     HIP_TRY(hipMalloc(&e->d_mt_part, (size_t)std::max(1, cj) * S * kMtN * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&e->d_spec_part, (size_t)std::max(1, cj) * S * kMtN * sizeof(uint32_t)));
     HIP_TRY(hipMemcpy(e->d_mt_polys, polys.data(), polys.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_mt_chunks, ch.data(), ch.size() * sizeof(MtChunk), hipMemcpyHostToDevice));
     e->mt_nchunks = (int32_t)ch.size();
@@ -1825,9 +1845,19 @@ static bool mt_speculate() {
 }
 constexpr int kSpecPause = 32;
 
+// the main stream waits for a speculative draw still running beside it (its slots, its input -- the final
+// state of the draw before it -- and the MT scratch are read or rewritten by what follows)
+static int spec_join(bcmpc_engine* e) {
+    if (!e->spec_side_pending) return BCMPC_OK;
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->spec_done_ev, 0));
+    e->spec_side_pending = false;
+    return BCMPC_OK;
+}
+
 // enqueue the speculative draw of the next call's rows into spec slot `slot`: from the device-resident
 // final state `in` of the draw just enqueued, same bounds and shard (mt_plan is the current one)
-static int mt_spec_enqueue(bcmpc_engine* e, const uint32_t* in, int slot, const double* low, const double* high) {
+static int mt_spec_enqueue(bcmpc_engine* e, const uint32_t* in, int slot, const double* low, const double* high,
+                           bool side) {
     const bcmpc_config& c = e->cfg;
     const int A = c.action_dim;
     const size_t n = (size_t)c.horizon * (size_t)c.num_paths * (size_t)A;
@@ -1846,22 +1876,38 @@ static int mt_spec_enqueue(bcmpc_engine* e, const uint32_t* in, int slot, const 
         HIP_TRY(hipMalloc(&sp.d_io, io_bytes));
         HIP_TRY(hipHostMalloc(&sp.h_io, io_bytes, hipHostMallocDefault));
     }
+    hipStream_t st = e->stream;
+    if (side) {                                   // beside this call's rollout, after its draw
+        if (!e->spec_st) {
+            HIP_TRY(hipStreamCreateWithFlags(&e->spec_st, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&e->spec_in_ev, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&e->spec_done_ev, hipEventDisableTiming));
+        }
+        if (!e->d_spec_xs) HIP_TRY(hipMalloc(&e->d_spec_xs, (size_t)kMtStream * sizeof(uint32_t)));
+        HIP_TRY(hipEventRecord(e->spec_in_ev, e->stream));
+        HIP_TRY(hipStreamWaitEvent(e->spec_st, e->spec_in_ev, 0));
+        st = e->spec_st;
+    }
     // (the slot's staging is rewritten two calls later at the earliest: its copy has run by then)
     double* hb = reinterpret_cast<double*>(sp.h_io + 640);
     for (int j = 0; j < A; ++j) { hb[j] = low[j]; hb[A + j] = high[j]; }
-    HIP_TRY(hipMemcpyAsync(sp.d_io + 640, hb, 2 * A * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(sp.d_io + 640, hb, 2 * A * sizeof(double), hipMemcpyHostToDevice, st));
     MtDrawArgs a{};
     a.in = in;
     a.bounds = reinterpret_cast<const double*>(sp.d_io + 640);
-    a.xs = e->d_mt_xs;
+    a.xs = side ? e->d_spec_xs : e->d_mt_xs;
     a.polys = e->d_mt_polys;
     a.chunks = e->d_mt_chunks;
-    a.part = e->d_mt_part;
+    a.part = side ? e->d_spec_part : e->d_mt_part;
     a.final_state = sp.d_io;
     a.out = sp.d_act;
     a.nchunks = e->mt_nchunks; a.Cj = e->mt_cj; a.S = e->mt_s; a.A = A;
-    HIP_TRY(launch_mt_draw(a, e->stream));
-    HIP_TRY(hipMemcpyAsync(sp.h_io, sp.d_io, (kMtN + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(launch_mt_draw(a, st));
+    HIP_TRY(hipMemcpyAsync(sp.h_io, sp.d_io, (kMtN + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (side) {
+        HIP_TRY(hipEventRecord(e->spec_done_ev, st));
+        e->spec_side_pending = true;
+    }
     return BCMPC_OK;
 }
 
@@ -2038,11 +2084,26 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         }
         e->spec_armed = false;
         const int cur = e->spec_slot;
+        if (const int jr = spec_join(e)) return jr;
         int rc = shit ? BCMPC_OK : mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
         // (the final-state copy was enqueued before the rollout: the argmin's done word implies it)
         const uint32_t* fin_d = shit ? e->spec[cur].d_io : e->d_mt_io + 640;
         const uint32_t* fin_h = shit ? e->spec[cur].h_io : e->h_mt_io + 640;
         e->want_done = lean && !costs_out;
+        // the next call's draw: slab-kernel engines draw it beside this rollout (on spec_st, from this draw's
+        // final state); team engines behind the argmin (the team's grid needs every CU it was given)
+        int nslot = -1;
+        const bool speculate = rc == BCMPC_OK && e->want_done && mt_speculate();
+        const bool side = e->kernel != BCMPC_KERNEL_TEAM;
+        bool paused = false;
+        if (speculate && e->spec_pause > 0) {
+            --e->spec_pause;
+            paused = true;
+        } else if (speculate && side) {
+            nslot = shit ? cur ^ 1 : 0;
+            if (mt_plan(e, k_global, cand_offset) != BCMPC_OK || mt_spec_enqueue(e, fin_d, nslot, low, high, true) != BCMPC_OK)
+                nslot = -1;
+        }
         if (rc == BCMPC_OK)
             rc = rollout_impl(e, lean ? nullptr : e->d_state, 0, shit ? e->spec[cur].d_act : e->d_actions, seed,
                               cand_offset, e->d_costs, nullptr,
@@ -2050,20 +2111,16 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
                               lean ? state : nullptr);
         const bool spin = e->want_done && rc == BCMPC_OK;
         e->want_done = false;
-        // the next call's draw, behind this call's argmin (a spinning call returns at the done word, so the
-        // draw runs while the caller steps its env); not when the call synchronises the stream
-        int nslot = -1;
-        if (spin && mt_speculate()) {
-            if (e->spec_pause > 0) {
-                --e->spec_pause;
-            } else {
-                nslot = shit ? cur ^ 1 : 0;
-                // (a hit skipped mt_plan: another shard / size drawn in between may have replaced the plan)
-                if (mt_plan(e, k_global, cand_offset) != BCMPC_OK ||
-                    mt_spec_enqueue(e, fin_d, nslot, low, high) != BCMPC_OK)
-                    nslot = -1;
-            }
+        // team engines: the next call's draw behind this call's argmin (a spinning call returns at the done
+        // word, so the draw runs while the caller steps its env); not when the call synchronises the stream
+        // (a hit skipped mt_plan: another shard / size drawn in between may have replaced the plan)
+        if (spin && speculate && !side && !paused) {
+            nslot = shit ? cur ^ 1 : 0;
+            if (mt_plan(e, k_global, cand_offset) != BCMPC_OK ||
+                mt_spec_enqueue(e, fin_d, nslot, low, high, false) != BCMPC_OK)
+                nslot = -1;
         }
+        if (!spin) nslot = -1;
         if (rc == BCMPC_OK && !lean &&
             hipMemcpyAsync(e->h_result, e->d_result, sizeof(bcmpc_result), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             rc = fail(BCMPC_ERR_HIP, "result copy failed");
@@ -2181,6 +2238,7 @@ int bcmpc_mt19937_uniform_device(bcmpc_engine* e, uint32_t* mt_key, int32_t* mt_
         return fail(BCMPC_ERR_ARG, "this engine's candidates must lie inside [0, k_global)");
     if (*mt_pos < 0 || *mt_pos > 624) return fail(BCMPC_ERR_ARG, "MT19937 position out of range");
     HIP_TRY(hipSetDevice(c.device));
+    if (const int jr = spec_join(e)) return jr;
     int rc = mt_draw_enqueue(e, mt_key, *mt_pos, low, high, k_global, cand_offset);
     const size_t n = (size_t)c.horizon * c.num_paths * c.action_dim;
     if (rc == BCMPC_OK &&
