@@ -286,6 +286,7 @@ struct bcmpc_engine {
     hipStream_t spec_st = nullptr;
     hipEvent_t spec_in_ev = nullptr, spec_done_ev = nullptr;
     bool spec_side_pending = false;
+    int ncu = 0;                        // the device's CUs
     uint32_t* d_spec_xs = nullptr;
     uint32_t* d_spec_part = nullptr;
     bcmpc_comm* comm = nullptr;         // attached communicator: results exchanged after every argmin
@@ -424,6 +425,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     // for each other).  Auto: whenever it fits, unless BCMPC_TEAM=0
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device);
+    e->ncu = ncu;
     const int tkind = reward ? 2 : e->PL > 0 ? 1 : 0;
     const int tmem = team_members(e->HP, tkind);
     // (a LayerNorm over a layer split across members: only the reward net's heads, whose statistics
@@ -2090,11 +2092,13 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         const uint32_t* fin_d = shit ? e->spec[cur].d_io : e->d_mt_io + 640;
         const uint32_t* fin_h = shit ? e->spec[cur].h_io : e->h_mt_io + 640;
         e->want_done = lean && !costs_out;
-        // the next call's draw: slab-kernel engines draw it beside this rollout (on spec_st, from this draw's
-        // final state); team engines behind the argmin (the team's grid needs every CU it was given)
+        // the next call's draw: slab-kernel engines whose grid leaves CUs free (K <= 32 per CU: cfg2's 4096)
+        // draw it beside this rollout (on spec_st, from this draw's final state); the others behind the argmin
+        // -- a team's grid needs every CU it was given, and at cfg3 (1024 workgroups) a draw beside the
+        // rollout delays it by more than it hides (profiles/r03_spec2_ab.txt)
         int nslot = -1;
         const bool speculate = rc == BCMPC_OK && e->want_done && mt_speculate();
-        const bool side = e->kernel != BCMPC_KERNEL_TEAM;
+        const bool side = e->kernel != BCMPC_KERNEL_TEAM && e->ncu > 0 && c.num_paths <= 32 * (int64_t)e->ncu;
         bool paused = false;
         if (speculate && e->spec_pause > 0) {
             --e->spec_pause;
