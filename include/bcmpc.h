@@ -251,8 +251,9 @@ int bcmpc_get_action_mt19937(bcmpc_engine* eng, const double* state, uint32_t* m
  * state; a call whose (key, pos, bounds, shard) equal that job's start uses them -- a hit (rows
  * complete, copied into HBM when the copy has landed) or, on team-kernel engines, a late hit (the job
  * still running: the kernel waits for the rows' sequence word in mapped memory) -- else it draws itself
- * (a miss).  Larger draws (the device path): right behind a synchronous call's argmin the NEXT call's
- * draw is enqueued on the device from this draw's final state (BCMPC_MT_SPECULATE=0: off), used by the
+ * (a miss).  Larger draws (the device path): the NEXT call's draw is enqueued on the device from this
+ * draw's final state -- behind a synchronous call's argmin, or beside its rollout on a stream of its own
+ * when the slab grid leaves CUs free (K <= 32 per CU) -- (BCMPC_MT_SPECULATE=0: off), used by the
  * next call when NumPy's state, bounds and shard equal its start (two misses in a row pause it for 32
  * calls).  out5 = {hits incl. late, late hits, misses, speculative hits, speculative misses} since
  * bcmpc_create. */
