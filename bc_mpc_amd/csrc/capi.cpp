@@ -473,13 +473,40 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                    x3_lds(e->HP, reward ? 3 : c.n_layers, n, c.action_dim, e->PL, e->PHP,
                           (c.activation == BCMPC_ACT_RELU ? 1 : 0) | (c.layer_norm ? 2 : 0)) <= 160 * 1024;
         };
-        if (nc == 0) {
+        int nw = nwx;
+        if (f16) {
+            // single-pass f16: the hi-only slab admits wider groups (x3_f16_layout_ok); BCMPC_F16_NC /
+            // BCMPC_F16_NW pick a layout for A/B runs
+            auto f16_fits = [&](int n, int w) {
+                return x3_f16_layout_ok(e->HP, n, w) &&
+                       x3_f16_lds(e->HP, c.n_layers, n, w, c.action_dim) <= 160 * 1024;
+            };
+            const char* en = std::getenv("BCMPC_F16_NC");
+            const char* ew = std::getenv("BCMPC_F16_NW");
+            if (en && *en) nc = std::atoi(en);
+            if (ew && *ew) nw = std::atoi(ew);
+            if (nc == 0 && !(ew && *ew) && e->HP == 512 && cols >= 4 * 512 && f16_fits(4, 4)) {
+                // two 64-candidate 4-wave groups per CU: 0.90 ms at cfg3 against 0.94 (one 8-wave group of
+                // 64) and 0.91 (one of 128), three boxes (profiles/r04_f16_layouts_ab.txt)
+                nc = 4;
+                nw = 4;
+            }
+            if (nc == 0) {
+                nc = 1;
+                for (int n : {8, 4, 2})
+                    if (f16_fits(n, nw) && cols >= (int64_t)n * 256 && !(n >= 4 && e->HP <= 256)) { nc = n; break; }
+            }
+            if (!f16_fits(nc, nw)) {
+                delete e;
+                return fail(BCMPC_ERR_UNSUPPORTED, "F16 precision: no single-pass layout for this shape / NC / NW");
+            }
+        } else if (nc == 0) {
             nc = 1;
             // (hidden <= 256: 32-candidate groups, two or three workgroups per CU, measured 6-18% ahead of 64)
             for (int n : {4, 2})
                 if (fits(n) && cols >= (int64_t)n * 256 && !(n == 4 && e->HP <= 256)) { nc = n; break; }
         }
-        if (!fits(nc)) {
+        if (!f16 && !fits(nc)) {
             delete e;
             return fail(BCMPC_ERR_UNSUPPORTED, e->PL ? "split kernel with a fused policy needs dynamics hidden 449..1024"
                                                      : "split kernel does not fit this shape");
@@ -487,7 +514,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->split = true;
         e->nc = nc;
         e->kernel = nc == 1 ? BCMPC_KERNEL_SPLIT1 : nc == 2 ? BCMPC_KERNEL_SPLIT2 : BCMPC_KERNEL_SPLIT4;
-        e->nw = nwx;
+        e->nw = nw;
         kern = e->kernel;
     }
     if (split_needs_team && !use_team) {
@@ -1220,6 +1247,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         }
     }
     a.f16_single = e->f16 ? 1 : 0;
+    a.x3_nw = e->nw;
     a.consts = e->d_consts;
     a.state = d_state; a.state_stride = stride;
     if (state_inline) {                       // the tiled state by value in the kernel arguments
@@ -1388,7 +1416,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         static uint64_t* d_st = nullptr;
         static size_t st_n = 0;
         const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
-        const int nw = x3_waves(e->HP);
+        const int nw = e->nw;
         const size_t blocks = (size_t)((c.num_paths + 16 * e->nc - 1) / (16 * e->nc));
         if (stamps) {
             if (st_n < blocks * nw * 10) {
@@ -1399,19 +1427,20 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             HIP_TRY(hipMemsetAsync(d_st, 0, st_n * sizeof(uint64_t), st));
             a.stamps = d_st;
         }
-        HIP_TRY(launch_rollout_x3(a, e->HP, e->nc, st));
+        HIP_TRY(e->f16 ? launch_rollout_x3_f16(a, e->HP, e->nc, st) : launch_rollout_x3(a, e->HP, e->nc, st));
         if (stamps) {
             std::vector<uint64_t> h(blocks * nw * 10);
             HIP_TRY(hipMemcpyAsync(h.data(), d_st, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             const char* names[10] = {"owner", "input", "B1", "layer0", "slab", "mm", "epi", "out", "B3B4", "-"};
+            // (waves 0..nw/2-1, the older half that wins the MFMA / VALU arbitration, vs the younger half)
             for (int grp = 0; grp < 2; ++grp) {
-                std::fprintf(stderr, "x3 stamps %s:", grp == 0 ? "owners " : "others ");
+                std::fprintf(stderr, "x3 stamps %s:", grp == 0 ? "waves<nw/2 " : "waves>=nw/2");
                 for (int k = 0; k < 9; ++k) {
                     double sum = 0; size_t n = 0;
                     for (size_t b = 0; b < blocks; ++b)
                         for (int w = 0; w < nw; ++w)
-                            if ((w < e->nc) == (grp == 0)) { sum += (double)h[(b * nw + w) * 10 + k]; ++n; }
+                            if ((2 * w < nw) == (grp == 0)) { sum += (double)h[(b * nw + w) * 10 + k]; ++n; }
                     std::fprintf(stderr, " %s=%.0f", names[k], n ? sum / n / c.horizon : 0.0);
                 }
                 std::fprintf(stderr, "  (per step, s_memtime ticks)\n");

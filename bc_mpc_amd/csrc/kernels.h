@@ -82,6 +82,7 @@ struct RolloutArgs {
     float pwinv[BCMPC_MAX_LAYERS + 1];       // the same for the fused policy's layers
     float hsc[BCMPC_MAX_LAYERS];             // split LN nets: power-of-two scale of hidden layer l's output
     int32_t f16_single;                      // BCMPC_PREC_F16: one f16 MFMA pass (hi x hi), no lo operands
+    int32_t x3_nw;                           // split kernel: waves per workgroup (0: x3_waves' default)
     uint64_t* stamps;                        // diagnostics (X3_STAMP builds): [blocks][NW][10] phase cycles
     // split kernel: np.argmin fused into the launch's tail (fused_argmin != 0): every workgroup
     // leaves its best (cost, index) in amin.scratch_c/i[blockIdx.x], the last to finish (ticket)
@@ -177,7 +178,11 @@ int x3_max_nc(int hidden_padded);
 size_t x3_lds(int hidden_padded, int n_layers, int nc, int action_dim, int policy_layers, int policy_hidden_padded,
               int ak = 0);
 bool x3_policy_ok(int hidden_padded, int nc);
+// single-pass f16 layouts (BCMPC_PREC_F16): the (nc, nw) pairs this build instantiates, and their LDS
+bool x3_f16_layout_ok(int hidden_padded, int nc, int nw);
+size_t x3_f16_lds(int hidden_padded, int n_layers, int nc, int nw, int action_dim);
 hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
+hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
 size_t rr_image_bytes(int hidden_padded);
 int rr_candidates_per_block();
 hipError_t launch_rollout_rr(const RolloutArgs& a, int hidden_padded, hipStream_t st);

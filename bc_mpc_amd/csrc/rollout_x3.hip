@@ -114,10 +114,10 @@ __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// slab index of (k-step p, column c, part) in f4 units of one lane
-template <int NC>
+// slab index of (k-step p, column c, part) in f4 units of one lane (F1: the hi part only)
+template <int NC, bool F1 = false>
 __device__ __forceinline__ int sidx(int p, int c, int part, int lane) {
-    return ((p * NC + c) * 2 + part) * 64 + lane;
+    return ((p * NC + c) * (F1 ? 1 : 2) + part) * 64 + lane;
 }
 
 // One operand unit: acc[g*G + j][c] += W[tile g*G + j] * X[c] for j < G (the G
@@ -172,8 +172,8 @@ template <int NC, bool F1 = false>
 __device__ __forceinline__ void bread_x3(const f4* slab, int p, int lane, h8 (&bh)[NC], h8 (&bl)[NC]) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        bh[c] = sread(slab + sidx<NC>(p, c, 0, lane));
-        bl[c] = F1 ? bh[c] : sread(slab + sidx<NC>(p, c, 1, lane));
+        bh[c] = sread(slab + sidx<NC, F1>(p, c, 0, lane));
+        bl[c] = F1 ? bh[c] : sread(slab + sidx<NC, F1>(p, c, 1, lane));
     }
 }
 
@@ -462,13 +462,23 @@ __host__ __device__ constexpr int x3_waves_per_eu(int HP, int NC, int NW) {
 
 // LDS carve-up: consts | biases (L*HP + 32) | policy biases + params (PL*PHP + kPolParams) |
 // column factors NC*16 | column max [2][NC*16] | penalty counts [2][NC*16] | action inputs
-// X3_NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab P*NC*2 KiB
-__host__ __device__ constexpr int x3_xa_bytes(int NC, int A) { return (X3_NCH * 16 * NC * A * 4 + 15) & ~15; }
+// NCH*16NC*A (16-B aligned; none with a policy) | layer-0 slab NC*2 KiB | slab P*NC*2 KiB (F1: the hi
+// halves only, NC*1 KiB | P*NC*1 KiB)
+// steps of action inputs staged per fill: X3_NCH, but 2 for the single-pass 4-wave groups (two of them
+// share a CU's 160 KiB)
+__host__ __device__ constexpr int x3_nch(int NW, bool F1) { return (F1 && NW <= 4) ? 2 : X3_NCH; }
+// slab: 1-KiB fragments per candidate column (the layer input's P k-steps x hi | lo; at least the
+// output-layer partials' 2 NW)
+__host__ __device__ constexpr int x3_slab_frags(int HP, int NW, bool F1) {
+    return (HP / 32) * (F1 ? 1 : 2) > 2 * NW ? (HP / 32) * (F1 ? 1 : 2) : 2 * NW;
+}
+__host__ __device__ constexpr int x3_xa_bytes(int NC, int A, int nch = X3_NCH) { return (nch * 16 * NC * A * 4 + 15) & ~15; }
 // | AK != 0: column exchange [NW][NC*16][2] | LN gamma [L][HP], beta [L][HP]
 __host__ __device__ constexpr int x3_lds_bytes_rt(int HP, int NC, int L, int A, int PL = 0, int PHP = 0, int AK = 0,
-                                                  int NW = 8) {
-    return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)) +
-           NC * 2048 + (HP / 32) * NC * 2048 + (AK != 0 ? NW * NC * 16 * 8 : 0) + ((AK & 2) ? 2 * L * HP * 4 : 0);
+                                                  int NW = 8, bool F1 = false) {
+    return param_bytes(L, HP) + pol_param_bytes(PL, PHP) + NC * 16 * 4 * 5 +
+           (PHP > 0 ? 0 : x3_xa_bytes(NC, A, x3_nch(NW, F1))) + NC * (F1 ? 1024 : 2048) +
+           x3_slab_frags(HP, NW, F1) * NC * 1024 + (AK != 0 ? NW * NC * 16 * 8 : 0) + ((AK & 2) ? 2 * L * HP * 4 : 0);
 }
 
 template <int HP, int NC, int NW, int PHP, bool RW, int AK, bool F1 = false>
@@ -490,7 +500,11 @@ void rollout_x3(const RolloutArgs a) {
     constexpr int G = x3_group(TW);     // tiles per streamed operand unit
     static_assert(TW % 2 == 0 && TW * NW == T, "each wave must own whole tile pairs");
     static_assert(NC <= NW, "one owner wave per column");
-    static_assert(P >= NW, "the output-layer partials reuse the slab");
+    constexpr int NPT = F1 ? 1 : 2;     // slab parts per B fragment: hi | lo (F1: hi)
+    constexpr int NCH = x3_nch(NW, F1); // steps of action inputs staged per fill
+    // slab fragments per column: the layer input, or the output-layer partials [NW][2 tiles] that reuse it
+    constexpr int SLABF = x3_slab_frags(HP, NW, F1);
+    static_assert(SLABF >= P * NPT && SLABF >= 2 * NW, "the output-layer partials reuse the slab");
     // fused policy (MPCcontrollerPolicyNet): one policy tile per wave, split ownership
     constexpr int PPn = PHP / 32;                       // policy hidden k-steps
     static_assert(PHP == 0 || (PHP / 16 == NW && 2 * NC <= NW && PPn + NW / 2 <= P),
@@ -536,10 +550,10 @@ void rollout_x3(const RolloutArgs a) {
                                            pol_param_bytes(PHP > 0 ? PL : 0, PHP));
     float* colmax = colf + NC * 16;                     // [half][NC*16]: per-half column max (split owners)
     int* penbuf = reinterpret_cast<int*>(colmax + 2 * NC * 16);   // [step & 1][NC*16] penalty counts
-    float* xa = reinterpret_cast<float*>(penbuf + 2 * NC * 16);   // [X3_NCH][CB][A] normalised action inputs
-    f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + (PHP > 0 ? 0 : x3_xa_bytes(NC, A)));
-    f4* slab = slab0 + NC * 2 * 64;
-    float* const xch = reinterpret_cast<float*>(slab + P * NC * 2 * 64);   // AK: column exchange
+    float* xa = reinterpret_cast<float*>(penbuf + 2 * NC * 16);   // [NCH][CB][A] normalised action inputs
+    f4* slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(xa) + (PHP > 0 ? 0 : x3_xa_bytes(NC, A, NCH)));
+    f4* slab = slab0 + NC * NPT * 64;
+    float* const xch = reinterpret_cast<float*>(slab + SLABF * NC * 64);   // AK: column exchange
     float* const lnp = xch + NW * NC * 16 * 2;                            // LN: gamma [L][HP], beta [L][HP]
     if constexpr (LNK)
         for (int l = 0; l < L; ++l)
@@ -581,10 +595,10 @@ void rollout_x3(const RolloutArgs a) {
         return a.actions ? a.actions[((int64_t)h * a.K + c) * A + j]
                          : rng_action(a.seed, g, h, j, C[6 * 32 + j], C[7 * 32 + j]);
     };
-    // stage X3_NCH steps' action inputs from step h0: f64 normalise (dynamics.py:110),
+    // stage NCH steps' action inputs from step h0: f64 normalise (dynamics.py:110),
     // cast to f32 (TF feed); threads [0, nt) of the block
     auto fill_actions = [&](int h0, int nt) __attribute__((always_inline)) {
-        const int nhs = (a.H - h0 < X3_NCH) ? a.H - h0 : X3_NCH;
+        const int nhs = (a.H - h0 < NCH) ? a.H - h0 : NCH;
         if (!a.cem_mu && !a.actions) {
             // device Philox: one block feeds actions 2p and 2p + 1 (every thread's share of the
             // chunk's blocks halves: this fill runs on every wave, on the step's critical path)
@@ -825,7 +839,7 @@ void rollout_x3(const RolloutArgs a) {
         float mx = 0.f;
         if (owner && !X3_DIAG_NOOWNER) {
             // ---- normalise the state (dynamics.py:109), cast to f32 (TF feed), column max ----
-            const float* xr = xa + ((h % X3_NCH) * CB + 16 * cw + m) * A;
+            const float* xr = xa + ((h % NCH) * CB + 16 * cw + m) * A;
 #pragma unroll
             for (int k = 0; k < NHV; ++k)
 #pragma unroll
@@ -875,14 +889,14 @@ void rollout_x3(const RolloutArgs a) {
                     xl[i] = ll[0]; xl[i + 1] = ll[1];
                 }
                 // this half's 4 slots are bytes [8*hv0, 8*hv0+8) of the lane's 16-byte B fragment
-                reinterpret_cast<h4*>(slab0 + (cw * 2 + 0) * 64 + lane)[hv0] = xh;
-                if constexpr (!F1) reinterpret_cast<h4*>(slab0 + (cw * 2 + 1) * 64 + lane)[hv0] = xl;
+                reinterpret_cast<h4*>(slab0 + (cw * NPT + 0) * 64 + lane)[hv0] = xh;
+                if constexpr (!F1) reinterpret_cast<h4*>(slab0 + (cw * NPT + 1) * 64 + lane)[hv0] = xl;
                 if (hv0 == 0 && q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kAct;
             } else {
                 h8 xh, xl;
                 split8(xin, xh, xl);
-                swrite(slab0 + (cw * 2 + 0) * 64 + lane, xh);
-                if constexpr (!F1) swrite(slab0 + (cw * 2 + 1) * 64 + lane, xl);
+                swrite(slab0 + (cw * NPT + 0) * 64 + lane, xh);
+                if constexpr (!F1) swrite(slab0 + (cw * NPT + 1) * 64 + lane, xl);
                 if (q == 0) colf[cw * 16 + m] = ldexpf(a.winv[0], -sh) * kAct;
             }
         }
@@ -900,8 +914,8 @@ void rollout_x3(const RolloutArgs a) {
             h8 bh[NC], bl[NC];
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
-                bh[c] = sread(slab0 + (c * 2 + 0) * 64 + lane);
-                bl[c] = F1 ? bh[c] : sread(slab0 + (c * 2 + 1) * 64 + lane);
+                bh[c] = sread(slab0 + (c * NPT + 0) * 64 + lane);
+                bl[c] = F1 ? bh[c] : sread(slab0 + (c * NPT + 1) * 64 + lane);
             }
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -1005,8 +1019,8 @@ void rollout_x3(const RolloutArgs a) {
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
-                    swrite(slab + sidx<NC>(w * PW + pp, c, 0, lane), xh[pp][c]);
-                    if constexpr (!F1) swrite(slab + sidx<NC>(w * PW + pp, c, 1, lane), xl[pp][c]);
+                    swrite(slab + sidx<NC, F1>(w * PW + pp, c, 0, lane), xh[pp][c]);
+                    if constexpr (!F1) swrite(slab + sidx<NC, F1>(w * PW + pp, c, 1, lane), xl[pp][c]);
                 }
             auto ready = [&]() __attribute__((always_inline)) { X3_BARRIER_ID(3); };   // layer input complete
             X3_ST(4);
@@ -1066,7 +1080,7 @@ void rollout_x3(const RolloutArgs a) {
         // the owners reach this point first (the older waves win the MFMA arbitration):
         // they stage the next chunk's action inputs while the others finish
         if constexpr (PHP == 0)
-            if (owner && (h + 1) % X3_NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * (SO ? 2 * NC : NC));
+            if (owner && (h + 1) % NCH == 0 && h + 1 < a.H) fill_actions(h + 1, 64 * (SO ? 2 * NC : NC));
         X3_ST(7);
         X3_BARRIER_ID(4);                              // every wave is done reading the slab
 #pragma unroll
@@ -1233,6 +1247,7 @@ void rollout_x3(const RolloutArgs a) {
 }
 
 // ------------------------------------------------------------ launchers ----
+#ifndef X3_PROBE           // (tools/x3_probe.sh: one instantiation, resource report only)
 // X3_PART splits the instantiations over two translation units so each can be built with its own
 // scheduler (Makefile): 1 = the plain tanh delta net without a policy (cfg2..cfg5; built with
 // -amdgpu-sched-strategy=iterative-ilp, measured -2% kernel time at cfg3), 2 = everything else plus
@@ -1245,7 +1260,7 @@ hipError_t launch_rollout_x3_plain(const RolloutArgs& a, int hidden_padded, int 
 
 template <int HP, int NC, int NW, int PHP = 0, bool RW = false, int AK = 0, bool F1 = false>
 static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
-    if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1, 0, 0, AK, NW) > 160 * 1024) {
+    if constexpr (NC > NW || x3_lds_bytes_rt(HP, NC, 1, 1, 0, 0, AK, NW, F1) > 160 * 1024) {
         (void)a; (void)st;
         return hipErrorInvalidValue;
     } else {
@@ -1260,7 +1275,7 @@ static hipError_t launch_x3_t(const RolloutArgs& a, hipStream_t st) {
         if (RW != (a.model == BCMPC_MODEL_REWARD) || (RW && (a.L != 2 || a.S < 16))) return hipErrorInvalidValue;
         if (AK != ((a.act == BCMPC_ACT_RELU ? 1 : 0) | (a.ln ? 2 : 0))) return hipErrorInvalidValue;
         if (F1 != (a.f16_single != 0)) return hipErrorInvalidValue;
-        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, RW ? 3 : a.L, a.A, PHP > 0 ? a.pL : 0, PHP, AK, NW);
+        const size_t lds = (size_t)x3_lds_bytes_rt(HP, NC, RW ? 3 : a.L, a.A, PHP > 0 ? a.pL : 0, PHP, AK, NW, F1);
         if (lds > 160 * 1024) return hipErrorInvalidValue;
         const int64_t blocks = (a.K + 16 * NC - 1) / (16 * NC);
         hipLaunchKernelGGL((rollout_x3<HP, NC, NW, PHP, RW, AK, F1>), dim3((unsigned)blocks), dim3(64 * NW), lds, st, a);
@@ -1337,7 +1352,27 @@ static hipError_t launch_x3_plain_nc(const RolloutArgs& a, int hidden_padded, hi
     return launch_x3_plain_ncf<NC, false>(a, hidden_padded, st);
 }
 #if X3_PART != 1 && !defined(X3_ONLY)
+// Single-pass layouts beyond the split kernel's (the hi-only slab is half the size): at hidden 512,
+// 128-candidate groups (NC = 8, 8 waves: each 1-KiB weight fragment feeds 8 MFMAs) and two 64-candidate
+// 4-wave groups per CU (NC = 4, NW = 4: one group's serial f64 / epilogue chain beside the other's
+// MFMAs); at hidden 768 / 1024, 64-candidate groups (NC = 4).
+bool x3_f16_layout_ok(int hidden_padded, int nc, int nw) {
+    const int nwd = x3_waves(hidden_padded);
+    if (nw == nwd && (nc == 1 || nc == 2)) return true;
+    if (nw == nwd && nc == 4) return true;
+    if (hidden_padded == 512) return (nc == 8 && nw == 8) || (nc == 4 && nw == 4);
+    return false;
+}
+size_t x3_f16_lds(int hidden_padded, int n_layers, int nc, int nw, int action_dim) {
+    return (size_t)x3_lds_bytes_rt(hidden_padded, nc, n_layers, action_dim, 0, 0, 0, nw, true);
+}
 hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st) {
+    const int nw = a.x3_nw ? a.x3_nw : x3_waves(hidden_padded);
+    if (!x3_f16_layout_ok(hidden_padded, nc, nw)) return hipErrorInvalidValue;
+    if (hidden_padded == 512 && nw == 4) return launch_x3_t<512, 4, 4, 0, false, 0, true>(a, st);
+    if (hidden_padded == 512 && nc == 8) return launch_x3_t<512, 8, 8, 0, false, 0, true>(a, st);
+    if (nc == 4 && hidden_padded == 768) return launch_x3_t<768, 4, 8, 0, false, 0, true>(a, st);
+    if (nc == 4 && hidden_padded == 1024) return launch_x3_t<1024, 4, X3_NW1024, 0, false, 0, true>(a, st);
     switch (nc) {
         case 1: return launch_x3_plain_ncf<1, true>(a, hidden_padded, st);
         case 2: return launch_x3_plain_ncf<2, true>(a, hidden_padded, st);
@@ -1446,5 +1481,6 @@ hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hi
     }
 }
 #endif  // X3_PART != 1
+#endif  // X3_PROBE
 
 }  // namespace bcmpc
