@@ -428,6 +428,7 @@ class MPCcontrollerPolicyNet(Controller):
                     self.last_costs = None
                     self.last_cost, self.last_index = res.best_cost, res.best_index
                     return res.first_action
+                self._seed_rng.unread(seed)                      # (nothing drawn: the slow path draws it)
             self._fast = None
         S = int(math.prod(self.env.observation_space.shape))
         A = len(self.env.action_space.high)

@@ -309,6 +309,15 @@ struct bcmpc_engine {
     double gamma = 1.0;
 };
 
+// (team launch ordering across streams: team_order_before / team_order_after below)
+struct TeamOrder {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;
+    hipStream_t ev_stream = nullptr;
+    bool pending = false;
+};
+static TeamOrder g_team_order[64];
+
 extern "C" {
 
 int bcmpc_abi_version(void) { return BCMPC_ABI_VERSION; }
@@ -651,6 +660,14 @@ int bcmpc_destroy(bcmpc_engine* e) {
     if (!e) return BCMPC_OK;
     if (e->fb) (void)bcmpc_destroy(e->fb);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->stream && e->cfg.device >= 0 && e->cfg.device < 64) {   // its team launches have completed
+        TeamOrder& d = g_team_order[e->cfg.device];
+        std::lock_guard<std::mutex> lk(d.mu);
+        if (d.ev_stream == e->stream) {
+            d.pending = false;
+            d.ev_stream = nullptr;
+        }
+    }
     if (e->spec_st) {
         (void)hipStreamSynchronize(e->spec_st);
         (void)hipStreamDestroy(e->spec_st);
@@ -1070,6 +1087,34 @@ static bool team_failed(bcmpc_engine* e) {
     }
     return false;
 }
+// a synchronous control step's failure check after its stream completed.  With a communicator
+// attached, the exchange carried every rank's team status (comm.hip, wire record flags): the answer
+// is the OR over the ranks, identical on every rank, so every rank reruns the step together (each on
+// its fallback engine, which exchanges again) or none does
+static bool step_failed(bcmpc_engine* e) {
+    const bool local = team_failed(e);
+    if (e->comm) return comm_any_flags(e->comm);
+    return local;
+}
+
+// the stream synchronisation of a synchronous call; with a communicator attached it is bounded
+// (BCMPC_COMM_TIMEOUT_MS, default 60 s): a rank that never joins the exchange aborts the
+// communicator and fails the call instead of holding every other rank forever
+static int sync_step(bcmpc_engine* e, hipStream_t st) {
+    if (!e->comm) {
+        const hipError_t se = hipStreamSynchronize(st);
+        if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+        return BCMPC_OK;
+    }
+    static const int64_t timeout_ms = [] {
+        const char* v = std::getenv("BCMPC_COMM_TIMEOUT_MS");
+        return v && *v ? std::max<int64_t>(1, std::atoll(v)) : int64_t(60000);
+    }();
+    std::string err;
+    const int rc = comm_wait(e->comm, st, timeout_ms, &err);
+    return rc == BCMPC_OK ? BCMPC_OK : fail(rc, err);
+}
+
 static int team_status(bcmpc_engine* e) {
     if (team_failed(e))
         return fail(BCMPC_ERR_HIP, "team kernel: a workgroup team did not meet (its grid was not resident -- "
@@ -1079,8 +1124,10 @@ static int team_status(bcmpc_engine* e) {
 
 // the fallback engine of a team engine, created on first need and kept in sync with the team
 // engine's weights / policy / discount / action bounds (host copies)
-static int team_fallback(bcmpc_engine* e) {
-    if (e->comm)
+static int team_fallback(bcmpc_engine* e, bool collective = false) {
+    // (collective: every rank learned of the failure from the exchange and reruns with it; otherwise a
+    //  rank with a communicator attached cannot rerun one step alone)
+    if (e->comm && !collective)
         return fail(BCMPC_ERR_HIP, "team kernel: a workgroup team did not meet; with a communicator attached "
                                    "the ranks cannot rerun the step alone");
     if (!e->fb) {
@@ -1097,6 +1144,7 @@ static int team_fallback(bcmpc_engine* e) {
         if (rc != BCMPC_OK) return rc;
     }
     bcmpc_engine* f = e->fb;
+    f->comm = collective ? e->comm : nullptr;        // (the rerun's exchange: every rank reruns)
     if (!e->fb_wset || e->fb_wver != e->version) {
         const auto& hc = e->hw_copy;
         std::vector<const float*> k, b, g, be;
@@ -1148,13 +1196,6 @@ static int team_fallback(bcmpc_engine* e) {
 // be in flight: each records an event, and a team launch on another stream waits for it while it is
 // pending.  No call on the earlier stream is made later (it may be gone by then); graph capture
 // skips the ordering.
-struct TeamOrder {
-    std::mutex mu;
-    hipEvent_t ev = nullptr;
-    hipStream_t ev_stream = nullptr;
-    bool pending = false;
-};
-static TeamOrder g_team_order[64];
 
 struct SyncCall {                                   // marks a synchronous entry point's launches
     bcmpc_engine* e;
@@ -1162,11 +1203,14 @@ struct SyncCall {                                   // marks a synchronous entry
     ~SyncCall() { e->sync_call = false; }
 };
 
-static int team_order_before(int device, hipStream_t st) {
+// (the same-stream shortcut only for an engine's own stream, which lives as long as the engine and is
+//  cleared from the record in bcmpc_destroy: a caller's stream may be destroyed and its handle handed to a
+//  new stream, whose team launch must then still wait for the old grid)
+static int team_order_before(int device, hipStream_t st, hipStream_t own) {
     if (device < 0 || device >= 64) return BCMPC_OK;
     TeamOrder& d = g_team_order[device];
     std::lock_guard<std::mutex> lk(d.mu);
-    if (!d.pending || d.ev_stream == st) return BCMPC_OK;
+    if (!d.pending || (d.ev_stream == st && st == own)) return BCMPC_OK;
     const hipError_t q = hipEventQuery(d.ev);
     if (q == hipSuccess) {
         d.pending = false;
@@ -1336,7 +1380,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         // reported as a team that gave up (forces the fallback path deterministically)
         const char* sv = std::getenv("BCMPC_TEAM_SPINS");
         a.team_spins = sv && *sv ? std::max(-1, std::atoi(sv)) : 0;
-        if (const int rc = team_order_before(c.device, st)) return rc;
+        if (const int rc = team_order_before(c.device, st, e->stream)) return rc;
         // diagnostics: TEAM_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_tst = nullptr;
         static size_t tst_n = 0;
@@ -1456,8 +1500,9 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     if (d_result && e->comm && !cem) {
         // the one collective of a sharded control step: every rank's record, then np.argmin's rule
         std::string err;
-        if (comm_exchange(e->comm, d_result, c.cost == BCMPC_COST_REWARD, st, &err) != BCMPC_OK)
-            return fail(BCMPC_ERR_HIP, err);
+        if (const int xr = comm_exchange(e->comm, d_result, c.cost == BCMPC_COST_REWARD, st, &err,
+                                         e->kernel == BCMPC_KERNEL_TEAM ? e->d_team_err : nullptr))
+            return fail(xr, err);
     }
     if (record_events) HIP_TRY(hipEventRecord(e->ev[2], st));
     e->timed = record_events && d_result != nullptr;
@@ -1561,10 +1606,10 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
     if (spin) {
         if (const int wr = wait_done(e, e->seq)) return wr;
     } else {
-        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (const int sr = sync_step(e, e->stream)) return sr;
     }
-    if (team_failed(e)) {
-        if (const int fr = team_fallback(e)) return fr;
+    if (step_failed(e)) {
+        if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
         return bcmpc_get_action(e->fb, state, actions, seed, cand_offset, out, costs_out);
     }
     *out = lean ? *e->h_result_map : *e->h_result;
@@ -1978,7 +2023,9 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         // late hit (team kernel): the worker is still drawing this call's rows (a caller with no host work
         // between calls) -- launch now, the kernel waits for the rows' sequence word instead of the host
         // waiting for the worker (the job's parameters are written only by this thread, in predraw_post)
-        const bool late = predraw && mt_predraw_late() && e->kernel == BCMPC_KERNEL_TEAM && e->h_rows_seq &&
+        // (not with a communicator attached: a kernel that gave up waiting would have run the exchange on
+        //  unpublished rows, and the ranks cannot rerun one step alone -- the host waits for the worker)
+        const bool late = predraw && mt_predraw_late() && e->kernel == BCMPC_KERNEL_TEAM && e->h_rows_seq && !e->comm &&
                           n <= e->zc_cap && e->pre.inflight.load(std::memory_order_acquire) && same_job();
         if (late) e->pre.claimed.store(true, std::memory_order_release);
         // (otherwise no pre-draw is running past this point: the worker finishes its job before the buffers
@@ -2068,17 +2115,21 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         if (spin) {
             if (const int wr = wait_done(e, e->seq)) return wr;
         } else {
-            const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: the kernel reads h_zc)
-            if (rc != BCMPC_OK) return rc;
-            if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+            if (e->comm && rc == BCMPC_OK) {                // (bounded: the exchange's peers)
+                if (const int sr = sync_step(e, e->stream)) return sr;
+            } else {
+                const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: the kernel reads h_zc)
+                if (rc != BCMPC_OK) return rc;
+                if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+            }
         }
         if (late) {                                   // (the job is finished: the kernel has read its rows)
             predraw_wait(e);
             g = e->pre.to;
             e->pre.ready = false;
         }
-        if (team_failed(e)) {                         // (NumPy's state not yet advanced)
-            if (const int fr = team_fallback(e)) return fr;
+        if (step_failed(e)) {                         // (NumPy's state not yet advanced)
+            if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
             return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
                                             out, costs_out);
         }
@@ -2163,12 +2214,16 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         if (spin) {
             if (const int wr = wait_done(e, e->seq)) return wr;
         } else {
-            const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: nothing left in flight)
-            if (rc != BCMPC_OK) return rc;
-            if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+            if (e->comm && rc == BCMPC_OK) {                // (bounded: the exchange's peers)
+                if (const int sr = sync_step(e, e->stream)) return sr;
+            } else {
+                const hipError_t se = hipStreamSynchronize(e->stream);   // (also on error: nothing left in flight)
+                if (rc != BCMPC_OK) return rc;
+                if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+            }
         }
-        if (team_failed(e)) {                         // (NumPy's state not yet advanced)
-            if (const int fr = team_fallback(e)) return fr;
+        if (step_failed(e)) {                         // (NumPy's state not yet advanced)
+            if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
             return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
                                             out, costs_out);
         }
@@ -2249,11 +2304,15 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         hipMemcpyAsync(costs_out, e->d_costs, sizeof(double) * K, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
         rc = fail(BCMPC_ERR_HIP, "costs copy failed");
     // (also on error: the staging buffer's copies are done before it can be reused)
-    const hipError_t se = hipStreamSynchronize(e->stream);
-    if (rc != BCMPC_OK) return rc;
-    if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
-    if (team_failed(e)) {
-        if (const int fr = team_fallback(e)) return fr;
+    if (e->comm && rc == BCMPC_OK) {                // (bounded: the exchange's peers)
+        if (const int sr = sync_step(e, e->stream)) return sr;
+    } else {
+        const hipError_t se = hipStreamSynchronize(e->stream);
+        if (rc != BCMPC_OK) return rc;
+        if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+    }
+    if (step_failed(e)) {
+        if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
         return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed, out,
                                         costs_out);
     }
@@ -2277,9 +2336,13 @@ int bcmpc_mt19937_uniform_device(bcmpc_engine* e, uint32_t* mt_key, int32_t* mt_
     if (rc == BCMPC_OK &&
         hipMemcpyAsync(out, e->d_actions, n * sizeof(double), hipMemcpyDeviceToHost, e->stream) != hipSuccess)
         rc = fail(BCMPC_ERR_HIP, "action copy failed");
-    const hipError_t se = hipStreamSynchronize(e->stream);
-    if (rc != BCMPC_OK) return rc;
-    if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+    if (e->comm && rc == BCMPC_OK) {                // (bounded: the exchange's peers)
+        if (const int sr = sync_step(e, e->stream)) return sr;
+    } else {
+        const hipError_t se = hipStreamSynchronize(e->stream);
+        if (rc != BCMPC_OK) return rc;
+        if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
+    }
     std::memcpy(mt_key, e->h_mt_io + 640, kMtN * sizeof(uint32_t));
     *mt_pos = (int32_t)e->h_mt_io[640 + kMtN];
     return BCMPC_OK;

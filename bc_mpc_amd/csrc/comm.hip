@@ -20,9 +20,11 @@
 #include <rccl/rccl.h>
 #include <stdint.h>
 
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include "../../include/bcmpc.h"
 #include "kernels.h"
@@ -37,6 +39,8 @@ struct Rccl {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllGather) all_gather = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;
     std::string error;
 };
 
@@ -55,7 +59,10 @@ const Rccl& rccl() {
         r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
         r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
         r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
-        if (!r.get_unique_id || !r.init_rank || !r.destroy || !r.all_gather || !r.error_string)
+        r.abort = reinterpret_cast<decltype(r.abort)>(dlsym(h, "ncclCommAbort"));
+        r.async_error = reinterpret_cast<decltype(r.async_error)>(dlsym(h, "ncclCommGetAsyncError"));
+        if (!r.get_unique_id || !r.init_rank || !r.destroy || !r.all_gather || !r.error_string || !r.abort ||
+            !r.async_error)
             r.error = "librccl.so.1 lacks an expected symbol";
     });
     return r;
@@ -87,6 +94,51 @@ __global__ __launch_bounds__(64) void select_records_kernel(const bcmpc_result* 
     for (int w = threadIdx.x; w < kWords; w += 64) dst[w] = src[w];
 }
 
+// What travels in the exchange: the rank's result record plus its status flags (bit 0: this rank's
+// team kernel gave up, so its record is not a result).  Every rank sees every flag, so every rank
+// takes the same decision: select, or rerun the step together on the fallback engines.
+struct WireRecord {
+    bcmpc_result r;
+    uint32_t flags;
+    uint32_t pad[3];
+};
+static_assert(sizeof(WireRecord) % 16 == 0, "wire record");
+
+// one wave: the rank's record and its team error word (mapped host memory, written by the team
+// kernel earlier on this stream) into the send slot
+__global__ __launch_bounds__(64) void pack_wire_kernel(const bcmpc_result* __restrict__ res,
+                                                       const unsigned* team_err, WireRecord* __restrict__ wire) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(res);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&wire->r);
+    constexpr int kWords = sizeof(bcmpc_result) / sizeof(uint64_t);
+    for (int w = threadIdx.x; w < kWords; w += 64) dst[w] = src[w];
+    if (threadIdx.x == 0) {
+        const unsigned f = team_err ? __hip_atomic_load(team_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+        wire->flags = f ? 1u : 0u;
+        wire->pad[0] = wire->pad[1] = wire->pad[2] = 0u;
+    }
+}
+
+// one wave: np.argmin's rule over the n gathered records (valid ones; all are valid unless a flag is
+// set), and the OR of every rank's flags into the mapped word the host reads after the stream
+__global__ __launch_bounds__(64) void select_wire_kernel(const WireRecord* __restrict__ recs, int n, int maximize,
+                                                         bcmpc_result* __restrict__ out, unsigned* any_flags) {
+    const double sg = maximize ? -1.0 : 1.0;
+    int best = 0;
+    unsigned f = recs[0].flags;
+    for (int k = 1; k < n; ++k) {
+        f |= recs[k].flags;
+        if (record_better(sg * recs[k].r.best_cost, recs[k].r.best_index, sg * recs[best].r.best_cost,
+                          recs[best].r.best_index))
+            best = k;
+    }
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&recs[best].r);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(out);
+    constexpr int kWords = sizeof(bcmpc_result) / sizeof(uint64_t);
+    for (int w = threadIdx.x; w < kWords; w += 64) dst[w] = src[w];
+    if (threadIdx.x == 0) __hip_atomic_store(any_flags, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 int comm_fail(int code, const std::string& msg) { return set_error(code, msg); }   // -> bcmpc_last_error()
 
 // the exchange's select (also bcmpc_select_results_async): "" or the launch error
@@ -103,21 +155,86 @@ std::string launch_select_records(const bcmpc_result* recs, int n, int maximize,
 struct bcmpc_comm {
     ncclComm_t nccl = nullptr;
     int nranks = 0, rank = 0, device = 0;
-    bcmpc_result* d_gather = nullptr;   // [nranks] records
+    bcmpc::WireRecord* d_send = nullptr;     // this rank's record + flags
+    bcmpc::WireRecord* d_gather = nullptr;   // [nranks]
+    unsigned* h_flags = nullptr;             // mapped: OR of every rank's flags of the last exchange
+    unsigned* d_flags = nullptr;
+    bool aborted = false;                    // ncclCommAbort'ed after a timed-out exchange
 };
 
 namespace bcmpc {
 
-// enqueue the exchange after the argmin launch: all-gather every rank's record, select in place
-int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream_t st, std::string* err) {
+// enqueue the exchange after the argmin launch: pack (record + this rank's team status), all-gather
+// every rank's, select in place (+ the OR of the flags into the mapped word comm_any_flags reads)
+int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream_t st, std::string* err,
+                  const unsigned* d_team_err) {
+    if (c->aborted) {
+        *err = "the communicator was aborted after an exchange timed out; create a new one";
+        return BCMPC_ERR_STATE;
+    }
     const Rccl& r = rccl();
-    const ncclResult_t rc = r.all_gather(d_result, c->d_gather, sizeof(bcmpc_result), ncclUint8, c->nccl, st);
+    hipLaunchKernelGGL(pack_wire_kernel, dim3(1), dim3(64), 0, st, d_result, d_team_err, c->d_send);
+    if (hipGetLastError() != hipSuccess) {
+        *err = "pack_wire_kernel launch failed";
+        return BCMPC_ERR_HIP;
+    }
+    const ncclResult_t rc = r.all_gather(c->d_send, c->d_gather, sizeof(WireRecord), ncclUint8, c->nccl, st);
     if (rc != ncclSuccess) {
         *err = std::string("ncclAllGather: ") + r.error_string(rc);
         return BCMPC_ERR_HIP;
     }
-    *err = launch_select_records(c->d_gather, c->nranks, maximize, d_result, st);
-    return err->empty() ? BCMPC_OK : BCMPC_ERR_HIP;
+    hipLaunchKernelGGL(select_wire_kernel, dim3(1), dim3(64), 0, st, c->d_gather, c->nranks, maximize, d_result,
+                       c->d_flags);
+    if (hipGetLastError() != hipSuccess) {
+        *err = "select_wire_kernel launch failed";
+        return BCMPC_ERR_HIP;
+    }
+    return BCMPC_OK;
+}
+
+// after the stream has completed: did any rank flag its record (a team that gave up)?  Cleared here.
+bool comm_any_flags(bcmpc_comm* c) {
+    const unsigned f = __atomic_load_n(c->h_flags, __ATOMIC_ACQUIRE);
+    __atomic_store_n(c->h_flags, 0u, __ATOMIC_RELEASE);
+    return f != 0;
+}
+
+// Bounded wait for a stream whose work includes this communicator's exchange.  A rank that never joins
+// (crashed, or stuck in a collective of its own) would otherwise hold every other rank in
+// hipStreamSynchronize forever: poll the stream and RCCL's asynchronous error, and after timeout_ms
+// abort the communicator (ncclCommAbort ends its pending collectives) and report.  The communicator is
+// unusable afterwards (every later exchange fails with BCMPC_ERR_STATE).
+int comm_wait(bcmpc_comm* c, hipStream_t st, int64_t timeout_ms, std::string* err) {
+    const Rccl& r = rccl();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; ++i) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) return BCMPC_OK;
+        if (q != hipErrorNotReady) {
+            *err = std::string("exchange stream: ") + hipGetErrorString(q);
+            return BCMPC_ERR_HIP;
+        }
+        if ((i & 63) == 0) {
+            ncclResult_t ae = ncclSuccess;
+            if (r.async_error(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                *err = std::string("RCCL asynchronous error during the exchange: ") + r.error_string(ae);
+                (void)r.abort(c->nccl);
+                c->nccl = nullptr;
+                c->aborted = true;
+                return BCMPC_ERR_HIP;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+                (void)r.abort(c->nccl);
+                c->nccl = nullptr;
+                c->aborted = true;
+                (void)hipStreamSynchronize(st);           // (the aborted collective has returned)
+                *err = "exchange timed out after " + std::to_string(timeout_ms) +
+                       " ms (a rank did not join the all-gather); the communicator was aborted";
+                return BCMPC_ERR_HIP;
+            }
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(i < 1000 ? 0 : 50));
+    }
 }
 
 int comm_rank(const bcmpc_comm* c) { return c->rank; }
@@ -154,16 +271,25 @@ int bcmpc_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t dev
     if (hipSetDevice(device) != hipSuccess) return comm_fail(BCMPC_ERR_HIP, "hipSetDevice failed");
     bcmpc_comm* c = new bcmpc_comm();
     c->nranks = nranks; c->rank = rank; c->device = device;
-    if (hipMalloc(&c->d_gather, (size_t)nranks * sizeof(bcmpc_result)) != hipSuccess) {
+    auto release = [&]() {
+        if (c->d_send) (void)hipFree(c->d_send);
+        if (c->d_gather) (void)hipFree(c->d_gather);
+        if (c->h_flags) (void)hipHostFree(c->h_flags);
         delete c;
+    };
+    if (hipMalloc(&c->d_send, sizeof(WireRecord)) != hipSuccess ||
+        hipMalloc(&c->d_gather, (size_t)nranks * sizeof(WireRecord)) != hipSuccess ||
+        hipHostMalloc(&c->h_flags, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->d_flags, c->h_flags, 0) != hipSuccess) {
+        release();
         return comm_fail(BCMPC_ERR_HIP, "device allocation failed");
     }
+    *c->h_flags = 0u;
     ncclUniqueId u;
     std::memcpy(u.internal, id, BCMPC_COMM_ID_BYTES);
     const ncclResult_t rc = r.init_rank(&c->nccl, nranks, u, rank);   // collective over the nranks
     if (rc != ncclSuccess) {
-        (void)hipFree(c->d_gather);
-        delete c;
+        release();
         return comm_fail(BCMPC_ERR_HIP, std::string("ncclCommInitRank: ") + r.error_string(rc));
     }
     *out = c;
@@ -175,7 +301,9 @@ int bcmpc_comm_destroy(bcmpc_comm* c) {
     if (!c) return BCMPC_OK;
     (void)hipSetDevice(c->device);
     if (c->nccl) (void)rccl().destroy(c->nccl);
+    if (c->d_send) (void)hipFree(c->d_send);
     if (c->d_gather) (void)hipFree(c->d_gather);
+    if (c->h_flags) (void)hipHostFree(c->h_flags);
     delete c;
     return BCMPC_OK;
 }

@@ -1283,8 +1283,11 @@ static int fit_iteration_reward(bcmpc_fitter* f, const int64_t* d_idx, int strid
         return BCMPC_OK;
     };
     if (int rc = head(2, S, f->d_dp, 1, 1, f->d_dh2)) return rc;     // delta head -> d_dh2
-    if (int rc = head(4, 1, f->d_dpr, 3, 2, f->d_dz)) return rc;     // reward head -> d_dz (its last use)
-    hipLaunchKernelGGL(fit_add, dim3((B * h + 255) / 256), dim3(256), 0, st, f->d_dh2, f->d_dz, B * h);
+    // reward head -> d_dh: free once the head's own fit_act_bwd has consumed it (its last GEMM reads d_dz as
+    // the A operand, so the result must not land in d_dz: the GEMM's tiles would overwrite rows that sibling
+    // workgroups still read)
+    if (int rc = head(4, 1, f->d_dpr, 3, 2, f->d_dh)) return rc;
+    hipLaunchKernelGGL(fit_add, dim3((B * h + 255) / 256), dim3(256), 0, st, f->d_dh2, f->d_dh, B * h);
     FIT_TRY(hipGetLastError());
     // trunk: dH0 (d_dh2) -> LN / tanh backward -> dense's gradients
     if (ln)

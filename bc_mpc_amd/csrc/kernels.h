@@ -159,7 +159,10 @@ hipError_t launch_mt_draw(const MtDrawArgs& a, hipStream_t st);
 
 // ---- library-owned min-loc exchange (comm.hip) ----
 int set_error(int code, const std::string& msg);          // bcmpc_last_error() text (capi.cpp)
-int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream_t st, std::string* err);
+int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream_t st, std::string* err,
+                  const unsigned* d_team_err);
+bool comm_any_flags(bcmpc_comm* c);
+int comm_wait(bcmpc_comm* c, hipStream_t st, int64_t timeout_ms, std::string* err);
 int comm_rank(const bcmpc_comm* c);
 int comm_size(const bcmpc_comm* c);
 int comm_device(const bcmpc_comm* c);

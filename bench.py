@@ -79,6 +79,7 @@ F16_MFMA_PEAK_TFLOPS = 2516.6     # dense f16/bf16 MFMA: 512 MAC/clk/SIMD x 1024
 # f32-equivalent (algorithmic) ceiling is a third of the f16 peak
 SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
+TRAFFIC_FILE = "r04_traffic_per_launch.json"
 
 
 def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None, reward=False):
@@ -151,10 +152,11 @@ def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explor
     per_call = el / calls
     # 1 thread: one full-K call unless it would take over ~6x the budget (assumed linear in the pool size)
     K1 = Ks if per_call * threads <= 6 * budget_s else max(256, int(Ks * 6 * budget_s / (per_call * threads)))
+    short = per_call * threads < 0.1 * budget_s          # (small K: many 1-thread calls, not one)
     with threadpool_limits(limits=1, user_api="blas"):
-        v1, calls1, el1 = timed(K1, 0.0, max_calls=1)
+        v1, calls1, el1 = timed(K1, budget_s / 2 if short else 0.0, max_calls=(1 << 30) if short else 1)
     return dict(value=v, unit="candidate-steps/s", cores=int(threads), kind="port", K_sampled=Ks,
-                value_1thread=v1, K_sampled_1thread=K1, cpu_model=_cpu_model(),
+                value_1thread=v1, K_sampled_1thread=K1, cpu_model=_cpu_model(), host_cpus=os.cpu_count(),
                 sample=f"{calls} oracle get_action calls at K={Ks} (workload K={K_full}), H={H}, {net}, "
                        f"OpenBLAS {threads} threads, {el:.1f} s; 1 thread: {calls1} call at K={K1}, {el1:.1f} s")
 
@@ -347,7 +349,64 @@ def make_engine(wl, prob, device, precision):
 SMALL_K = ("ppo_defaults", "ppo_mpc_default", "runsh_recipe", "cfg1")
 
 
-def small_k_lines(device, calls=200, warmup=20):
+def roofline_line(K, H, fpcs, kernel_ms, precision, iters=1):
+    """The MFMA roofline of one launch: algorithmic FLOPs (K x H x flop_per_cand_step) / HIP-event kernel
+    time, against the peak of the precision the engine computes in."""
+    peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16": F16_MFMA_PEAK_TFLOPS}.get(precision, SPLIT_PEAK_TFLOPS)
+    tf = K * H * iters * fpcs / (kernel_ms / 1e3) / 1e12
+    return {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s", "frac": tf / peak,
+            "flop_per_launch": K * H * iters * fpcs}
+
+
+def oracle_weights(prob, wl):
+    from oracle import mpc_oracle as orc      # (the cpu_baseline leg only: the checker, timed on the host)
+    if prob["reward"]:
+        return orc.RewardMLPWeights(prob["kernels"], prob["biases"], prob["ln_g"], prob["ln_b"])
+    return orc.MLPWeights(prob["kernels"], prob["biases"], wl["act"], prob["ln_g"], prob["ln_b"])
+
+
+def net_label(wl, prob):
+    net = (f"reward net {wl['hidden']}" if prob["reward"] else f"{wl['L']}x{wl['hidden']} {wl['act']}") + \
+        (" + LN" if prob["ln"] else "") + (f" + policy {prob['policy']}" if prob["policy"] else "")
+    if prob["policy"] and wl.get("policy_mode") == "stochastic":
+        net += " (oracle policy in its deterministic explore branch: TF's sampler is not restatable)"
+    return net
+
+
+def cfg2_line(device, calls=100, warmup=10, cpu_seconds=4.0, dropin_calls=20, with_cpu=True):
+    """BASELINE configs[1] (K=4096, H=20, 2x500 tanh, 1 GPU, fp32 tolerance): complete get_action p50, the
+    rollout kernel's HIP-event time and roofline, the drop-in controller's p50 and the oracle on the host."""
+    wl = WORKLOADS["cfg2"]
+    prob = synthetic_problem(wl)
+    eng = make_engine(wl, prob, device, "auto")
+    ts = []
+    for i in range(warmup + calls):
+        t0 = time.perf_counter()
+        eng.get_action(prob["state"], None, seed=0xC2 + i)
+        if i >= warmup:
+            ts.append(time.perf_counter() - t0)
+    eng.set_timing(True)
+    ks = []
+    for i in range(max(20, calls // 2)):
+        eng.get_action(prob["state"], None, seed=0xC2 + i)
+        ks.append(eng.last_kernel_ms()[0])
+    fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
+    row = {"K": wl["K"], "H": wl["H"], "kernel": eng.info()["kernel"], "precision": eng.precision,
+           "value": wl["K"] * wl["H"] / float(np.median(ts)), "unit": "candidate-steps/s",
+           "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
+           "roofline": roofline_line(wl["K"], wl["H"], fpcs, float(np.mean(ks)), eng.precision)}
+    eng.close()
+    if dropin_calls:
+        d = dropin_parity_p50(wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"], False, prob["kernels"],
+                              prob["biases"], None, None, prob["norm"], prob["state"], device, dropin_calls, 1)
+        row["dropin_parity_p50_ms"] = d["p50_ms"]
+    if with_cpu:
+        row["cpu_baseline"] = cpu_baseline(oracle_weights(prob, wl), prob["norm"], prob["state"], wl["H"], cpu_seconds,
+                                           wl["K"], net_label(wl, prob))
+    return row
+
+
+def small_k_lines(device, calls=200, warmup=20, cpu_seconds=3.0, with_cpu=True):
     """get_action p50 (host state in, device-drawn actions, host result out) and the rollout kernel's
     HIP-event time for the small-K workloads the reference actually runs (train_mpc_ppo.py:71,77: K=400;
     run.sh:27-31; BASELINE cfg1), with the auto kernel (the team kernel, rollout_team.hip) and with the
@@ -389,11 +448,21 @@ def small_k_lines(device, calls=200, warmup=20):
             row[tag + "kernel_ms"] = float(np.mean(ks))
             eng.close()
         row["speedup_p50"] = row["slab_p50_ms"] / row["p50_ms"]
+        fpcs = flop_per_cand_step(wl["hidden"], wl["L"], policy=prob["policy"], reward=prob["reward"])
+        row["roofline"] = roofline_line(wl["K"], wl["H"], fpcs, row["kernel_ms"], row["precision"])
+        row["roofline"]["note"] = ("small K is latency-bound by design (a few dozen 16-candidate columns on "
+                                   "256 CUs); the line's figure of merit is p50")
         # the drop-in controller in parity mode (NumPy's stream, controllers.py:53 / :191 / :310)
         d = dropin_small_k(name, wl, prob, device)
         row["dropin_controller"] = d["controller"]
         row["dropin_parity_p50_ms"] = d["p50_ms"]
         row["dropin_parity_p50_gap50us_ms"] = d["p50_gap50us_ms"]
+        if with_cpu:
+            # the reference's own configuration on the host: the oracle (NumPy restatement) at this full K
+            row["cpu_baseline"] = cpu_baseline(oracle_weights(prob, wl), prob["norm"], prob["state"], wl["H"],
+                                               cpu_seconds, wl["K"], net_label(wl, prob), prob["pol_arrays"],
+                                               wl.get("explore", 0.5), prob["gamma"], None)
+            row["cpu_baseline"]["p50_ms_per_get_action"] = wl["K"] * wl["H"] / row["cpu_baseline"]["value"] * 1e3
         out[name] = row
     return out
 
@@ -445,6 +514,7 @@ def main():
                     help="skip the f16_single_pass line (BASELINE cfg3's bf16-class GEMM on the f16 engine)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cfg2", action="store_true", help="skip the cfg2 line (BASELINE configs[1], K=4096)")
     ap.add_argument("--no-small-k", action="store_true",
                     help="skip the small-K get_action lines (ppo_defaults, runsh_recipe, cfg1: team vs slab kernel)")
     args = ap.parse_args()
@@ -637,7 +707,10 @@ def main():
         "cpu_baseline": None,
         "small_k": None,
     }
-    prof = os.path.join(REPO, "profiles", "traffic_per_launch.json")
+    # PMC HBM traffic per launch of THIS round's kernels (tools/r04_traffic.sh: rocprofv3 --pmc FETCH_SIZE /
+    # WRITE_SIZE in separate passes, the gfx950 FETCH_SIZE x2 correction calibrated on the action tensor)
+    prof = os.path.join(REPO, "profiles", TRAFFIC_FILE)
+    out["roofline"]["traffic_source"] = f"profiles/{TRAFFIC_FILE}"
     if os.path.exists(prof):
         try:
             # PMC traffic of this kernel in this action mode (device: Philox actions in-kernel, hbm: read)
@@ -658,7 +731,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, net,
                                            pol_arrays, wl.get("explore", 0.5), gamma, cem)
     if rank == 0 and world == 1 and not args.no_small_k:
-        out["small_k"] = small_k_lines(local)
+        out["small_k"] = small_k_lines(local, with_cpu=not args.no_cpu_baseline)
+    if rank == 0 and world == 1 and not args.no_cfg2 and args.workload == "cfg3" and not args.no_small_k:
+        out["cfg2"] = cfg2_line(local, with_cpu=not args.no_cpu_baseline)
     if (rank == 0 and world == 1 and not args.no_f16 and not (cem or policy or reward or ln) and act == "tanh"
             and eng.precision != "f16"):
         out["f16_single_pass"] = f16_line(wl, prob, local)

@@ -72,6 +72,49 @@ def test_single_rank_exchange_is_identity():
     comm.close()
 
 
+def test_single_rank_exchange_team_giveup_reruns_collectively(monkeypatch):
+    """A team that gives up while a communicator is attached: the exchange carries the rank's status
+    flag (comm.hip wire record), every rank sees the OR of the flags, and every rank reruns the step on
+    its fallback engine with the communicator attached (one rank here: the whole path on one card).
+    Forced with BCMPC_TEAM_SPINS=-1; the answer is the reference fixture's, NumPy's stream advances once."""
+    from bc_mpc_amd import _lib
+    from conftest import Golden
+    from test_gpu_parity import _engine, argmin_is_decidable, assert_costs_close
+    lib = _lib.load()
+    idbuf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    _lib.check(lib.bcmpc_comm_unique_id(idbuf))
+    comm = _Comm(idbuf, 1, 0)
+    assert comm.rc == 0, comm.err
+    g = Golden("cfg1_2x500_tanh")
+    eng = _engine(g, kernel="team")
+    assert eng.info()["kernel"] == "team"
+    eng.set_comm(comm)
+    monkeypatch.setenv("BCMPC_TEAM_SPINS", "-1")
+    res = eng.get_action(g.state, g.actions(), return_costs=True)
+    assert eng.team_reruns == 1
+    assert_costs_close(res.costs, g.costs, g.near, "cfg1 collective rerun")
+    if argmin_is_decidable(g):
+        assert res.best_index == g.argmin and np.array_equal(res.first_action, g.opt_action)
+    # the NumPy-stream drop-in path: the rerun draws again from the same state, the stream advances once
+    np.random.seed(9)
+    st = np.random.get_state()
+    low, high = -np.ones(g.A), np.ones(g.A)
+    r1 = eng.get_action_numpy_stream(g.state, low, high, g.K)
+    after = np.random.get_state()
+    assert eng.team_reruns == 2
+    monkeypatch.delenv("BCMPC_TEAM_SPINS")
+    np.random.set_state(st)
+    r2 = eng.get_action_numpy_stream(g.state, low, high, g.K)       # the team meets: no rerun
+    assert eng.team_reruns == 2
+    # (the rerun ran the fallback's split slab kernel, r2 the team kernel: same arithmetic, another
+    #  summation order of the output partials -- the stated tolerance, same argmin)
+    assert r1.best_index == r2.best_index and abs(r1.best_cost - r2.best_cost) <= 1e-4 + 1e-5 * abs(r2.best_cost)
+    assert np.array_equal(np.random.get_state()[1], after[1]) and np.random.get_state()[2] == after[2]
+    eng.set_comm(None)
+    eng.close()
+    comm.close()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
