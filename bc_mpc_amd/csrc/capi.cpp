@@ -155,6 +155,7 @@ struct bcmpc_engine {
     int pack_tb = 4;                   // output tiles per packed block of layers 0..L-1
     bool split = false;                // BCMPC_PREC_SPLIT_F16 or F16 (rollout_x3)
     bool f16 = false;                  // BCMPC_PREC_F16: single MFMA pass
+    bool pp = false;                   // BCMPC_PREC_F16 on the two-group pipelined kernel (rollout_pp)
     int nc = 0;                        // split kernel: 16-candidate columns per workgroup
     int nwl = 0;                       // packed weight layers (RolloutArgs.w entries)
     float winv[BCMPC_MAX_LAYERS + 1]{};  // split kernel: 1 / operand scales per layer
@@ -492,9 +493,18 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
             };
             const char* en = std::getenv("BCMPC_F16_NC");
             const char* ew = std::getenv("BCMPC_F16_NW");
+            const char* ep = std::getenv("BCMPC_F16_PP");
+            if (ep && ep[0] == '1' && !(en && *en) && !(ew && *ew) &&
+                x3_pp_ok(e->HP, c.n_layers, c.state_dim, c.action_dim) && cols >= 8) {
+                // the two-group pipelined kernel (rollout_pp): 128 candidates per workgroup, 4 waves per
+                // group own 8 hidden tiles each (weights packed 8 tiles per wave)
+                e->pp = true;
+                nc = 8;
+                nw = 8;
+            }
             if (en && *en) nc = std::atoi(en);
             if (ew && *ew) nw = std::atoi(ew);
-            if (nc == 0 && !(ew && *ew) && e->HP == 512 && cols >= 4 * 512 && f16_fits(4, 4)) {
+            if (!e->pp && nc == 0 && !(ew && *ew) && e->HP == 512 && cols >= 4 * 512 && f16_fits(4, 4)) {
                 // two 64-candidate 4-wave groups per CU: 0.90 ms at cfg3 against 0.94 (one 8-wave group of
                 // 64) and 0.91 (one of 128), three boxes (profiles/r04_f16_layouts_ab.txt)
                 nc = 4;
@@ -505,7 +515,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                 for (int n : {8, 4, 2})
                     if (f16_fits(n, nw) && cols >= (int64_t)n * 256 && !(n >= 4 && e->HP <= 256)) { nc = n; break; }
             }
-            if (!f16_fits(nc, nw)) {
+            if (!e->pp && !f16_fits(nc, nw)) {
                 delete e;
                 return fail(BCMPC_ERR_UNSUPPORTED, "F16 precision: no single-pass layout for this shape / NC / NW");
             }
@@ -545,7 +555,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     }
     e->kernel = kern;
     e->nw = nw;
-    e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->T / nw;   // split: output tiles per wave
+    e->pack_tb = kern == BCMPC_KERNEL_SOLO ? 4 : e->pp ? e->T / 4 : e->T / nw;   // split: output tiles per wave
     const int L = c.n_layers, T = e->T;
     size_t off = 0, boff = 0;
     e->nwl = reward ? 3 : L + 1;
@@ -1292,6 +1302,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     }
     a.f16_single = e->f16 ? 1 : 0;
     a.x3_nw = e->nw;
+    a.x3_pp = e->pp ? 1 : 0;
     a.consts = e->d_consts;
     a.state = d_state; a.state_stride = stride;
     if (state_inline) {                       // the tiled state by value in the kernel arguments

@@ -83,6 +83,7 @@ struct RolloutArgs {
     float hsc[BCMPC_MAX_LAYERS];             // split LN nets: power-of-two scale of hidden layer l's output
     int32_t f16_single;                      // BCMPC_PREC_F16: one f16 MFMA pass (hi x hi), no lo operands
     int32_t x3_nw;                           // split kernel: waves per workgroup (0: x3_waves' default)
+    int32_t x3_pp;                           // single-pass f16: the two-group pipelined kernel (rollout_pp)
     uint64_t* stamps;                        // diagnostics (X3_STAMP builds): [blocks][NW][10] phase cycles
     // split kernel: np.argmin fused into the launch's tail (fused_argmin != 0): every workgroup
     // leaves its best (cost, index) in amin.scratch_c/i[blockIdx.x], the last to finish (ticket)
@@ -184,6 +185,7 @@ bool x3_policy_ok(int hidden_padded, int nc);
 // single-pass f16 layouts (BCMPC_PREC_F16): the (nc, nw) pairs this build instantiates, and their LDS
 bool x3_f16_layout_ok(int hidden_padded, int nc, int nw);
 size_t x3_f16_lds(int hidden_padded, int n_layers, int nc, int nw, int action_dim);
+bool x3_pp_ok(int hidden_padded, int n_layers, int state_dim, int action_dim);   // rollout_pp's shapes
 hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
 hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
 size_t rr_image_bytes(int hidden_padded);

@@ -1246,6 +1246,426 @@ void rollout_x3(const RolloutArgs a) {
     }
 }
 
+// ------------------------------------------------------------ rollout_pp ----
+// Single-pass f16 (BCMPC_PREC_F16) as a two-group software pipeline (round 4; the plain 2-layer tanh
+// delta net at hidden 512).  rollout_x3's step is a lock-step chain: every wave of the workgroup runs the
+// same phase at once (f64 state update, layer 0 and its tanh, the hidden layer's MFMAs, its tanh and the
+// output layer), so the SIMDs' matrix pipes idle through the VALU phases and the VALU through the MFMA
+// phase (PMC + stamps + ablations: profiles/r04_pmc_f16/).  Here a 512-thread workgroup holds TWO
+// independent 64-candidate groups, waves 0-3 and 4-7 (waves w and w + 4 share a SIMD), each with its own
+// hi-only slab.  A group's control step is three segments:
+//   C  (wave wl owns column wl of its group, all 32 state dims): the output partials of the previous step
+//      summed in fixed order, f64 de-normalise + residual + cheetah cost, f64 normalise of the next input
+//      (column power-of-two scale), layer 0 for its OWN column from registers (all 32 tiles: the B fragment
+//      is the lane's own 8 inputs, no slab, no barrier), its tanh, its column of the hidden-layer slab;
+//   M  the hidden layer's MFMAs (wave wl: tiles [8wl, 8wl + 8) of all 4 columns, slab B fragments);
+//   E  its tanh, the K-split output layer (the wave's own 4 k-steps from registers), the partials into
+//      the slab, the next action inputs staged.
+// Every segment ends at the workgroup barrier, and group 1 runs one segment ahead of group 0, so each
+// barrier interval pairs C with E (VALU beside VALU: the two waves of a SIMD interleave their VALU), M with
+// C and E with M (the matrix pipe of one wave beside the other's VALU).  C touches only its own column of
+// the slab (partials and layer input alike: fragment index = c mod NC), so it needs no barrier of its own;
+// M reads what every C of its group wrote (one interval earlier); E overwrites the slab only after every M
+// of its group has read it (one interval earlier).  Arithmetic as rollout_x3<..., F1 = true>: the same
+// f16 operands and power-of-two scales, f32 accumulate, f64 state / cost.
+#ifndef PP_NCH
+#define PP_NCH 4                 // steps of action inputs staged per fill
+#endif
+__host__ __device__ constexpr int pp_xa_bytes(int A) { return (PP_NCH * 64 * A * 4 + 15) & ~15; }
+__host__ __device__ constexpr int pp_group_bytes(int HP, int A) { return pp_xa_bytes(A) + (HP / 32) * 4 * 1024; }
+__host__ __device__ constexpr int pp_lds_bytes(int HP, int A) { return param_bytes(2, HP) + 2 * pp_group_bytes(HP, A); }
+// (+ the groups' counters [2][2] ints | layer-0 slabs [2][NC] fragments | column factors [2][64])
+__host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_bytes(HP, A) + 16 + 2 * 4 * 1024 + 2 * 64 * 4; }
+
+// The hidden layer of one group (single pass, hi operands): acc[j][c] += W[tile j] x X[c] over the P
+// k-steps, fully unrolled (no loop-carried operand sets: fixed accumulator registers).  Weights in units of
+// PG tiles through PD + 1 register sets, PD units in flight ahead of the MFMAs (the wave is alone on its
+// SIMD's matrix pipe in this segment: nothing else hides its L2 latency); s0 holds units 0..PD-1.
+#ifndef PP_G
+#define PP_G 2
+#endif
+#ifndef PP_D
+#define PP_D 3
+#endif
+template <int TW, int NC, int P, int PG, int PD>
+__device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
+                                      int lane, const h8 (&s0)[PD * PG]) {
+    constexpr int NG = TW / PG, NU = P * NG, NS = PD + 1;
+    const int voff = lane * 16;
+    h8 sr[NS][PG], bh[NC];
+#pragma unroll
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+        for (int j = 0; j < PG; ++j) sr[d][j] = s0[d * PG + j];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        if (u + PD < NU) {
+            const int un = u + PD;
+#pragma unroll
+            for (int j = 0; j < PG; ++j)
+                sr[un % NS][j] = fload(rs, voff, wbase + (un / NG) * TW * 2048 + ((un % NG) * PG + j) * 2048);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (u % NG == 0) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) bh[c] = sread(slab + sidx<NC, true>(u / NG, c, 0, lane));
+        }
+        const int g = u % NG;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int j = 0; j < PG; ++j) acc[g * PG + j][c] = mfma16(sr[u % NS][j], bh[c], acc[g * PG + j][c]);
+    }
+}
+
+template <int HP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void rollout_pp(const RolloutArgs a) {
+    constexpr int NC = 4;                         // 16-candidate columns per group
+    constexpr int T = HP / 16, P = T / 2;         // hidden tiles, k-steps
+    constexpr int TW = T / 4, PW = TW / 2;        // per wave (4 waves per group)
+    constexpr int CB = 16 * NC;                   // candidates per group
+    static_assert(T == 32 && TW == 8 && PW == 4, "hidden 512");
+    extern __shared__ __attribute__((aligned(16))) f4 lds[];
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = w >> 2, wl = w & 3;
+    const int q = lane >> 4, m = lane & 15;
+    const int64_t gc0 = (int64_t)blockIdx.x * (2 * CB) + grp * CB;     // the group's first candidate
+    const int64_t cand = gc0 + 16 * wl + m;                           // this lane's candidate (column wl)
+    const bool valid = cand < a.K;
+    const int S = a.S, A = a.A;
+
+    double* C = reinterpret_cast<double*>(lds);
+    float* Bl = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + kConstRows * kConstCols * 8);
+    for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
+    for (int l = 0; l < 2; ++l)
+        for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kTanhK;
+    float* const Bout = Bl + 2 * HP;
+    for (int i = threadIdx.x; i < 32; i += blockDim.x) Bout[i] = a.b[2][i];
+    char* const gbase = reinterpret_cast<char*>(lds) + param_bytes(2, HP) + grp * pp_group_bytes(HP, A);
+    float* const xa = reinterpret_cast<float*>(gbase);                  // [PP_NCH][CB][A] normalised actions
+    f4* const slab = reinterpret_cast<f4*>(gbase + pp_xa_bytes(A));     // [P][NC] hi fragments | partials
+
+    // lane (q, m) holds dims 16k + 4q + r (k = 0, 1) of its candidate: the MFMA B-fragment order
+    double s[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int d = 16 * k + 4 * q + r;
+            s[k][r] = (valid && d < S) ? (a.state_inline ? a.state_v[d] : a.state[cand * a.state_stride + d]) : 0.0;
+        }
+    if (a.traj && valid) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * k + 4 * q + r;
+                if (d < S) a.traj[cand * S + d] = s[k][r];
+            }
+    }
+    double cost = 0.0;                                  // trajectory_cost = 0 (cost_functions.py:60)
+
+    // the group's action inputs of PP_NCH steps from h0: f64 normalise (dynamics.py:110), f32 (the TF
+    // feed); the group's 256 threads
+    const int gt = threadIdx.x - 256 * grp;
+    auto fill_actions = [&](int h0) __attribute__((always_inline)) {
+        const int nhs = (a.H - h0 < PP_NCH) ? a.H - h0 : PP_NCH;
+        if (!a.cem_mu && !a.actions) {
+            const int AP = (A + 1) >> 1, per = CB * AP;
+            for (int i = gt; i < nhs * per; i += 256) {
+                const int hh = i / per, rem = i - hh * per, kl = rem / AP, p2 = rem - kl * AP;
+                const int j0 = 2 * p2, j1 = min(2 * p2 + 1, A - 1);
+                float x0 = 0.f, x1 = 0.f;
+                if (gc0 + kl < a.K) {
+                    double v0, v1;
+                    rng_action_pair(a.seed, (uint64_t)(a.cand_offset + gc0 + kl), h0 + hh, p2, C[6 * 32 + j0],
+                                    C[7 * 32 + j0], C[6 * 32 + j1], C[7 * 32 + j1], v0, v1);
+                    x0 = (float)div_rn(__dsub_rn(v0, C[2 * 32 + j0]), C[3 * 32 + j0], C[9 * 32 + j0]);
+                    x1 = (float)div_rn(__dsub_rn(v1, C[2 * 32 + j1]), C[3 * 32 + j1], C[9 * 32 + j1]);
+                }
+                float* const dst = xa + (hh * CB + kl) * A;
+                dst[j0] = x0;
+                if (2 * p2 + 1 < A) dst[j1] = x1;
+            }
+            return;
+        }
+        const int per = CB * A;
+        for (int i = gt; i < nhs * per; i += 256) {
+            const int hh = i / per, rem = i - hh * per, kl = rem / A, j = rem - kl * A;
+            float xv = 0.f;
+            if (gc0 + kl < a.K) {
+                const int64_t c = gc0 + kl;
+                const uint64_t gg = (uint64_t)(a.cand_offset + c);
+                const double v = a.cem_mu ? cem_action(a.seed, gg, h0 + hh, j, a.cem_iter, a.cem_mu[(h0 + hh) * A + j],
+                                                       a.cem_sigma[(h0 + hh) * A + j], C[6 * 32 + j], C[7 * 32 + j])
+                                          : a.actions[((int64_t)(h0 + hh) * a.K + c) * A + j];
+                xv = (float)div_rn(__dsub_rn(v, C[2 * 32 + j]), C[3 * 32 + j], C[9 * 32 + j]);
+            }
+            xa[(hh * CB + kl) * A + j] = xv;
+        }
+    };
+    fill_actions(0);
+    __syncthreads();
+
+    const int voff = lane * 16;
+    const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
+    const __amdgpu_buffer_rsrc_t rs1 = layer_rsrc(a.w[1], a.wbytes[1]);
+    const __amdgpu_buffer_rsrc_t rso = layer_rsrc(a.w[2], a.wbytes[2]);
+    const float f1 = a.winv[1] * kTanhK, fo = a.winv[2];
+    const int wbase1 = wl * P * TW * 2048;              // this wave's hidden-layer weight slice
+    f4* const slab0 = reinterpret_cast<f4*>(reinterpret_cast<char*>(lds) + pp_lds_bytes(HP, A) + 16) + grp * NC * 64;
+    float* const colf = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + pp_lds_bytes(HP, A) + 16 +
+                                                 2 * NC * 1024) + grp * CB;
+    // per-group LDS counters (monotone over the steps): C's layer-0 inputs published, M's slab reads done
+    int* const cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + pp_lds_bytes(HP, A)) + 2 * grp;
+    if (threadIdx.x < 4) reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + pp_lds_bytes(HP, A))[threadIdx.x] = 0;
+    __syncthreads();
+
+    f4 acc[TW][NC];
+    h8 uh[PP_D * PP_G];                                 // ME's first PP_D operand units (issued in C)
+    h8 a0[TW];                                          // layer-0 fragments of this wave's tiles (issued in ME)
+#pragma unroll
+    for (int j = 0; j < TW; ++j) a0[j] = fload(rs0, voff, (wl * TW + j) * 2048);
+    // (X3_STAMP variant builds: s_memtime per phase; slots 0 C/owner, 1 C/wait for the group's inputs,
+    //  2 C/layer 0 + tanh, 3 ME/MFMAs, 4 ME/tanh + output, 5 ME/group wait, 6 ME/partials + fill,
+    //  7 barrier, 8 idle segments)
+    uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    const int nseg = 2 * a.H + 1;                       // C(0) ME(0) ... ME(H-1) C(H) (the last cost)
+    for (int k = 0; k < nseg + 1; ++k) {
+        // (an opaque zero added to every weight offset and LDS table base: the weights and tables are the
+        //  same every step, and without it the compiler hoists the loop-invariant loads out of the loop)
+        int wz = 0;
+        asm volatile("" : "+s"(wz));
+        const double* const Cz = C + wz;
+        const float* const Blz = Bl + wz;
+        const float* const Boutz = Bout + wz;
+        const int seg = k - (grp == 0 ? 1 : 0);         // group 1 runs one segment ahead
+        if (seg >= 0 && seg < nseg) {
+            const int h = seg >> 1;
+            if ((seg & 1) == 0) {
+                // ---------------- C(h) ----------------
+                if (h > 0) {
+                    f4 o[2];
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) o[v] = slab[((0 * 2 + v) * NC + wl) * 64 + lane];
+#pragma unroll
+                    for (int g2 = 1; g2 < 4; ++g2)                 // fixed summation order
+#pragma unroll
+                        for (int v = 0; v < 2; ++v) o[v] += slab[((g2 * 2 + v) * NC + wl) * 64 + lane];
+                    // cheetah penalties on the current state (cost_functions.py:16-26): dims 5..7 in row q = 1
+                    const int npen = partner_row16((s[0][1] >= 0.2) + (s[0][2] >= 0.0) + (s[0][3] >= 0.0));
+                    const double s17 = s[1][1];
+                    // de-normalise + residual (dynamics.py:113,116), f64, no FMA
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) {
+                        const f4 bv = *reinterpret_cast<const f4*>(Boutz + 16 * v + 4 * q);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int d = 16 * v + 4 * q + r;
+                            if (d < S) {
+                                const float dn = fmaf(o[v][r], fo, bv[r]);
+                                const double ud = __dadd_rn(__dmul_rn((double)dn, Cz[5 * 32 + d]), Cz[4 * 32 + d]);
+                                s[v][r] = __dadd_rn(s[v][r], ud);
+                            }
+                        }
+                    }
+                    if (a.cost == BCMPC_COST_CHEETAH) {
+                        const double score = __dsub_rn(10.0 * (double)npen,
+                                                       div_rn(__dsub_rn(s[1][1], s17), 0.01, 1.0 / 0.01));
+                        cost = __dadd_rn(cost, score);
+                    }
+                    if (a.traj && valid) {
+#pragma unroll
+                        for (int v = 0; v < 2; ++v)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int d = 16 * v + 4 * q + r;
+                                if (d < S) a.traj[((int64_t)h * a.K + cand) * S + d] = s[v][r];
+                            }
+                    }
+                }
+                if (h < a.H) {
+                    // normalise the state (dynamics.py:109), f32 (TF feed), the staged actions; the column's
+                    // power-of-two scale; its B fragment into the layer-0 slab
+                    const float* xr = xa + ((h % PP_NCH) * CB + 16 * wl + m) * A;
+                    float xin[8];
+#pragma unroll
+                    for (int v = 0; v < 2; ++v)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int d = 16 * v + 4 * q + r;
+                            float xv = 0.f;
+                            if (d < S) xv = (float)div_rn(__dsub_rn(s[v][r], Cz[0 * 32 + d]), Cz[1 * 32 + d], Cz[8 * 32 + d]);
+                            else if (d < S + A) xv = xr[d - S];
+                            xin[4 * v + r] = xv;
+                        }
+                    float mx = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fabsf(xin[i]));
+                    mx = max_rows32(max_rows16(mx));
+                    int e = 0;
+                    (void)frexpf(mx, &e);                      // column scale: max |x| -> [2^11, 2^12)
+                    int sh = 12 - e;
+                    sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
+                    const float sc = ldexpf(1.0f, sh);
+                    h8 bown;                                   // (the k order of pack_x3_layer)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) bown[i] = (_Float16)(xin[i] * sc);
+                    swrite(slab0 + wl * 64 + lane, bown);
+                    if (q == 0) colf[16 * wl + m] = ldexpf(a.winv[0], -sh) * kTanhK;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+                if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                X3_ST(0);
+                if (h < a.H) {
+                    // the group's four layer-0 inputs published (and every partial of the slab read)
+                    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (h + 1))
+                        __builtin_amdgcn_s_sleep(1);
+                    X3_ST(1);
+                    // layer 0 [S+A -> h]: this wave's 8 tiles x the group's 4 columns
+                    h8 b0[NC];
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) b0[c] = sread(slab0 + c * 64 + lane);
+                    const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int c = 0; c < NC; ++c)
+#pragma unroll
+                        for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0[j], b0[c], z4);
+                    // ME's first operand units, in flight through the tanh below and the barrier
+#pragma unroll
+                    for (int j = 0; j < PP_D * PP_G; ++j)          // (units 0..PP_D-1: k-step 0 onwards)
+                        uh[j] = fload(rs1, voff, wz + wbase1 + ((j / TW) * TW + (j % TW)) * 2048);
+                    // tanh, this wave's 4 k-steps of the hidden-layer slab (all 4 columns)
+#pragma unroll
+                    for (int pp = 0; pp < PW; ++pp)
+#pragma unroll
+                        for (int c = 0; c < NC; ++c) {
+                            h8 xh, xl;
+                            epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[16 * c + m], Blz, wl * TW + 2 * pp, q,
+                                     xh, xl);
+                            swrite(slab + ((wl * PW + pp) * NC + c) * 64 + lane, xh);
+                        }
+                }
+                X3_ST(2);
+            } else {
+                // ---------------- ME(h): the hidden layer's MFMAs, its tanh, the output layer ----------------
+#pragma unroll
+                for (int j = 0; j < TW; ++j)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
+                mm_pp<TW, NC, P, PP_G, PP_D>(rs1, wz + wbase1, slab, acc, lane, uh);
+                // this wave's slab reads have returned: count it (the group's partials overwrite the slab
+                // only once all 4 waves have, below)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                X3_ST(3);
+                f4 po[2][NC];
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) po[v][c] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int pp = 0; pp < PW; ++pp) {
+                    h8 oh[2];
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) oh[v] = fload(rso, voff, wz + (((wl * PW + pp) * 2 + v) * 2) * 1024);
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        h8 xh, xl;
+                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f1, Blz + HP, wl * TW + 2 * pp, q, xh, xl);
+#pragma unroll
+                        for (int v = 0; v < 2; ++v) po[v][c] = mfma16(oh[v], xh, po[v][c]);
+                    }
+                }
+                X3_ST(4);
+                // every wave of the group has finished reading the slab (by now the others are normally long
+                // past their MFMAs)
+                while (__hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (h + 1))
+                    __builtin_amdgcn_s_sleep(1);
+                X3_ST(5);
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) slab[((wl * 2 + v) * NC + c) * 64 + lane] = po[v][c];
+                if ((h + 1) % PP_NCH == 0 && h + 1 < a.H) fill_actions(h + 1);
+                // the next step's layer-0 fragments (in flight through the barrier and C's owner phase)
+#pragma unroll
+                for (int j = 0; j < TW; ++j) a0[j] = fload(rs0, voff, wz + (wl * TW + j) * 2048);
+                X3_ST(6);
+            }
+        } else {
+            X3_ST(8);
+        }
+        __syncthreads();
+        X3_ST(7);
+    }
+    if constexpr (X3_STAMP) {
+        if (a.stamps && lane == 0)
+            for (int k2 = 0; k2 < 10; ++k2) a.stamps[((size_t)blockIdx.x * 8 + w) * 10 + k2] = ph_[k2];
+    }
+
+    const bool holder = valid && q == 0;                // cost in row 0 (dims 1, 17 and the penalty count)
+    if (a.costs && holder) a.costs[cand] = cost;
+    if (a.fused_argmin) {
+        // np.argmin fused (as rollout_x3): this workgroup's best, the last workgroup reduces the records
+        const ArgminArgs& am = a.amin;
+        Best best{__builtin_inf(), INT64_MAX};
+        if (holder) best = Best{am.maximize ? -cost : cost, cand};
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const Best o{__shfl_xor(best.c, off), __shfl_xor(best.i, off)};
+            if (better(o, best)) best = o;
+        }
+        double* rc = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + param_bytes(2, HP) + pp_xa_bytes(A));
+        int64_t* ri = reinterpret_cast<int64_t*>(rc + 16);
+        if (lane == 0) { rc[w] = best.c; ri[w] = best.i; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < 8; ++k) {
+                const Best o{rc[k], ri[k]};
+                if (better(o, best)) best = o;
+            }
+            __hip_atomic_store(&am.scratch_c[blockIdx.x], best.c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&am.scratch_i[blockIdx.x], best.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned tk = __hip_atomic_fetch_add(a.amin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = tk == gridDim.x - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            ri[16] = last ? 1 : 0;
+        }
+        __syncthreads();
+        if (ri[16] == 0) return;
+        best = Best{__builtin_inf(), INT64_MAX};
+        for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+            const Best o{am.scratch_c[b], am.scratch_i[b]};
+            if (better(o, best)) best = o;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const Best o{__shfl_xor(best.c, off), __shfl_xor(best.i, off)};
+            if (better(o, best)) best = o;
+        }
+        __syncthreads();
+        if (lane == 0) { rc[w] = best.c; ri[w] = best.i; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < 8; ++k) {
+                const Best o{rc[k], ri[k]};
+                if (better(o, best)) best = o;
+            }
+            argmin_write(am, best);
+            *a.amin_ticket = 0;
+        }
+    }
+}
+
 // ------------------------------------------------------------ launchers ----
 #ifndef X3_PROBE           // (tools/x3_probe.sh: one instantiation, resource report only)
 // X3_PART splits the instantiations over two translation units so each can be built with its own
@@ -1366,7 +1786,26 @@ bool x3_f16_layout_ok(int hidden_padded, int nc, int nw) {
 size_t x3_f16_lds(int hidden_padded, int n_layers, int nc, int nw, int action_dim) {
     return (size_t)x3_lds_bytes_rt(hidden_padded, nc, n_layers, action_dim, 0, 0, 0, nw, true);
 }
+bool x3_pp_ok(int hidden_padded, int n_layers, int state_dim, int action_dim) {
+    return hidden_padded == 512 && n_layers == 2 && state_dim + action_dim <= 32 &&
+           pp_lds_total(512, action_dim) <= 160 * 1024;
+}
 hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st) {
+    if (a.x3_pp) {
+        if (!x3_pp_ok(hidden_padded, a.L, a.S, a.A) || a.model != BCMPC_MODEL_DELTA || a.pL > 0 ||
+            a.act != BCMPC_ACT_TANH || a.ln || !a.f16_single)
+            return hipErrorInvalidValue;
+        static bool attr_set = false;
+        if (!attr_set) {
+            const hipError_t e = hipFuncSetAttribute((const void*)rollout_pp<512>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+            attr_set = true;
+        }
+        const int64_t blocks = (a.K + 127) / 128;
+        hipLaunchKernelGGL(rollout_pp<512>, dim3((unsigned)blocks), dim3(512), (size_t)pp_lds_total(512, a.A), st, a);
+        return hipGetLastError();
+    }
     const int nw = a.x3_nw ? a.x3_nw : x3_waves(hidden_padded);
     if (!x3_f16_layout_ok(hidden_padded, nc, nw)) return hipErrorInvalidValue;
     if (hidden_padded == 512 && nw == 4) return launch_x3_t<512, 4, 4, 0, false, 0, true>(a, st);

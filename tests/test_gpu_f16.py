@@ -138,6 +138,54 @@ def test_f16_full_size_cfg3_properties():
         e.close()
 
 
+@pytest.fixture
+def pp_kernel(monkeypatch):
+    monkeypatch.setenv("BCMPC_F16_PP", "1")
+    yield
+    monkeypatch.delenv("BCMPC_F16_PP", raising=False)
+
+
+def _pp_fixtures():
+    out = []
+    for n in _mpc_tanh_fixtures():
+        g = Golden(n)
+        if g.meta["hidden"] > 256 and g.meta["hidden"] <= 512 and g.meta["L"] == 2 and g.K >= 128:
+            out.append(n)
+    return out
+
+
+@pytest.mark.parametrize("name", _pp_fixtures())
+def test_f16_pp_vs_reference_fixture(name, pp_kernel):
+    """The two-group pipelined single-pass kernel (rollout_pp, BCMPC_F16_PP=1) on the reference-run
+    fixtures it takes (2-layer tanh, hidden 257..512, K >= 128): the f16 bar, NaN pattern, argmin quality."""
+    test_f16_engine_vs_reference_fixture(name, "auto")
+
+
+@pytest.mark.parametrize("K,H", [(128, 1), (200, 3), (1000, 15), (4096, 7)])
+def test_f16_pp_ragged_vs_oracle(K, H, pp_kernel):
+    """Ragged K (a partly empty second group, a partly empty column), H = 1 and an odd H: the pipelined
+    kernel against the oracle on the same Philox actions (the f16 bar), and deterministic."""
+    from oracle import mpc_oracle as orc
+    w = orc.synthetic_weights(20, 6, 500, 2, "tanh", False, seed_base=31)
+    norm = orc.synthetic_normalization()
+    state = orc.synthetic_state(norm)
+    eng = _engine(20, 6, w, H, K, norm)
+    res = eng.get_action(state, None, seed=77, return_costs=True)
+    acts = orc.device_rng_actions(77, 0, K, H, -np.ones(6), np.ones(6))
+    want, states = orc.rollout(orc.NumpyDynamics(w, norm), state, acts)
+    _check(res.costs, want, orc.near_threshold_mask(states, F16_NEAR), H, f"pp K{K} H{H}")
+    assert res.best_index == int(np.argmin(res.costs))
+    r2 = eng.get_action(state, None, seed=77, return_costs=True)
+    assert np.array_equal(r2.costs, res.costs)                       # deterministic
+    eng.close()
+
+
+def test_f16_pp_full_size_cfg3_properties(pp_kernel):
+    """cfg3 at full size on the pipelined kernel: the full-size properties of the single-group test
+    (determinism, bitwise shard invariance, oracle sample, the split engine's whole cost vector)."""
+    test_f16_full_size_cfg3_properties()
+
+
 def test_f16_refuses_other_nets():
     from bc_mpc_amd.engine import RolloutEngine
     with pytest.raises(Exception):

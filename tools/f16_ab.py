@@ -1,6 +1,7 @@
 """A/B of single-pass f16 layouts (BCMPC_F16_NC / BCMPC_F16_NW) at cfg3 (K=65536, H=20, 2x500 tanh):
 complete get_action (device Philox actions), HIP-event kernel time, rounds alternating the layouts.
-usage: python tools/f16_ab.py [--rounds 2] [--steps 30] nc,nw [nc,nw ...]   (nc,nw = 0,0: split engine)"""
+usage: python tools/f16_ab.py [--rounds 2] [--steps 30] nc,nw [nc,nw ...]   (nc,nw = 0,0: split engine;
+"pp": the two-group pipelined single-pass kernel)"""
 import argparse
 import json
 import os
@@ -30,11 +31,13 @@ def weights(hidden=500, S=20, A=6, L=2):
 def run(layout, k, b, norm, steps, warmup, K=65536, H=20):
     nc, nw = layout
     prec = "split" if nc == 0 else "f16"
-    if nc:
+    if nc == -1:                                  # the two-group pipelined kernel
+        os.environ["BCMPC_F16_PP"] = "1"
+    elif nc:
         os.environ["BCMPC_F16_NC"], os.environ["BCMPC_F16_NW"] = str(nc), str(nw)
     eng = RolloutEngine(20, 6, 500, 2, "tanh", False, H, K, precision=prec)
-    os.environ.pop("BCMPC_F16_NC", None)
-    os.environ.pop("BCMPC_F16_NW", None)
+    for v in ("BCMPC_F16_NC", "BCMPC_F16_NW", "BCMPC_F16_PP"):
+        os.environ.pop(v, None)
     eng.set_weights(MLPSpec(k, b, "tanh"), norm, version=1)
     eng.set_timing(True)
     state = np.linspace(-0.5, 0.5, 20)
@@ -51,7 +54,8 @@ def run(layout, k, b, norm, steps, warmup, K=65536, H=20):
     km = float(np.mean(ks))
     peak = 2516.6 if nc else 2516.6 / 3
     tf = K * H * FLOP / (km / 1e3) / 1e12
-    return {"layout": f"{prec} nc={info.get('nc', nc)} nw={info.get('waves_per_block', nw)}",
+    return {"layout": "f16 pp (two-group pipeline)" if nc == -1 else
+            f"{prec} nc={info.get('nc', nc)} nw={info.get('waves_per_block', nw)}",
             "kernel": info["kernel"], "value": K * H / float(np.mean(ts)), "p50_ms": float(np.median(ts) * 1e3),
             "kernel_ms": km, "tflops": tf, "frac": tf / peak}
 
@@ -64,7 +68,7 @@ def main():
     ap.add_argument("layouts", nargs="+")
     a = ap.parse_args()
     k, b, norm = weights()
-    lays = [tuple(int(x) for x in s.split(",")) for s in a.layouts]
+    lays = [(-1, 0) if s == "pp" else tuple(int(x) for x in s.split(",")) for s in a.layouts]
     for r in range(a.rounds):
         for lay in lays:
             print(json.dumps(dict(round=r, **run(lay, k, b, norm, a.steps, a.warmup))), flush=True)
