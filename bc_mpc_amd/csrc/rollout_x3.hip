@@ -1285,7 +1285,7 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 #define PP_G 2
 #endif
 #ifndef PP_D
-#define PP_D 3
+#define PP_D 2
 #endif
 template <int TW, int NC, int P, int PG, int PD>
 __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
@@ -1426,9 +1426,6 @@ void rollout_pp(const RolloutArgs a) {
 
     f4 acc[TW][NC];
     h8 uh[PP_D * PP_G];                                 // ME's first PP_D operand units (issued in C)
-    h8 a0[TW];                                          // layer-0 fragments of this wave's tiles (issued in ME)
-#pragma unroll
-    for (int j = 0; j < TW; ++j) a0[j] = fload(rs0, voff, (wl * TW + j) * 2048);
     // (X3_STAMP variant builds: s_memtime per phase; slots 0 C/owner, 1 C/wait for the group's inputs,
     //  2 C/layer 0 + tanh, 3 ME/MFMAs, 4 ME/tanh + output, 5 ME/group wait, 6 ME/partials + fill,
     //  7 barrier, 8 idle segments)
@@ -1448,6 +1445,10 @@ void rollout_pp(const RolloutArgs a) {
             const int h = seg >> 1;
             if ((seg & 1) == 0) {
                 // ---------------- C(h) ----------------
+                // this wave's layer-0 fragments, in flight through the owner phase
+                h8 a0[TW];
+#pragma unroll
+                for (int j = 0; j < TW; ++j) a0[j] = fload(rs0, voff, wz + (wl * TW + j) * 2048);
                 if (h > 0) {
                     f4 o[2];
 #pragma unroll
@@ -1592,9 +1593,6 @@ void rollout_pp(const RolloutArgs a) {
 #pragma unroll
                     for (int c = 0; c < NC; ++c) slab[((wl * 2 + v) * NC + c) * 64 + lane] = po[v][c];
                 if ((h + 1) % PP_NCH == 0 && h + 1 < a.H) fill_actions(h + 1);
-                // the next step's layer-0 fragments (in flight through the barrier and C's owner phase)
-#pragma unroll
-                for (int j = 0; j < TW; ++j) a0[j] = fload(rs0, voff, wz + (wl * TW + j) * 2048);
                 X3_ST(6);
             }
         } else {

@@ -484,6 +484,16 @@ def f16_line(wl, prob, device, steps=50, warmup=5):
         ts.append(time.perf_counter() - t0)
         ks.append(eng.last_kernel_ms()[0])
     kern = eng.info()["kernel"]
+    # argmin agreement with the f32-grade split engine (within the fp32 envelope of the oracle:
+    # tests/test_gpu_parity.py; against the oracle itself: tests/test_gpu_f16.py) over 16 seeds
+    split = make_engine(wl, prob, device, "split")
+    agree, regret = 0, []
+    for sd in range(1, 17):
+        rf = eng.get_action(prob["state"], None, seed=sd)
+        rs = split.get_action(prob["state"], None, seed=sd, return_costs=True)
+        agree += int(rf.best_index == rs.best_index)
+        regret.append(float(rs.costs[rf.best_index] - rs.best_cost))
+    split.close()
     eng.close()
     fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
     tf = K * H * fpcs / (float(np.mean(ks)) / 1e3) / 1e12
@@ -491,7 +501,11 @@ def f16_line(wl, prob, device, steps=50, warmup=5):
             "kernel": kern, "value": K * H / float(np.mean(ts)), "unit": "candidate-steps/s",
             "p50_ms": float(np.percentile(ts, 50) * 1e3), "kernel_ms_avg": float(np.mean(ks)),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tf / F16_MFMA_PEAK_TFLOPS}}
+                         "frac": tf / F16_MFMA_PEAK_TFLOPS},
+            "argmin_agreement": {"seeds": 16, "top1_equal": agree,
+                                 "reference": "the split (f32-grade) engine's argmin on the same actions",
+                                 "regret_median": float(np.median(regret)), "regret_max": float(np.max(regret)),
+                                 "regret_unit": "split-engine cost of the f16 choice minus its minimum"}}
 
 
 def main():
