@@ -637,6 +637,13 @@ void rollout_x3(const RolloutArgs a) {
     const __amdgpu_buffer_rsrc_t rs0 = layer_rsrc(a.w[0], a.wbytes[0]);
     const __amdgpu_buffer_rsrc_t rso = layer_rsrc(a.w[LO], a.wbytes[LO]);
     const float fo = a.winv[LO];
+    // An opaque zero, refreshed every step, added to the step loop's weight offsets and LDS table bases:
+    // the weights, biases and constants are the same every step, and without it the compiler hoists
+    // their loop-invariant loads out of the step loop and keeps them in registers for the whole launch
+    // (round 4: 76 spilled registers at the 4-wave single-pass layout).
+    int wz = 0;
+    const double* Cv = C;
+    const float* Blv = Bl;
 
     // Operand sets in flight ahead of their MFMAs (issued before the preceding VALU phase):
     //   a0h/a0l : layer-0 fragments of the NEXT step (issued after the output MFMAs)
@@ -655,14 +662,14 @@ void rollout_x3(const RolloutArgs a) {
         constexpr int slot = decltype(SLOTc)::value;
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
-            const int o = (((w * PW + pp) * 2 + v) * 2) * 1024;
+            const int o = wz + (((w * PW + pp) * 2 + v) * 2) * 1024;
             oh[2 * slot + v] = fload(rso, voff, o);
             ol[2 * slot + v] = F1 ? oh[2 * slot + v] : fload(rso, voff, o + 1024);
         }
     };
     auto load_next = [&](int l_next) __attribute__((always_inline)) {
         if (l_next < L) {
-            aload_x3<G, F1>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, w * P * TW * 2048 + kown * TW * 2048, uh, ul);
+            aload_x3<G, F1>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, wz + w * P * TW * 2048 + kown * TW * 2048, uh, ul);
         } else {
             load_out(0, std::integral_constant<int, 0>{});
             if constexpr (OP > 1) load_out(1, std::integral_constant<int, OP - 1>{});
@@ -828,6 +835,10 @@ void rollout_x3(const RolloutArgs a) {
     uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp_ = X3_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.H; ++h) {
+        wz = 0;
+        asm volatile("" : "+s"(wz));
+        Cv = C + wz;
+        Blv = Bl + wz;
         double pact[4] = {0.0, 0.0, 0.0, 0.0};            // policy actions of dims 16 + 4q + r (half-1 owners)
         if constexpr (PHP > 0) {
             policy_step(h, pact);
@@ -847,11 +858,11 @@ void rollout_x3(const RolloutArgs a) {
                     const int d = 16 * (hv0 + k) + 4 * q + r;
                     float xv = 0.f;
                     if (d < S) {
-                        xv = (float)div_rn(__dsub_rn(s[k][r], C[0 * 32 + d]), C[1 * 32 + d], C[8 * 32 + d]);
+                        xv = (float)div_rn(__dsub_rn(s[k][r], Cv[0 * 32 + d]), Cv[1 * 32 + d], Cv[8 * 32 + d]);
                     } else if (d < S + A) {
                         if constexpr (PHP > 0) {              // the policy's action (dynamics.py:110)
                             const int j = d - S;
-                            xv = (float)div_rn(__dsub_rn(pact[r], C[2 * 32 + j]), C[3 * 32 + j], C[9 * 32 + j]);
+                            xv = (float)div_rn(__dsub_rn(pact[r], Cv[2 * 32 + j]), Cv[3 * 32 + j], Cv[9 * 32 + j]);
                         } else {
                             xv = xr[d - S];
                         }
@@ -937,13 +948,13 @@ void rollout_x3(const RolloutArgs a) {
             float f0[NC];
 #pragma unroll
             for (int c = 0; c < NC; ++c) f0[c] = colf[c * 16 + m];
-            epi_colx<AK, TW, NC, NW>(acc, f0, Bl, lnp, lnp + L * HP, a.hsc[0], a.hidden, xch, w, lane, xh, xl, fcol);
+            epi_colx<AK, TW, NC, NW>(acc, f0, Blv, lnp, lnp + L * HP, a.hsc[0], a.hidden, xch, w, lane, xh, xl, fcol);
         } else {
 #pragma unroll
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
-                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[c * 16 + m], Bl, w * TW + 2 * pp, q,
+                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[c * 16 + m], Blv, w * TW + 2 * pp, q,
                              xh[pp][c], xl[pp][c]);
         }
         X3_ST(3);
@@ -986,7 +997,7 @@ void rollout_x3(const RolloutArgs a) {
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
-                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], fr, Bl + 2 * HP, w * TW + 2 * pp, q, xh[pp][c],
+                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], fr, Blv + 2 * HP, w * TW + 2 * pp, q, xh[pp][c],
                              xl[pp][c]);
 #pragma unroll
             for (int pp = 0; pp < PW; ++pp)
@@ -1008,7 +1019,7 @@ void rollout_x3(const RolloutArgs a) {
             for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
-                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], fd, Bl + HP, w * TW + 2 * pp, q, xh[pp][c],
+                    epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], fd, Blv + HP, w * TW + 2 * pp, q, xh[pp][c],
                              xl[pp][c]);
         }
         // ---- hidden layers 1..L-1 [h -> h] through the slab ----
@@ -1039,14 +1050,14 @@ void rollout_x3(const RolloutArgs a) {
                 float fl[NC];
 #pragma unroll
                 for (int c = 0; c < NC; ++c) fl[c] = DYN ? f * fcol[c] : f;
-                epi_colx<AK, TW, NC, NW>(acc, fl, Bl + l * HP, lnp + l * HP, lnp + (L + l) * HP, a.hsc[l], a.hidden,
+                epi_colx<AK, TW, NC, NW>(acc, fl, Blv + l * HP, lnp + l * HP, lnp + (L + l) * HP, a.hsc[l], a.hidden,
                                          xch, w, lane, xh, xl, fcol);
             } else {
 #pragma unroll
                 for (int pp = 0; pp < PW; ++pp)
 #pragma unroll
                     for (int c = 0; c < NC; ++c)
-                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Bl + l * HP, w * TW + 2 * pp, q,
+                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f, Blv + l * HP, w * TW + 2 * pp, q,
                                  xh[pp][c], xl[pp][c]);
             }
         }
@@ -1076,7 +1087,7 @@ void rollout_x3(const RolloutArgs a) {
             }
         }
         __builtin_amdgcn_sched_barrier(0);              // (not hoisted above the MFMAs' operand waits)
-        if constexpr (PHP == 0) aload_x3<TW, F1>(rs0, voff, w * TW * 2048, a0h, a0l);   // next step's layer 0
+        if constexpr (PHP == 0) aload_x3<TW, F1>(rs0, voff, wz + w * TW * 2048, a0h, a0l);   // next step's layer 0
         // the owners reach this point first (the older waves win the MFMA arbitration):
         // they stage the next chunk's action inputs while the others finish
         if constexpr (PHP == 0)
@@ -1114,13 +1125,13 @@ void rollout_x3(const RolloutArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < NHV; ++k) {
-            const f4 bv = *reinterpret_cast<const f4*>(Bout + 16 * (hv0 + k) + 4 * q);
+            const f4 bv = *reinterpret_cast<const f4*>(Blv + LB * HP + 16 * (hv0 + k) + 4 * q);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int d = 16 * (hv0 + k) + 4 * q + r;
                 if (d < S) {
                     const float dn = fmaf(o[k][r], foc, bv[r]);            // BiasAdd (f32)
-                    const double ud = __dadd_rn(__dmul_rn((double)dn, C[5 * 32 + d]), C[4 * 32 + d]);
+                    const double ud = __dadd_rn(__dmul_rn((double)dn, Cv[5 * 32 + d]), Cv[4 * 32 + d]);
                     s[k][r] = __dadd_rn(s[k][r], ud);
                 }
             }
@@ -1287,10 +1298,11 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 #ifndef PP_D
 #define PP_D 2
 #endif
-template <int TW, int NC, int P, int PG, int PD>
-__device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
+template <int TW, int NC, int P, int PG, int PD, int TWH = TW, int T0 = 0>
+__device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TWH][NC],
                                       int lane, const h8 (&s0)[PD * PG]) {
-    constexpr int NG = TW / PG, NU = P * NG, NS = PD + 1;
+    // (TWH < TW: tiles [T0, T0 + TWH) of the wave's TW only)
+    constexpr int NG = TWH / PG, NU = P * NG, NS = PD + 1;
     const int voff = lane * 16;
     h8 sr[NS][PG], bh[NC];
 #pragma unroll
@@ -1303,7 +1315,7 @@ __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, cons
             const int un = u + PD;
 #pragma unroll
             for (int j = 0; j < PG; ++j)
-                sr[un % NS][j] = fload(rs, voff, wbase + (un / NG) * TW * 2048 + ((un % NG) * PG + j) * 2048);
+                sr[un % NS][j] = fload(rs, voff, wbase + (un / NG) * TW * 2048 + (T0 + (un % NG) * PG + j) * 2048);
             __builtin_amdgcn_sched_barrier(0);
         }
         if (u % NG == 0) {
@@ -1326,6 +1338,7 @@ void rollout_pp(const RolloutArgs a) {
     constexpr int TW = T / 4, PW = TW / 2;        // per wave (4 waves per group)
     constexpr int CB = 16 * NC;                   // candidates per group
     static_assert(T == 32 && TW == 8 && PW == 4, "hidden 512");
+    static_assert(PP_D * PP_G <= TW / 2, "the prefetched first units lie in k-step 0 of a tile half");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
@@ -1554,34 +1567,52 @@ void rollout_pp(const RolloutArgs a) {
                 X3_ST(2);
             } else {
                 // ---------------- ME(h): the hidden layer's MFMAs, its tanh, the output layer ----------------
-#pragma unroll
-                for (int j = 0; j < TW; ++j)
-#pragma unroll
-                    for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
-                mm_pp<TW, NC, P, PP_G, PP_D>(rs1, wz + wbase1, slab, acc, lane, uh);
-                // this wave's slab reads have returned: count it (the group's partials overwrite the slab
-                // only once all 4 waves have, below)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                X3_ST(3);
                 f4 po[2][NC];
 #pragma unroll
                 for (int v = 0; v < 2; ++v)
 #pragma unroll
                     for (int c = 0; c < NC; ++c) po[v][c] = (f4){0.f, 0.f, 0.f, 0.f};
+                // in two halves of the wave's 8 tiles (64 accumulator registers instead of 128; each slab k-step
+                // read twice): half 0's tanh and output MFMAs run after its MFMAs while half 1's first weight
+                // units are in flight
+                auto half = [&](auto HFc) __attribute__((always_inline)) {
+                    constexpr int hf = decltype(HFc)::value;
+                    constexpr int TWH = TW / 2;
+                    f4 ah[TWH][NC];
 #pragma unroll
-                for (int pp = 0; pp < PW; ++pp) {
-                    h8 oh[2];
+                    for (int j = 0; j < TWH; ++j)
 #pragma unroll
-                    for (int v = 0; v < 2; ++v) oh[v] = fload(rso, voff, wz + (((wl * PW + pp) * 2 + v) * 2) * 1024);
+                        for (int c = 0; c < NC; ++c) ah[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
+                    mm_pp<TW, NC, P, PP_G, PP_D, TWH, hf * TWH>(rs1, wz + wbase1, slab, ah, lane, uh);
+                    if constexpr (hf == 0) {
 #pragma unroll
-                    for (int c = 0; c < NC; ++c) {
-                        h8 xh, xl;
-                        epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], f1, Blz + HP, wl * TW + 2 * pp, q, xh, xl);
-#pragma unroll
-                        for (int v = 0; v < 2; ++v) po[v][c] = mfma16(oh[v], xh, po[v][c]);
+                        for (int j = 0; j < PP_D * PP_G; ++j)      // half 1's first units
+                            uh[j] = fload(rs1, voff, wz + wbase1 + (TWH + (j % TWH) + (j / TWH) * TW) * 2048);
+                    } else {
+                        // this wave's slab reads have returned: count it (the group's partials overwrite the
+                        // slab only once all 4 waves have, below)
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        if (lane == 0) __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                }
+#pragma unroll
+                    for (int pp2 = 0; pp2 < PW / 2; ++pp2) {
+                        const int pp = hf * (PW / 2) + pp2;            // this wave's k-step of the output layer
+                        h8 oh[2];
+#pragma unroll
+                        for (int v = 0; v < 2; ++v)
+                            oh[v] = fload(rso, voff, wz + (((wl * PW + pp) * 2 + v) * 2) * 1024);
+#pragma unroll
+                        for (int c = 0; c < NC; ++c) {
+                            h8 xh, xl;
+                            epi_pair(ah[2 * pp2][c], ah[2 * pp2 + 1][c], f1, Blz + HP, wl * TW + 2 * pp, q, xh, xl);
+#pragma unroll
+                            for (int v = 0; v < 2; ++v) po[v][c] = mfma16(oh[v], xh, po[v][c]);
+                        }
+                    }
+                };
+                half(std::integral_constant<int, 0>{});
+                half(std::integral_constant<int, 1>{});
+                X3_ST(3);
                 X3_ST(4);
                 // every wave of the group has finished reading the slab (by now the others are normally long
                 // past their MFMAs)
