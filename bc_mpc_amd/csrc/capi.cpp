@@ -1796,9 +1796,13 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
 // (2^18 with the pre-draw worker measured worse at cfg1's 180k words back to back: the kernel's own reads of
 // 720 KB of rows over the bus, +30 us -- profiles/r03_dropin_zc_bound_ab.txt; draws whose rows are not read,
 // the stochastic policy's, take the host path at any size: only NumPy's state advances)
-static int64_t mt_zero_copy_words() {
+// (round 4: the next call's rows are drawn from the moment this call's rollout is launched, so a team
+//  engine -- whose grid leaves no CUs for a device draw beside it -- draws up to 2^18 words on the host:
+//  cfg1's 180k-word draw overlaps the previous rollout; tools/dropin_zc_ab.py)
+static int64_t mt_zero_copy_words(const bcmpc_engine* e) {
     const char* v = std::getenv("BCMPC_MT_ZC_WORDS");
-    return (v && *v) ? std::max<int64_t>(0, std::atoll(v)) : int64_t(1) << 16;
+    if (v && *v) return std::max<int64_t>(0, std::atoll(v));
+    return e->kernel == BCMPC_KERNEL_TEAM && mt_predraw_enabled() ? int64_t(1) << 18 : int64_t(1) << 16;
 }
 
 static bool mt_device_path() {
@@ -2013,7 +2017,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
     // MPCcontrollerPolicyNet with self_exp=True draws its exploration array (controllers.py:191) but rolls out
     // the policy's own samples (:202-203): only NumPy's state has to advance, no row is read
     const bool rows_needed = !(e->PL > 0 && c.policy_mode == BCMPC_POLICY_STOCHASTIC);
-    if ((draw_words <= mt_zero_copy_words() || !rows_needed) && mt_device_path()) {
+    if ((draw_words <= mt_zero_copy_words(e) || !rows_needed) && mt_device_path()) {
         // small draw: the host generates the shard's rows of every step into pinned memory (the
         // reference's own draw order), the kernel reads them in place; state in the kernel
         // arguments, result into mapped memory, one spin -- no copy either way
@@ -2115,6 +2119,15 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
                               lean ? e->d_result_map : e->d_result, e->stream, nullptr, true, nullptr,
                               lean ? state : nullptr);
         e->rows_wait_seq = 0;
+        // the next call's rows start at once, while this call's rollout runs (round 4; the worker is idle
+        // here unless this call claimed its in-flight job late).  They start from NumPy's state after this
+        // call's draw: a rerun on the fallback engine consumes the same draw, and a call that fails leaves
+        // NumPy's state unadvanced, so the next call misses them (same_job) and draws afresh
+        const bool posted_early = predraw && !late && rc == BCMPC_OK;
+        if (posted_early) {
+            e->zc_last = b;
+            predraw_post(e, g, low, high, A, k_global, cand_offset, rows_needed);
+        }
         const bool spin = e->want_done && rc == BCMPC_OK;
         e->want_done = false;
         if (rc == BCMPC_OK && !lean &&
@@ -2148,7 +2161,7 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         *mt_pos = g.pos;
         *out = lean ? *e->h_result_map : *e->h_result;
         e->zc_last = b;
-        if (predraw) predraw_post(e, g, low, high, A, k_global, cand_offset, rows_needed);   // the next call's rows
+        if (predraw && !posted_early) predraw_post(e, g, low, high, A, k_global, cand_offset, rows_needed);
         return BCMPC_OK;
     }
     if (mt_device_path()) {
