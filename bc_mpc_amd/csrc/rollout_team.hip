@@ -963,50 +963,76 @@ void rollout_team(const RolloutArgs a) {
                     tot[(tm * 2 + 0) * 64 + lane] = mp[0];
                     tot[(tm * 2 + 1) * 64 + lane] = mp[1];
                 }
-                // member (tm + o) % T is collected by wave o % NWV
+                // member (tm + o) % T is collected by wave o % NWV; a wave with several members polls them
+                // together (round 4: one round trip for all of them, not one after the other)
+                constexpr int MO = (T - 1 + NWV - 1) / NWV;   // members per collecting wave (at most)
+                f4 got[MO][2];
+                bool have[MO];
+                const gu64* srcs[MO];
+                int tsrc[MO];
 #pragma unroll
-                for (int o = 1; o < T; ++o) {
-                    if (o % NWV != w) continue;
-                    const int t = (tm + o) % T;
-                    const gu64* const src = gb + (slot + t) * 512;
-                    f4 got[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
-                    for (int spins = 0; !dead; ++spins) {
+                for (int i = 0; i < MO; ++i) {
+                    const int o = (w == 0 ? NWV : w) + i * NWV;  // o in [1, T), o % NWV == w
+                    have[i] = !(o < T);                            // (no such member: nothing to collect)
+                    tsrc[i] = (tm + (o < T ? o : 0)) % T;
+                    srcs[i] = gb + (slot + tsrc[i]) * 512;
+                    got[i][0] = got[i][1] = (f4){0.f, 0.f, 0.f, 0.f};
+                }
+                bool all_have = true;
+#pragma unroll
+                for (int i = 0; i < MO; ++i) all_have = all_have && have[i];
+                for (int spins = 0; !dead && !all_have; ++spins) {
+                    all_have = true;
+#pragma unroll
+                    for (int i = 0; i < MO; ++i) {
+                        if (have[i]) continue;
                         bool ok = true;
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
                             if (xrow(16 * (k >> 2) + 4 * q + (k & 3))) {
                                 const unsigned long long xv =
-                                    __hip_atomic_load(src + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                got[k >> 2][k & 3] = __uint_as_float((unsigned)xv);
+                                    __hip_atomic_load(srcs[i] + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                got[i][k >> 2][k & 3] = __uint_as_float((unsigned)xv);
                                 ok &= (unsigned)(xv >> 32) == ep;
                             }
-                        if (__all(ok)) break;
-                        // (off the success path: every 32nd failed poll looks for a dead tag in row 0)
-                        bool gone = false;
-                        if ((spins & 31) == 31)
-                            gone = (unsigned)(__hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
-                                              32) == dep;
-                        if (__any(gone) || spins >= spin_limit) {
-                            // give up: raise the mapped error word (the host reruns the call on its fallback
-                            // engine), tell this member's other waves (LDS) and the team (dead tags)
-                            dead = true;
-                            if (lane == 0) {
-                                *tdead = 1;
-                                if (a.team_err)
-                                    __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            }
-                            // (granule row k = 0 of both parities: every poller reads it, rows 4q < R)
-                            gu64* const mine = gb + ((size_t)col * 2 * T + tm) * 512 + lane;
-                            __hip_atomic_store(mine, (unsigned long long)dep << 32, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                            __hip_atomic_store(mine + (size_t)T * 512, (unsigned long long)dep << 32,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
+                        have[i] = __all(ok);
+                        all_have = all_have && have[i];
                     }
-                    tot[(t * 2 + 0) * 64 + lane] = got[0];
-                    tot[(t * 2 + 1) * 64 + lane] = got[1];
+                    if (all_have) break;
+                    // (off the success path: every 32nd failed poll looks for a dead tag in row 0)
+                    bool gone = false;
+                    if ((spins & 31) == 31)
+#pragma unroll
+                        for (int i = 0; i < MO; ++i)
+                            if (!have[i])
+                                gone = gone || (unsigned)(__hip_atomic_load(srcs[i] + lane, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT) >> 32) == dep;
+                    if (__any(gone) || spins >= spin_limit) {
+                        // give up: raise the mapped error word (the host reruns the call on its fallback
+                        // engine), tell this member's other waves (LDS) and the team (dead tags)
+                        dead = true;
+                        if (lane == 0) {
+                            *tdead = 1;
+                            if (a.team_err)
+                                __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        }
+                        // (granule row k = 0 of both parities: every poller reads it, rows 4q < R)
+                        gu64* const mine = gb + ((size_t)col * 2 * T + tm) * 512 + lane;
+                        __hip_atomic_store(mine, (unsigned long long)dep << 32, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(mine + (size_t)T * 512, (unsigned long long)dep << 32,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+#pragma unroll
+                for (int i = 0; i < MO; ++i) {
+                    const int o = (w == 0 ? NWV : w) + i * NWV;
+                    if (o < T) {
+                        tot[(tsrc[i] * 2 + 0) * 64 + lane] = got[i][0];
+                        tot[(tsrc[i] * 2 + 1) * 64 + lane] = got[i][1];
+                    }
                 }
                 lds_barrier();                               // every member's partial in LDS
                 dead = dead || *tdead != 0;
