@@ -1298,6 +1298,20 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 #ifndef PP_D
 #define PP_D 2
 #endif
+// wave priority per segment (s_setprio): the group in its latency-bound C segment ahead of the group in its
+// MFMA segment (without it the arbiter's age order favours group 0 in both of its segments and group 1's
+// C stretches the interval: stamps, profiles/r04_pp_stamps.log)
+#ifndef PP_PRIO_C
+#define PP_PRIO_C 2
+#endif
+#ifndef PP_PRIO_ME
+#define PP_PRIO_ME 0
+#endif
+// byte offset of operand j of mm_pp's first units (unit j / PP_G: k-step u / NG, tile group u % NG of the half
+// [T0, T0 + TWH); the order mm_pp loads them in)
+__device__ __forceinline__ constexpr int pp_unit_off(int j, int T0, int TW, int TWH) {
+    return ((j / PP_G) / (TWH / PP_G)) * TW * 2048 + (T0 + ((j / PP_G) % (TWH / PP_G)) * PP_G + j % PP_G) * 2048;
+}
 template <int TW, int NC, int P, int PG, int PD, int TWH = TW, int T0 = 0>
 __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TWH][NC],
                                       int lane, const h8 (&s0)[PD * PG]) {
@@ -1338,7 +1352,7 @@ void rollout_pp(const RolloutArgs a) {
     constexpr int TW = T / 4, PW = TW / 2;        // per wave (4 waves per group)
     constexpr int CB = 16 * NC;                   // candidates per group
     static_assert(T == 32 && TW == 8 && PW == 4, "hidden 512");
-    static_assert(PP_D * PP_G <= TW / 2, "the prefetched first units lie in k-step 0 of a tile half");
+    static_assert(PP_D <= P * (TW / 2 / PP_G) && (TW / 2) % PP_G == 0, "prefetch within one tile half's units");
     extern __shared__ __attribute__((aligned(16))) f4 lds[];
 
     const int lane = threadIdx.x & 63;
@@ -1458,6 +1472,7 @@ void rollout_pp(const RolloutArgs a) {
             const int h = seg >> 1;
             if ((seg & 1) == 0) {
                 // ---------------- C(h) ----------------
+                __builtin_amdgcn_s_setprio(PP_PRIO_C);
                 // this wave's layer-0 fragments, in flight through the owner phase
                 h8 a0[TW];
 #pragma unroll
@@ -1551,8 +1566,8 @@ void rollout_pp(const RolloutArgs a) {
                         for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0[j], b0[c], z4);
                     // ME's first operand units, in flight through the tanh below and the barrier
 #pragma unroll
-                    for (int j = 0; j < PP_D * PP_G; ++j)          // (units 0..PP_D-1: k-step 0 onwards)
-                        uh[j] = fload(rs1, voff, wz + wbase1 + ((j / TW) * TW + (j % TW)) * 2048);
+                    for (int j = 0; j < PP_D * PP_G; ++j)          // (units 0..PP_D-1 of tile half 0)
+                        uh[j] = fload(rs1, voff, wz + wbase1 + pp_unit_off(j, 0, TW, TW / 2));
                     // tanh, this wave's 4 k-steps of the hidden-layer slab (all 4 columns)
 #pragma unroll
                     for (int pp = 0; pp < PW; ++pp)
@@ -1567,6 +1582,7 @@ void rollout_pp(const RolloutArgs a) {
                 X3_ST(2);
             } else {
                 // ---------------- ME(h): the hidden layer's MFMAs, its tanh, the output layer ----------------
+                __builtin_amdgcn_s_setprio(PP_PRIO_ME);
                 f4 po[2][NC];
 #pragma unroll
                 for (int v = 0; v < 2; ++v)
@@ -1587,7 +1603,7 @@ void rollout_pp(const RolloutArgs a) {
                     if constexpr (hf == 0) {
 #pragma unroll
                         for (int j = 0; j < PP_D * PP_G; ++j)      // half 1's first units
-                            uh[j] = fload(rs1, voff, wz + wbase1 + (TWH + (j % TWH) + (j / TWH) * TW) * 2048);
+                            uh[j] = fload(rs1, voff, wz + wbase1 + pp_unit_off(j, TWH, TW, TWH));
                     } else {
                         // this wave's slab reads have returned: count it (the group's partials overwrite the
                         // slab only once all 4 waves have, below)
