@@ -494,8 +494,13 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
             const char* en = std::getenv("BCMPC_F16_NC");
             const char* ew = std::getenv("BCMPC_F16_NW");
             const char* ep = std::getenv("BCMPC_F16_PP");
-            if (ep && ep[0] == '1' && !(en && *en) && !(ew && *ew) &&
-                x3_pp_ok(e->HP, c.n_layers, c.state_dim, c.action_dim) && cols >= 8) {
+            // (default at large K, where it measured ahead of the two-group 4x4 layout below on every box:
+            //  0.835-0.848 vs 0.898-0.900 ms at cfg3, profiles/r04_pp_ab.jsonl; BCMPC_F16_PP=1 forces it at any
+            //  K, =0 turns it off)
+            const bool pp_env = ep && *ep;
+            if (!(en && *en) && !(ew && *ew) && x3_pp_ok(e->HP, c.n_layers, c.state_dim, c.action_dim) &&
+                !reward && e->PL == 0 && c.activation == BCMPC_ACT_TANH && !c.layer_norm &&
+                (pp_env ? ep[0] == '1' && cols >= 8 : cols >= 4 * 512)) {
                 // the two-group pipelined kernel (rollout_pp): 128 candidates per workgroup, 4 waves per
                 // group own 8 hidden tiles each (weights packed 8 tiles per wave)
                 e->pp = true;
@@ -1796,13 +1801,14 @@ static void predraw_post(bcmpc_engine* e, const Mt19937& from, const double* low
 // (2^18 with the pre-draw worker measured worse at cfg1's 180k words back to back: the kernel's own reads of
 // 720 KB of rows over the bus, +30 us -- profiles/r03_dropin_zc_bound_ab.txt; draws whose rows are not read,
 // the stochastic policy's, take the host path at any size: only NumPy's state advances)
-// (round 4: the next call's rows are drawn from the moment this call's rollout is launched, so a team
-//  engine -- whose grid leaves no CUs for a device draw beside it -- draws up to 2^18 words on the host:
-//  cfg1's 180k-word draw overlaps the previous rollout; tools/dropin_zc_ab.py)
-static int64_t mt_zero_copy_words(const bcmpc_engine* e) {
+// (round 4: the next call's rows are drawn from the moment this call's rollout is launched.  Taking cfg1's
+//  180k-word draw on the host that way measured worse back to back than the device draw -- 0.234 vs 0.197 ms,
+//  the host draw outlasts the 0.14-ms rollout it overlaps -- and equal with host work between calls:
+//  profiles/r04_dropin_zc_ab.jsonl; the bound stays 2^16)
+static int64_t mt_zero_copy_words(const bcmpc_engine*) {
     const char* v = std::getenv("BCMPC_MT_ZC_WORDS");
     if (v && *v) return std::max<int64_t>(0, std::atoll(v));
-    return e->kernel == BCMPC_KERNEL_TEAM && mt_predraw_enabled() ? int64_t(1) << 18 : int64_t(1) << 16;
+    return int64_t(1) << 16;
 }
 
 static bool mt_device_path() {

@@ -1298,14 +1298,15 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 #ifndef PP_D
 #define PP_D 2
 #endif
-// wave priority per segment (s_setprio): the group in its latency-bound C segment ahead of the group in its
-// MFMA segment (without it the arbiter's age order favours group 0 in both of its segments and group 1's
-// C stretches the interval: stamps, profiles/r04_pp_stamps.log)
+// wave priority per segment (s_setprio).  Without it the arbiter's age order favours group 0 in both of its
+// segments (stamps: group 1's C segment 20k ticks, group 0's 13.7k; profiles/r04_pp_stamps.log).  C ahead
+// of ME evens the groups out (profiles/r04_ppprio_stamps.log) but the interval stays bound by ME; ME ahead
+// measured best by 1-2% (profiles/r04_ppprio_ab.jsonl: 0.860-0.867 vs 0.876-0.887 ms C-first, 0.867-0.873 none)
 #ifndef PP_PRIO_C
-#define PP_PRIO_C 2
+#define PP_PRIO_C 0
 #endif
 #ifndef PP_PRIO_ME
-#define PP_PRIO_ME 0
+#define PP_PRIO_ME 2
 #endif
 // byte offset of operand j of mm_pp's first units (unit j / PP_G: k-step u / NG, tile group u % NG of the half
 // [T0, T0 + TWH); the order mm_pp loads them in)
