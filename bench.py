@@ -349,13 +349,26 @@ def make_engine(wl, prob, device, precision):
 SMALL_K = ("ppo_defaults", "ppo_mpc_default", "runsh_recipe", "cfg1")
 
 
-def roofline_line(K, H, fpcs, kernel_ms, precision, iters=1):
+def pmc_traffic(key):
+    """HBM bytes per launch measured by the PMC passes of this round (profiles/TRAFFIC_FILE), or None."""
+    try:
+        tr = json.load(open(os.path.join(REPO, "profiles", TRAFFIC_FILE))).get(key)
+        return tr["hbm_bytes_per_launch"] if tr else None
+    except Exception:
+        return None
+
+
+def roofline_line(K, H, fpcs, kernel_ms, precision, iters=1, traffic_key=None):
     """The MFMA roofline of one launch: algorithmic FLOPs (K x H x flop_per_cand_step) / HIP-event kernel
     time, against the peak of the precision the engine computes in."""
     peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16": F16_MFMA_PEAK_TFLOPS}.get(precision, SPLIT_PEAK_TFLOPS)
     tf = K * H * iters * fpcs / (kernel_ms / 1e3) / 1e12
-    return {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s", "frac": tf / peak,
-            "flop_per_launch": K * H * iters * fpcs}
+    out = {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s", "frac": tf / peak,
+           "flop_per_launch": K * H * iters * fpcs}
+    if traffic_key:
+        out["traffic"] = pmc_traffic(traffic_key)
+        out["traffic_source"] = f"profiles/{TRAFFIC_FILE} [{traffic_key}]"
+    return out
 
 
 def oracle_weights(prob, wl):
@@ -394,7 +407,8 @@ def cfg2_line(device, calls=100, warmup=10, cpu_seconds=4.0, dropin_calls=20, wi
     row = {"K": wl["K"], "H": wl["H"], "kernel": eng.info()["kernel"], "precision": eng.precision,
            "value": wl["K"] * wl["H"] / float(np.median(ts)), "unit": "candidate-steps/s",
            "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
-           "roofline": roofline_line(wl["K"], wl["H"], fpcs, float(np.mean(ks)), eng.precision)}
+           "roofline": roofline_line(wl["K"], wl["H"], fpcs, float(np.mean(ks)), eng.precision,
+                                     traffic_key="cfg2:split:device" if eng.precision == "split" else None)}
     eng.close()
     if dropin_calls:
         d = dropin_parity_p50(wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"], False, prob["kernels"],
@@ -467,7 +481,7 @@ def small_k_lines(device, calls=200, warmup=20, cpu_seconds=3.0, with_cpu=True):
     return out
 
 
-def f16_line(wl, prob, device, steps=50, warmup=5):
+def f16_line(wl, prob, device, steps=50, warmup=5, name="cfg3"):
     """BASELINE configs[2] as it is worded ("bf16 MFMA GEMM + fp32 cost accumulate"): the same complete
     get_action with the single-pass f16 engine (precision "f16"; f16's 11-bit significand,
     f32 accumulate, f64 state and cost).  Not `value`: its costs meet the f16 bar of tests/test_gpu_f16.py,
@@ -497,11 +511,24 @@ def f16_line(wl, prob, device, steps=50, warmup=5):
     eng.close()
     fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
     tf = K * H * fpcs / (float(np.mean(ks)) / 1e3) / 1e12
+    # the layout capi.cpp picks for this shape (the pipelined kernel at >= 2048 columns, BCMPC_F16_PP=0 off)
+    pp = (os.environ.get("BCMPC_F16_PP", "") != "0" and not os.environ.get("BCMPC_F16_NC")
+          and not os.environ.get("BCMPC_F16_NW") and wl["hidden"] in range(497, 513) and wl["L"] == 2
+          and wl.get("act", "tanh") == "tanh" and K >= 2048 * 16)
+    layout = ("rollout_pp<512> (two 64-candidate groups per workgroup, software-pipelined)" if pp
+              else f"rollout_x3 single-pass ({kern})")
+    traffic = None
+    try:
+        tr = json.load(open(os.path.join(REPO, "profiles", TRAFFIC_FILE))).get(f"{name}:f16:device")
+        traffic = tr["hbm_bytes_per_launch"] if tr and pp else None
+    except Exception:
+        pass
     return {"precision": "f16 (one v_mfma_f32_16x16x32_f16 pass, f32 accumulate; f64 state / cost)",
-            "kernel": kern, "value": K * H / float(np.mean(ts)), "unit": "candidate-steps/s",
+            "kernel": kern, "layout": layout, "value": K * H / float(np.mean(ts)), "unit": "candidate-steps/s",
             "p50_ms": float(np.percentile(ts, 50) * 1e3), "kernel_ms_avg": float(np.mean(ks)),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tf / F16_MFMA_PEAK_TFLOPS},
+                         "frac": tf / F16_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_source": f"profiles/{TRAFFIC_FILE}"},
             "argmin_agreement": {"seeds": 16, "top1_equal": agree,
                                  "reference": "the split (f32-grade) engine's argmin on the same actions",
                                  "regret_median": float(np.median(regret)), "regret_max": float(np.max(regret)),
@@ -750,7 +777,7 @@ def main():
         out["cfg2"] = cfg2_line(local, with_cpu=not args.no_cpu_baseline)
     if (rank == 0 and world == 1 and not args.no_f16 and not (cem or policy or reward or ln) and act == "tanh"
             and eng.precision != "f16"):
-        out["f16_single_pass"] = f16_line(wl, prob, local)
+        out["f16_single_pass"] = f16_line(wl, prob, local, name=args.workload)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if lib_comm is not None:

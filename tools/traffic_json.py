@@ -65,8 +65,19 @@ def main():
           "actions read from HBM (61440 KB tensor) + weights + costs; WRITE_SIZE pass taken in device mode")
     entry("cfg3:split:device", "fetch_dev", "write_dev", W_SPLIT, K3 * 8,
           "device-RNG actions: packed weights (each XCD misses them into its own L2) + the cost vector")
-    entry("cfg3:f16:device", "f16_fetch_dev", "f16_write_dev", W_F16, K3 * 8,
-          "single-pass f16: hi fragments only")
+    entry("cfg3:f16_4x4:device", "f16_fetch_dev", "f16_write_dev", W_F16, K3 * 8,
+          "single-pass f16, the 4x4 two-workgroup layout (default until the pipelined kernel): it spills 66 "
+          "VGPRs at its 256-register cap, WRITE_SIZE is its scratch")
+    # the pipelined kernel (rollout_pp, f16 default at large K), PMC passes of tools/r04_final.sh
+    global SRC
+    src0 = SRC
+    SRC = os.path.join(os.path.dirname(src0), "r04_pmc_f16")
+    entry("cfg3:f16:device", "fetch_pp", "write_pp", W_F16, K3 * 8,
+          "single-pass f16, rollout_pp (two 64-candidate groups per workgroup, spill-free): hi fragments only")
+    if "cfg3:f16:device" in res:
+        res["cfg3:f16:device"]["source"] = res["cfg3:f16:device"]["source"].replace("r04_traffic/", "r04_pmc_f16/") \
+            .replace("tools/r04_traffic.sh", "tools/r04_final.sh")
+    SRC = src0
     entry("cfg2:split:device", "cfg2_fetch_dev", "cfg2_write_dev", W_SPLIT, 4096 * 8,
           "cfg2 K=4096: 256 columns, one per CU")
     if "cfg3:split" in res and "cfg3:split:device" in res:
