@@ -1426,6 +1426,14 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             HIP_TRY(hipStreamSynchronize(st));
             const char* names[10] = {"tail", "fill", "l0in", "layer0", "slabbar", "l1mm", "l1epi", "out+bar",
                                      "xchg", "prologue"};
+            if (const char* dump = std::getenv("BCMPC_STAMP_DUMP")) {   // raw [blocks][waves][10] records
+                if (FILE* f = std::fopen(dump, "ab")) {
+                    const int32_t hdr[4] = {(int32_t)blocks, (int32_t)nwv, c.horizon, (int32_t)c.num_paths};
+                    std::fwrite(hdr, sizeof(hdr), 1, f);
+                    std::fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+                    std::fclose(f);
+                }
+            }
             std::fprintf(stderr, "team stamps (per step, s_memtime ticks; wave 0 | others):");
             for (int k = 0; k < 10; ++k) {
                 double s0 = 0, s1 = 0;

@@ -305,6 +305,15 @@ void rollout_team(const RolloutArgs a) {
             tp_ = t_;
         }
     };
+    // TEAM_STAMP 3: s_memrealtime (100 MHz, one clock for the whole chip) at five points of the exchange of
+    // steps H/2 and H/2 + 1 (slots 5 k + 0 partials done, 1 published, 2 this wave's members in, 3 every member
+    // in, 4 totals): member skew and hand-off latency (BCMPC_STAMP_DUMP writes the raw records)
+    auto rstamp = [&](int h, int k) __attribute__((always_inline)) {
+        if constexpr (TEAM_STAMP == 3) {
+            const int d = h - a.H / 2;
+            if (d == 0 || d == 1) ph_[5 * d + k] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
     unsigned gen = 0;
     if constexpr (T > 1) gen = __hip_atomic_load(a.team_ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
@@ -332,43 +341,123 @@ void rollout_team(const RolloutArgs a) {
         const char* const plw = base + off + (PHP > 0 ? pol_param_bytes(a.pL, PHP) : 0);   // policy weights
         double* const pdraw = reinterpret_cast<double*>(const_cast<char*>(plw));  // (offset by pw_total below)
 
-        for (int i = threadIdx.x; i < kConstRows * kConstCols; i += blockDim.x) C[i] = a.consts[i];
-        for (int l = 0; l < NB; ++l)
-            for (int i = threadIdx.x; i < HP; i += blockDim.x) Bl[l * HP + i] = a.b[l][i] * kAct;
-        for (int i = threadIdx.x; i < 32; i += blockDim.x) Bl[NB * HP + i] = a.b[NB][i];
+        // Parameters into LDS.  Every load is issued before the first LDS store (register batches with
+        // compile-time trip counts): a load -> wait -> store loop per array paid one global round trip per
+        // array and pass, ~3 us of the prologue at K = 400 (TEAM_STAMP 2, profiles/r02c_team_prologue_stamps.txt)
+        // and one per 4-KB pass of the policy's hidden weights (16 at 2x128)
+        constexpr int BS = 64 * NWV;
+        constexpr int NCn = (kConstRows * kConstCols + BS - 1) / BS, NHn = (HP + BS - 1) / BS;
         int pw_total = 0;                                 // policy: every layer's packed bytes, copied once
         if constexpr (PHP > 0) {
             for (int l = 1; l < a.pL; ++l) pw_total += a.pwbytes[l];
-            for (int l = 0; l < a.pL; ++l)
-                for (int i = threadIdx.x; i < PHP; i += blockDim.x) Pb[l * PHP + i] = a.pb[l][i] * kTanhK;
-            for (int i = threadIdx.x; i < kPolParams; i += blockDim.x) Pb[a.pL * PHP + i] = a.pparams[i];
-            const f4* src = a.pw[1];                      // hidden layers 1..pL-1 (contiguous, capi.cpp pw_off)
-            for (int i = threadIdx.x; i < pw_total / 16; i += blockDim.x)
-                reinterpret_cast<f4*>(const_cast<char*>(plw))[i] = src[i];
+            // the policy's hidden layers 1..pL-1 (contiguous, capi.cpp pw_off): 16 f4 per thread in flight
+            const f4* src = a.pw[1];
+            f4* const dst = reinterpret_cast<f4*>(const_cast<char*>(plw));
+            const int n4 = pw_total / 16;
+            for (int i0 = threadIdx.x; i0 < n4; i0 += 16 * BS) {
+                f4 r[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (i0 + u * BS < n4) r[u] = src[i0 + u * BS];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (i0 + u * BS < n4) dst[i0 + u * BS] = r[u];
+            }
         }
-        if constexpr (HLN) {
-            // the trunk's gamma / beta at [0, HP) / [2 HP, 3 HP); [HP, ..): the heads' centring table
-            // head_rs [T][32], then Chan's merge weights (nb / nn, n nb / nn) of the T members in order
-            for (int i = threadIdx.x; i < HP; i += blockDim.x) {
-                lnp[i] = a.lng[0][i];
-                lnp[2 * HP + i] = a.lnb[0][i];
+        {
+            const int t = threadIdx.x;
+            double rc[NCn];
+            float rb[NB][NHn], rbo = 0.f;
+#pragma unroll
+            for (int u = 0; u < NCn; ++u)
+                if (t + u * BS < kConstRows * kConstCols) rc[u] = a.consts[t + u * BS];
+#pragma unroll
+            for (int l = 0; l < NB; ++l)
+#pragma unroll
+                for (int u = 0; u < NHn; ++u)
+                    if (t + u * BS < HP) rb[l][u] = a.b[l][t + u * BS];
+            if (t < 32) rbo = a.b[NB][t];
+            // (LayerNorm: gamma / beta of the trunk, and of layer 1 without the reward net's heads)
+            constexpr int NLN = LNK ? (HLN ? 1 : 2) : 0;
+            float rg[NLN > 0 ? NLN : 1][NHn], rbt[NLN > 0 ? NLN : 1][NHn];
+#pragma unroll
+            for (int l = 0; l < NLN; ++l)
+#pragma unroll
+                for (int u = 0; u < NHn; ++u)
+                    if (t + u * BS < HP) {
+                        rg[l][u] = a.lng[l][t + u * BS];
+                        rbt[l][u] = a.lnb[l][t + u * BS];
+                    }
+            // (policy: biases of its pL <= 3 layers and its parameters)
+            constexpr int NPn = PHP > 0 ? (PHP + BS - 1) / BS : 1, NQn = (kPolParams + BS - 1) / BS;
+            float rpb[3][NPn], rpp[NQn];
+            if constexpr (PHP > 0) {
+#pragma unroll
+                for (int l = 0; l < 3; ++l)
+#pragma unroll
+                    for (int u = 0; u < NPn; ++u)
+                        if (l < a.pL && t + u * BS < PHP) rpb[l][u] = a.pb[l][t + u * BS];
+#pragma unroll
+                for (int u = 0; u < NQn; ++u)
+                    if (t + u * BS < kPolParams) rpp[u] = a.pparams[t + u * BS];
             }
-            for (int i = threadIdx.x; i < T * 32; i += blockDim.x) lnp[HP + i] = a.head_rs[i];
-            if (threadIdx.x == 0) {
-                float n = 0.f;
-                for (int t = 0; t < T; ++t) {
-                    const float nb = (float)min(max(a.hidden - 16 * TPW * NH * t, 0), 16 * TPW * NH), nn = n + nb;
-                    lnp[HP + T * 32 + 2 * t] = nb > 0.f ? nb / nn : 0.f;
-                    lnp[HP + T * 32 + 2 * t + 1] = nb > 0.f ? n * nb / nn : 0.f;
-                    n = nn;
-                }
+            constexpr int NRn = (T * 32 + BS - 1) / BS;
+            float rrs[NRn];
+            if constexpr (HLN)
+#pragma unroll
+                for (int u = 0; u < NRn; ++u)
+                    if (t + u * BS < T * 32) rrs[u] = a.head_rs[t + u * BS];
+            // ---- the stores ----
+#pragma unroll
+            for (int u = 0; u < NCn; ++u)
+                if (t + u * BS < kConstRows * kConstCols) C[t + u * BS] = rc[u];
+#pragma unroll
+            for (int l = 0; l < NB; ++l)
+#pragma unroll
+                for (int u = 0; u < NHn; ++u)
+                    if (t + u * BS < HP) Bl[l * HP + t + u * BS] = rb[l][u] * kAct;
+            if (t < 32) Bl[NB * HP + t] = rbo;
+            if constexpr (PHP > 0) {
+#pragma unroll
+                for (int l = 0; l < 3; ++l)
+#pragma unroll
+                    for (int u = 0; u < NPn; ++u)
+                        if (l < a.pL && t + u * BS < PHP) Pb[l * PHP + t + u * BS] = rpb[l][u] * kTanhK;
+#pragma unroll
+                for (int u = 0; u < NQn; ++u)
+                    if (t + u * BS < kPolParams) Pb[a.pL * PHP + t + u * BS] = rpp[u];
             }
-        } else if constexpr (LNK) {
-            for (int l = 0; l < 2; ++l)
-                for (int i = threadIdx.x; i < HP; i += blockDim.x) {
-                    lnp[l * HP + i] = a.lng[l][i];
-                    lnp[(2 + l) * HP + i] = a.lnb[l][i];
+            if constexpr (HLN) {
+                // the trunk's gamma / beta at [0, HP) / [2 HP, 3 HP); [HP, ..): the heads' centring table
+                // head_rs [T][32], then Chan's merge weights (nb / nn, n nb / nn) of the T members in order
+#pragma unroll
+                for (int u = 0; u < NHn; ++u)
+                    if (t + u * BS < HP) {
+                        lnp[t + u * BS] = rg[0][u];
+                        lnp[2 * HP + t + u * BS] = rbt[0][u];
+                    }
+#pragma unroll
+                for (int u = 0; u < NRn; ++u)
+                    if (t + u * BS < T * 32) lnp[HP + t + u * BS] = rrs[u];
+                if (t == 0) {
+                    float n = 0.f;
+                    for (int tt = 0; tt < T; ++tt) {
+                        const float nb = (float)min(max(a.hidden - 16 * TPW * NH * tt, 0), 16 * TPW * NH), nn = n + nb;
+                        lnp[HP + T * 32 + 2 * tt] = nb > 0.f ? nb / nn : 0.f;
+                        lnp[HP + T * 32 + 2 * tt + 1] = nb > 0.f ? n * nb / nn : 0.f;
+                        n = nn;
+                    }
                 }
+            } else if constexpr (LNK) {
+#pragma unroll
+                for (int l = 0; l < 2; ++l)
+#pragma unroll
+                    for (int u = 0; u < NHn; ++u)
+                        if (t + u * BS < HP) {
+                            lnp[l * HP + t + u * BS] = rg[l][u];
+                            lnp[(2 + l) * HP + t + u * BS] = rbt[l][u];
+                        }
+            }
         }
 
         if constexpr (T > 1)
@@ -920,6 +1009,7 @@ void rollout_team(const RolloutArgs a) {
             parts[(w * 2 + 1) * 64 + lane] = po[1];
             lds_barrier();                                   // partials complete; every wave is done with the slab
             stamp(7);
+            rstamp(h, 0);
             if constexpr (T == 1) {
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
@@ -963,6 +1053,7 @@ void rollout_team(const RolloutArgs a) {
                     tot[(tm * 2 + 0) * 64 + lane] = mp[0];
                     tot[(tm * 2 + 1) * 64 + lane] = mp[1];
                 }
+                rstamp(h, 1);
                 // member (tm + o) % T is collected by wave o % NWV; a wave with several members polls them
                 // together (round 4: one round trip for all of them, not one after the other)
                 constexpr int MO = (T - 1 + NWV - 1) / NWV;   // members per collecting wave (at most)
@@ -1026,6 +1117,7 @@ void rollout_team(const RolloutArgs a) {
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+                rstamp(h, 2);
 #pragma unroll
                 for (int i = 0; i < MO; ++i) {
                     const int o = (w == 0 ? NWV : w) + i * NWV;
@@ -1035,6 +1127,7 @@ void rollout_team(const RolloutArgs a) {
                     }
                 }
                 lds_barrier();                               // every member's partial in LDS
+                rstamp(h, 3);
                 dead = dead || *tdead != 0;
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
@@ -1088,6 +1181,7 @@ void rollout_team(const RolloutArgs a) {
                 }
             }
             stamp(8);
+            rstamp(h, 4);
         }
         if (writer && a.costs && valid && q == qc) a.costs[cand] = cost;
         if (writer && valid && q == qc) mybest = Best{a.amin.maximize ? -cost : cost, cand};
