@@ -1073,19 +1073,30 @@ void rollout_team(const RolloutArgs a) {
 #pragma unroll
                 for (int i = 0; i < MO; ++i) all_have = all_have && have[i];
                 for (int spins = 0; !dead && !all_have; ++spins) {
+                    // one sweep: every granule of every missing member requested before any is tested (loads
+                    // under a per-lane row test were each issued in an exec-masked branch and waited for
+                    // before the next: 8 round trips per member per sweep, ~3 us from the last member's
+                    // publish to every member in, TEAM_STAMP 3).  Granules of rows nobody exchanges are
+                    // read too (in the buffer, never written) and ignored.
+                    unsigned long long xv[MO][8];
+#pragma unroll
+                    for (int i = 0; i < MO; ++i)
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            xv[i][k] = have[i] ? 0ull
+                                               : __hip_atomic_load(srcs[i] + k * 64 + lane, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
                     all_have = true;
 #pragma unroll
                     for (int i = 0; i < MO; ++i) {
                         if (have[i]) continue;
                         bool ok = true;
 #pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            if (xrow(16 * (k >> 2) + 4 * q + (k & 3))) {
-                                const unsigned long long xv =
-                                    __hip_atomic_load(srcs[i] + k * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                got[i][k >> 2][k & 3] = __uint_as_float((unsigned)xv);
-                                ok &= (unsigned)(xv >> 32) == ep;
-                            }
+                        for (int k = 0; k < 8; ++k) {
+                            const bool vr = xrow(16 * (k >> 2) + 4 * q + (k & 3));
+                            got[i][k >> 2][k & 3] = __uint_as_float((unsigned)xv[i][k]);
+                            ok &= !vr || (unsigned)(xv[i][k] >> 32) == ep;
+                        }
                         have[i] = __all(ok);
                         all_have = all_have && have[i];
                     }
