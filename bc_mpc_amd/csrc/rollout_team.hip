@@ -344,7 +344,8 @@ void rollout_team(const RolloutArgs a) {
         // Parameters into LDS.  Every load is issued before the first LDS store (register batches with
         // compile-time trip counts): a load -> wait -> store loop per array paid one global round trip per
         // array and pass, ~3 us of the prologue at K = 400 (TEAM_STAMP 2, profiles/r02c_team_prologue_stamps.txt)
-        // and one per 4-KB pass of the policy's hidden weights (16 at 2x128)
+        // and one per 4-KB pass of the policy's hidden weights (16 at 2x128).  The loads are unconditional
+        // (clamped indices: a load under the same test as its store was fused with it, load -> wait -> store)
         constexpr int BS = 64 * NWV;
         constexpr int NCn = (kConstRows * kConstCols + BS - 1) / BS, NHn = (HP + BS - 1) / BS;
         int pw_total = 0;                                 // policy: every layer's packed bytes, copied once
@@ -370,13 +371,13 @@ void rollout_team(const RolloutArgs a) {
             float rb[NB][NHn], rbo = 0.f;
 #pragma unroll
             for (int u = 0; u < NCn; ++u)
-                if (t + u * BS < kConstRows * kConstCols) rc[u] = a.consts[t + u * BS];
+                rc[u] = a.consts[min(t + u * BS, kConstRows * kConstCols - 1)];
 #pragma unroll
             for (int l = 0; l < NB; ++l)
 #pragma unroll
                 for (int u = 0; u < NHn; ++u)
-                    if (t + u * BS < HP) rb[l][u] = a.b[l][t + u * BS];
-            if (t < 32) rbo = a.b[NB][t];
+                    rb[l][u] = a.b[l][min(t + u * BS, HP - 1)];
+            rbo = a.b[NB][min(t, 31)];
             // (LayerNorm: gamma / beta of the trunk, and of layer 1 without the reward net's heads)
             constexpr int NLN = LNK ? (HLN ? 1 : 2) : 0;
             float rg[NLN > 0 ? NLN : 1][NHn], rbt[NLN > 0 ? NLN : 1][NHn];
@@ -384,9 +385,9 @@ void rollout_team(const RolloutArgs a) {
             for (int l = 0; l < NLN; ++l)
 #pragma unroll
                 for (int u = 0; u < NHn; ++u)
-                    if (t + u * BS < HP) {
-                        rg[l][u] = a.lng[l][t + u * BS];
-                        rbt[l][u] = a.lnb[l][t + u * BS];
+                {
+                        rg[l][u] = a.lng[l][min(t + u * BS, HP - 1)];
+                        rbt[l][u] = a.lnb[l][min(t + u * BS, HP - 1)];
                     }
             // (policy: biases of its pL <= 3 layers and its parameters)
             constexpr int NPn = PHP > 0 ? (PHP + BS - 1) / BS : 1, NQn = (kPolParams + BS - 1) / BS;
@@ -396,17 +397,17 @@ void rollout_team(const RolloutArgs a) {
                 for (int l = 0; l < 3; ++l)
 #pragma unroll
                     for (int u = 0; u < NPn; ++u)
-                        if (l < a.pL && t + u * BS < PHP) rpb[l][u] = a.pb[l][t + u * BS];
+                        rpb[l][u] = a.pb[min(l, a.pL - 1)][min(t + u * BS, PHP - 1)];
 #pragma unroll
                 for (int u = 0; u < NQn; ++u)
-                    if (t + u * BS < kPolParams) rpp[u] = a.pparams[t + u * BS];
+                    rpp[u] = a.pparams[min(t + u * BS, kPolParams - 1)];
             }
             constexpr int NRn = (T * 32 + BS - 1) / BS;
             float rrs[NRn];
             if constexpr (HLN)
 #pragma unroll
                 for (int u = 0; u < NRn; ++u)
-                    if (t + u * BS < T * 32) rrs[u] = a.head_rs[t + u * BS];
+                    rrs[u] = a.head_rs[min(t + u * BS, T * 32 - 1)];
             // ---- the stores ----
 #pragma unroll
             for (int u = 0; u < NCn; ++u)
