@@ -851,24 +851,59 @@ void rollout_x3(const RolloutArgs a) {
         if (owner && !X3_DIAG_NOOWNER) {
             // ---- normalise the state (dynamics.py:109), cast to f32 (TF feed), column max ----
             const float* xr = xa + ((h % NCH) * CB + 16 * cw + m) * A;
+            if constexpr (PHP > 0 || AK != 0 || F1 || HP > 512) {
 #pragma unroll
-            for (int k = 0; k < NHV; ++k)
+                for (int k = 0; k < NHV; ++k)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int d = 16 * (hv0 + k) + 4 * q + r;
-                    float xv = 0.f;
-                    if (d < S) {
-                        xv = (float)div_rn(__dsub_rn(s[k][r], Cv[0 * 32 + d]), Cv[1 * 32 + d], Cv[8 * 32 + d]);
-                    } else if (d < S + A) {
-                        if constexpr (PHP > 0) {              // the policy's action (dynamics.py:110)
-                            const int j = d - S;
-                            xv = (float)div_rn(__dsub_rn(pact[r], Cv[2 * 32 + j]), Cv[3 * 32 + j], Cv[9 * 32 + j]);
-                        } else {
-                            xv = xr[d - S];
+                    for (int r = 0; r < 4; ++r) {
+                        const int d = 16 * (hv0 + k) + 4 * q + r;
+                        float xv = 0.f;
+                        if (d < S) {
+                            xv = (float)div_rn(__dsub_rn(s[k][r], Cv[0 * 32 + d]), Cv[1 * 32 + d], Cv[8 * 32 + d]);
+                        } else if (d < S + A) {
+                            if constexpr (PHP > 0) {              // the policy's action (dynamics.py:110)
+                                const int j = d - S;
+                                xv = (float)div_rn(__dsub_rn(pact[r], Cv[2 * 32 + j]), Cv[3 * 32 + j], Cv[9 * 32 + j]);
+                            } else {
+                                xv = xr[d - S];
+                            }
                         }
+                        xin[4 * k + r] = xv;
                     }
-                    xin[4 * k + r] = xv;
-                }
+            } else {
+                // (branch-free: every slot's operands are requested first -- the constants table has 32
+                //  columns, the action index is clamped -- and each slot picks its value after; per-slot
+                //  branches issued each slot's LDS reads and waited for them before the next slot's.  Only the
+                //  plain tanh split kernels up to hidden 512: the others have no registers to spare -- 2 to 14
+                //  more spilled registers each)
+                double c0[NHV][4], c1[NHV][4], c8[NHV][4];
+                float av[NHV][4];
+#pragma unroll
+                for (int k = 0; k < NHV; ++k)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int d = 16 * (hv0 + k) + 4 * q + r;
+                        c0[k][r] = Cv[0 * 32 + d];
+                        c1[k][r] = Cv[1 * 32 + d];
+                        c8[k][r] = Cv[8 * 32 + d];
+                        av[k][r] = xr[min(max(d - S, 0), A - 1)];
+                    }
+                float xs_[NHV][4];
+#pragma unroll
+                for (int k = 0; k < NHV; ++k)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        xs_[k][r] = (float)div_rn(__dsub_rn(s[k][r], c0[k][r]), c1[k][r], c8[k][r]);
+                        asm volatile("" : "+v"(xs_[k][r]));     // (every lane, every slot: not sunk into a branch)
+                    }
+#pragma unroll
+                for (int k = 0; k < NHV; ++k)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int d = 16 * (hv0 + k) + 4 * q + r;
+                        xin[4 * k + r] = d < S ? xs_[k][r] : (d < S + A ? av[k][r] : 0.f);
+                    }
+            }
 #pragma unroll
             for (int i = 0; i < 4 * NHV; ++i) mx = fmaxf(mx, fabsf(xin[i]));
             mx = max_rows32(max_rows16(mx));
@@ -1123,16 +1158,42 @@ void rollout_x3(const RolloutArgs a) {
             for (int c = 0; c < NC; ++c)
                 if (c == cw) foc = fo * fcol[c];
         }
+        if constexpr (PHP > 0 || AK != 0 || F1 || HP > 512) {
 #pragma unroll
-        for (int k = 0; k < NHV; ++k) {
-            const f4 bv = *reinterpret_cast<const f4*>(Blv + LB * HP + 16 * (hv0 + k) + 4 * q);
+            for (int k = 0; k < NHV; ++k) {
+                const f4 bv = *reinterpret_cast<const f4*>(Blv + LB * HP + 16 * (hv0 + k) + 4 * q);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int d = 16 * (hv0 + k) + 4 * q + r;
-                if (d < S) {
-                    const float dn = fmaf(o[k][r], foc, bv[r]);            // BiasAdd (f32)
-                    const double ud = __dadd_rn(__dmul_rn((double)dn, Cv[5 * 32 + d]), Cv[4 * 32 + d]);
-                    s[k][r] = __dadd_rn(s[k][r], ud);
+                for (int r = 0; r < 4; ++r) {
+                    const int d = 16 * (hv0 + k) + 4 * q + r;
+                    if (d < S) {
+                        const float dn = fmaf(o[k][r], foc, bv[r]);            // BiasAdd (f32)
+                        const double ud = __dadd_rn(__dmul_rn((double)dn, Cv[5 * 32 + d]), Cv[4 * 32 + d]);
+                        s[k][r] = __dadd_rn(s[k][r], ud);
+                    }
+                }
+            }
+        } else {
+            // (branch-free, as the layer-0 input above: the constants of every slot requested first, every
+            //  slot's update computed, the dims < S keep theirs)
+            double c4[NHV][4], c5[NHV][4];
+#pragma unroll
+            for (int k = 0; k < NHV; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int d = 16 * (hv0 + k) + 4 * q + r;
+                    c4[k][r] = Cv[4 * 32 + d];
+                    c5[k][r] = Cv[5 * 32 + d];
+                }
+#pragma unroll
+            for (int k = 0; k < NHV; ++k) {
+                const f4 bv = *reinterpret_cast<const f4*>(Blv + LB * HP + 16 * (hv0 + k) + 4 * q);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int d = 16 * (hv0 + k) + 4 * q + r;
+                    const float dn = fmaf(o[k][r], foc, bv[r]);                // BiasAdd (f32)
+                    double sn = __dadd_rn(s[k][r], __dadd_rn(__dmul_rn((double)dn, c5[k][r]), c4[k][r]));
+                    asm volatile("" : "+v"(sn));
+                    s[k][r] = d < S ? sn : s[k][r];
                 }
             }
         }
