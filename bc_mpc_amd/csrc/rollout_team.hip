@@ -800,20 +800,37 @@ void rollout_team(const RolloutArgs a) {
                 for (int x = 1; x < NWV; ++x) o += pparts[x * 64 + lane];   // fixed summation order
                 const float fo_p = a.pwinv[a.pL];
                 const double* const dr = pdr + ((h % kPolNch) * 16 + m) * 16;
+                // (branch-free over the 4 rows: every row's LDS operands requested first -- the action index
+                //  clamped -- and rows outside [S, S + A) drop their value after; per-row branches issued each
+                //  row's reads and waited for them before the next row's)
+                float pb_[4], ls_[4];
+                double dr_[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int j = 16 + 4 * q + r - S;
-                    if (j < 0 || j >= A) continue;
-                    const float mean = o[r] * fo_p + pm[80 + 4 * q + r];       // dense bias (f32)
+                    const int jc = min(max(16 + 4 * q + r - S, 0), A - 1);
+                    pb_[r] = pm[80 + 4 * q + r];
+                    ls_[r] = pm[64 + jc];
+                    dr_[r] = dr[jc];
+                }
+                double pv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float mean = o[r] * fo_p + pb_[r];                    // dense bias (f32)
                     if (a.pol_mode == BCMPC_POLICY_STOCHASTIC) {
-                        const float sd = expf(pm[64 + j]);
-                        pact[r] = (double)(mean + sd * (float)dr[j]);
+                        pv[r] = (double)(mean + expf(ls_[r]) * (float)dr_[r]);
                     } else {
                         // (1 - explore) * mean in f32 (NumPy keeps the f32 dtype), + explore * U in f64
                         const float t1 = (float)(1.0 - a.explore) * mean;
-                        pact[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, dr[j]));
+                        pv[r] = __dadd_rn((double)t1, __dmul_rn(a.explore, dr_[r]));
                     }
-                    if (writer && a.act_out && h < a.act_out_steps && valid)   // action_paths (controllers.py:213)
+                    asm volatile("" : "+v"(pv[r]));
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 + 4 * q + r - S;
+                    const bool in = j >= 0 && j < A;
+                    pact[r] = in ? pv[r] : 0.0;
+                    if (in && writer && a.act_out && h < a.act_out_steps && valid)   // action_paths (controllers.py:213)
                         __hip_atomic_store(&a.act_out[((int64_t)h * a.K + cand) * A + j], pact[r], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
