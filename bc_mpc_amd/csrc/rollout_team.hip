@@ -98,6 +98,21 @@ __device__ __forceinline__ float tanh4096(float z) {     // tanh(y) * 2^12 from 
 
 __host__ __device__ constexpr int team_wpe(int NWV) { return NWV >= 8 ? 2 : 1; }
 
+// The LDS constants table behind a compiler-opaque value, so the step loop re-reads it instead of hoisting
+// it into registers: an opaque zero offset (keeps the LDS address space: ds_read), or (PTR) an opaque
+// pointer (generic: flat loads; fewer live registers in the kernels that have none to spare)
+template <bool PTR>
+__device__ __forceinline__ const double* team_opaque_lds(const double* C) {
+    if constexpr (PTR) {
+        asm volatile("" : "+v"(C));
+        return C;
+    } else {
+        int cz = 0;
+        asm volatile("" : "+s"(cz));
+        return C + cz;
+    }
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // global loads (a __syncthreads() fence drains vmcnt too, which would hold every barrier of the
 // first step behind the weight prologue's ~80 loads per wave).  Every hand-off between waves in
@@ -262,6 +277,7 @@ void rollout_team(const RolloutArgs a) {
     // whose per-member statistics ride along with the output partials (below)
     static_assert(!LNK || T == 1 || RW, "LayerNorm geometry");
     constexpr bool HLN = RW && LNK;                     // the reward net's LayerNorm heads (dynamics.py:165-177)
+    constexpr bool OPQ_PTR = RW || (PHP > 0 && HP > 256);   // (team_opaque_lds)
     // fused policy (MPCcontrollerPolicyNet, ppo_bc_policy.py:54-88): each wave owns one policy tile
     // pair; it shares the dynamics slab (free once the step's partials barrier has passed) and, when
     // a team barrier ends the step (T > 1), the partials buffer; at T == 1 waves may still be summing
@@ -660,10 +676,12 @@ void rollout_team(const RolloutArgs a) {
                 // (branch-free: dims >= S carry the padded constants -- mean 0, std 0 -- and are never read)
                 f4 bv[2];
                 double c4[2][4], c5[2][4];
-                // (the constants are re-read from LDS every step: an opaque base keeps the compiler from
-                //  hoisting 40 doubles per lane out of the step loop, registers the resident weights need)
-                const double* Cs = C;
-                asm volatile("" : "+v"(Cs));
+                // (the constants are re-read from LDS every step: an opaque offset keeps the compiler from
+                //  hoisting 40 doubles per lane out of the step loop, registers the resident weights need.
+                //  An offset, not an opaque pointer: that lost the LDS address space -- flat loads)
+                //  (Kept an opaque pointer in the 512-wide policy / reward-net kernels: the LDS-addressed
+                //  form spilled 9-12 more registers there, run.sh recipe +12.6 us)
+                const double* Cs = team_opaque_lds<OPQ_PTR>(C);
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
                     bv[v] = *reinterpret_cast<const f4*>(Bout + 16 * v + 4 * q);
@@ -846,8 +864,7 @@ void rollout_team(const RolloutArgs a) {
                 const float* const xr = xas + ((h % kTeamNch) * 16 + m) * 16;
                 double c0[2][4], c1[2][4], c8[2][4];
                 float av[2][4];
-                const double* Cs = C;
-                asm volatile("" : "+v"(Cs));
+                const double* Cs = team_opaque_lds<OPQ_PTR>(C);     // (as in the tail)
 #pragma unroll
                 for (int v = 0; v < 2; ++v)
 #pragma unroll
@@ -856,7 +873,14 @@ void rollout_team(const RolloutArgs a) {
                         c0[v][r] = Cs[0 * 32 + d];
                         c1[v][r] = Cs[1 * 32 + d];
                         c8[v][r] = Cs[8 * 32 + d];
-                        if constexpr (PHP > 0) {              // the policy's action (dynamics.py:110)
+                        if constexpr (PHP > 0 && !OPQ_PTR) {  // the policy's action (dynamics.py:110)
+                            // (computed in every lane and kept only in the action rows: a per-row branch
+                            //  waited for each row's LDS constants before the next row's)
+                            const int j = min(max(d - S, 0), A - 1);
+                            float an = (float)div_rn(__dsub_rn(pact[r], Cs[2 * 32 + j]), Cs[3 * 32 + j], Cs[9 * 32 + j]);
+                            asm volatile("" : "+v"(an));
+                            av[v][r] = v == 1 && d >= S && d < S + A ? an : 0.f;
+                        } else if constexpr (PHP > 0) {       // (the 512-wide kernels: no registers to spare)
                             const int j = min(max(d - S, 0), A - 1);
                             av[v][r] = v == 1 && d >= S && d < S + A
                                            ? (float)div_rn(__dsub_rn(pact[r], C[2 * 32 + j]), C[3 * 32 + j], C[9 * 32 + j])
