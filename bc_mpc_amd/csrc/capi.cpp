@@ -1647,12 +1647,14 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
 // per ns per workgroup).  cfg3 (15.7M words): 2^16 words -> 240 chunks x 17 slices, draw ~0.18 ms
 // (tools/mt_device_sweep.py, profiles/r02_mt_device_sweep.txt).  Smaller draws want smaller chunks (the
 // serial generation of one chunk is the draw's critical path once the chip has spare workgroups): ~60
-// chunks per draw, as a power of two in [2^14, 2^16] words -- cfg2 (983k words) 0.366 -> 0.322 ms and a
-// K = 1000 x 15 draw 0.262 -> 0.223 ms per drop-in get_action at 2^14 (profiles/r02c_mt_chunk_sweep.txt).
+// chunks per draw, as a power of two in [2^12, 2^16] words -- cfg2 (983k words) 0.366 -> 0.322 ms and a
+// K = 1000 x 15 draw 0.262 -> 0.223 ms per drop-in get_action at 2^14 (profiles/r02c_mt_chunk_sweep.txt);
+// round 4 (the team kernel 30% faster): the K = 1000 x 15 draw at 2^12-word chunks, back to back 0.162 ->
+// 0.153 ms, with host work between calls 0.111 -> 0.105 (profiles/r04_cfg1_chunk_ab.jsonl; 2^13 0.155, 2^15 0.173).
 static int64_t mt_chunk_words(int64_t shard_words) {
     const char* v = std::getenv("BCMPC_MT_CHUNK_WORDS");
     if (v && *v) return std::max<int64_t>(2, std::atoll(v)) & ~int64_t(1);
-    int64_t w = int64_t(1) << 14;
+    int64_t w = int64_t(1) << 12;
     while (w < (int64_t(1) << 16) && 2 * w <= shard_words / 60) w *= 2;
     return w;
 }
