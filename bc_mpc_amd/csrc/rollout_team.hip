@@ -98,6 +98,28 @@ __device__ __forceinline__ float tanh4096(float z) {     // tanh(y) * 2^12 from 
 
 __host__ __device__ constexpr int team_wpe(int NWV) { return NWV >= 8 ? 2 : 1; }
 
+// s[v] = p[(0 * 2 + v) * 64 + lane] + ... + p[((N - 1) * 2 + v) * 64 + lane] in that order (the same bits in
+// every wave and member), both halves v together, the next term's parts requested before the current adds:
+// one read at a time, each waited for, made 2 N dependent LDS round trips of it
+template <int N>
+__device__ __forceinline__ void ordered_sum2(const f4* p, int lane, f4 (&s)[2]) {
+    s[0] = p[(0 * 2 + 0) * 64 + lane];
+    s[1] = p[(0 * 2 + 1) * 64 + lane];
+    if constexpr (N > 1) {
+        f4 nx[2] = {p[(1 * 2 + 0) * 64 + lane], p[(1 * 2 + 1) * 64 + lane]};
+#pragma unroll
+        for (int t = 1; t < N; ++t) {
+            const f4 c0 = nx[0], c1 = nx[1];
+            if (t + 1 < N) {
+                nx[0] = p[((t + 1) * 2 + 0) * 64 + lane];
+                nx[1] = p[((t + 1) * 2 + 1) * 64 + lane];
+            }
+            s[0] += c0;
+            s[1] += c1;
+        }
+    }
+}
+
 // The LDS constants table behind a compiler-opaque value, so the step loop re-reads it instead of hoisting
 // it into registers: an opaque zero offset (keeps the LDS address space: ds_read), or (PTR) an opaque
 // pointer (generic: flat loads; fewer live registers in the kernels that have none to spare)
@@ -1053,6 +1075,7 @@ void rollout_team(const RolloutArgs a) {
             stamp(7);
             rstamp(h, 0);
             if constexpr (T == 1) {
+                // (one term at a time here: the pipelined ordered_sum2 measured +1.5 us at ppo_defaults)
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
                     ot[v] = parts[(0 * 2 + v) * 64 + lane];
@@ -1062,12 +1085,7 @@ void rollout_team(const RolloutArgs a) {
             } else {
                 // member partial: every wave sums the parts in wave order (the same bits in each)
                 f4 mp[2];
-#pragma unroll
-                for (int v = 0; v < 2; ++v) {
-                    mp[v] = parts[(0 * 2 + v) * 64 + lane];
-#pragma unroll
-                    for (int x = 1; x < NWV; ++x) mp[v] += parts[(x * 2 + v) * 64 + lane];
-                }
+                ordered_sum2<NWV>(parts, lane, mp);
                 // exchange (rows < S, + row S for the reward net): wave 0 publishes this member's partial
                 // as granules {epoch, f32} at k * 64 + lane (k = 4 v + r); member (tm + o) % T's are
                 // collected by wave o % NWV; every partial lands in the LDS slot of its member
@@ -1182,12 +1200,7 @@ void rollout_team(const RolloutArgs a) {
                 lds_barrier();                               // every member's partial in LDS
                 rstamp(h, 3);
                 dead = dead || *tdead != 0;
-#pragma unroll
-                for (int v = 0; v < 2; ++v) {
-                    ot[v] = tot[(0 * 2 + v) * 64 + lane];
-#pragma unroll
-                    for (int t = 1; t < T; ++t) ot[v] += tot[(t * 2 + v) * 64 + lane];     // member order
-                }
+                ordered_sum2<T>(tot, lane, ot);              // member order
                 if constexpr (HLN) {
                     // the heads' LayerNorm, completed: the team's (mean, M2) per head from the members'
                     // statistics (Chan, member order, identical in every member), then per output row i
