@@ -90,6 +90,11 @@ def _dp(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
+# RolloutEngine.get_action's prepared-argument path for the per-step call (BCMPC_PY_FASTPATH=0: build the
+# ctypes arguments every call, for A/B runs)
+_GA_FAST = os.environ.get("BCMPC_PY_FASTPATH", "1") != "0"
+
+
 _MT_STATE = [None]          # (bit generator, key pointer, pos pointer) of the verified global MT19937
 
 
@@ -199,6 +204,7 @@ class RolloutEngine:
         self._pol = None
         self.comm = None
         self._mt_fast = None        # get_action_numpy_stream's prepared ctypes arguments
+        self._ga_fast = None        # get_action's (device actions, no cost vector) prepared ctypes arguments
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, spec: MLPSpec, normalization: Sequence, version: int) -> None:
@@ -310,6 +316,28 @@ class RolloutEngine:
     def get_action(self, state, actions: Optional[np.ndarray] = None, seed: int = 0,
                    cand_offset: int = 0, return_costs: bool = False) -> StepResult:
         """Synchronous host-memory control step (bcmpc_get_action)."""
+        if actions is None and not return_costs and _GA_FAST:
+            # the per-step call with in-kernel actions: ctypes arguments built once per shard offset and
+            # reused (state copied into an engine-owned buffer, the first action out of a NumPy view on the
+            # result record) -- as get_action_numpy_stream's fast path, several us of Python less per call
+            fa = self._ga_fast
+            if fa is None or fa[0] != cand_offset:
+                sbuf = np.zeros(self.state_dim, dtype=np.float64)
+                res = _lib.Result()
+                first = np.ctypeslib.as_array(res.first_action)[: self.action_dim]
+                cseed = ctypes.c_uint64(0)
+                args = (self._h, _dp(sbuf), None, cseed, ctypes.c_int64(cand_offset), ctypes.byref(res), None)
+                fa = self._ga_fast = (cand_offset, sbuf, res, first, args, cseed)
+            _, sbuf, res, first, args, cseed = fa
+            s = state if type(state) is np.ndarray else _f64(state)
+            if s.size != self.state_dim:
+                raise ValueError(f"state has {s.size} dims, expected {self.state_dim}")
+            np.copyto(sbuf, s.reshape(-1), casting="unsafe")
+            cseed.value = seed & (2**64 - 1)
+            rc = self._lib.bcmpc_get_action(*args)
+            if rc:
+                _lib.check(rc)
+            return StepResult(res.best_index, res.best_cost, first.copy(), None)
         st = _f64(state).reshape(-1)
         if st.shape[0] != self.state_dim:
             raise ValueError(f"state has {st.shape[0]} dims, expected {self.state_dim}")
