@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method threa
 tail -1 gpurun_out/r04_x3_ab_tests.log
 rm -f gpurun_out/r04_x3_ab.jsonl
 for r in 0 1; do
-  for v in new x3old; do
+  for v in new ${VARIANTS:-x3old}; do
     if [ $v = new ]; then L=""; else L=$PWD/build/variants/libbcmpc_$v.so; fi
     for wl in cfg3 cfg2; do
       BCMPC_LIB=$L timeout -k 10 300 python bench.py --workload $wl --steps 40 --warmup 5 --no-cpu-baseline --no-small-k \
