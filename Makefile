@@ -36,9 +36,13 @@ build/rollout_rr.o: $(SRC)/rollout_rr.hip $(HDR) $(SRC)/split_common.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# the team kernels with the iterative ILP scheduler: ppo_defaults -2.4 us, ppo_mpc_default -5.5 us, run.sh
+# recipe -4.8 us per call against the default (max-ilp +2.5..+21 us, iterative-minreg +0..+24 us;
+# profiles/r04_team_sched_ab.jsonl)
+TEAMSCHED ?= -mllvm -amdgpu-sched-strategy=iterative-ilp
 build/rollout_team.o: $(SRC)/rollout_team.hip $(HDR) $(SRC)/split_common.h
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(TEAMSCHED) -c $< -o $@
 
 build/fit.o: $(SRC)/fit.hip $(HDR)
 	@mkdir -p build

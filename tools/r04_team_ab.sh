@@ -4,9 +4,9 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread -m gpu tests \
   \
-  > gpurun_out/r04_team_lnw2_tests.log 2>&1 || { tail -30 gpurun_out/r04_team_lnw2_tests.log; exit 1; }
-tail -1 gpurun_out/r04_team_lnw2_tests.log
-rm -f gpurun_out/r04_team_lnw2_ab.jsonl
+  > gpurun_out/r04_team_sched2_tests.log 2>&1 || { tail -30 gpurun_out/r04_team_sched2_tests.log; exit 1; }
+tail -1 gpurun_out/r04_team_sched2_tests.log
+rm -f gpurun_out/r04_team_sched2_ab.jsonl
 for r in 0 1; do
   for v in new ${VARIANTS:-oldteam}; do
     if [ $v = new ]; then L=""; else L=$PWD/build/variants/libbcmpc_$v.so; fi
@@ -15,7 +15,7 @@ for r in 0 1; do
 import json,sys
 d=json.loads(sys.stdin.read().strip().splitlines()[-1])
 print(json.dumps({'lib': '$v', 'round': $r, **{k: [round(v['p50_ms']*1e3,1), round(v['kernel_ms']*1e3,1), round(v['dropin_parity_p50_ms']*1e3,1) if v.get('dropin_parity_p50_ms') else None] for k, v in d['small_k'].items()}}))
-" >> gpurun_out/r04_team_lnw2_ab.jsonl || exit 1
+" >> gpurun_out/r04_team_sched2_ab.jsonl || exit 1
   done
 done
-cat gpurun_out/r04_team_lnw2_ab.jsonl
+cat gpurun_out/r04_team_sched2_ab.jsonl

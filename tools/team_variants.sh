@@ -10,7 +10,7 @@ make -s -j8 ARCH=gfx950 >/dev/null
 OBJS="build/rollout.o build/rollout_grp.o build/rollout_x3.o build/rollout_x3_plain.o build/rollout_rr.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  ( $H $flags -c bc_mpc_amd/csrc/rollout_team.hip -o build/variants/rollout_team_$name.o &&
+  ( $H ${TEAMSCHED:--mllvm -amdgpu-sched-strategy=iterative-ilp} $flags -c bc_mpc_amd/csrc/rollout_team.hip -o build/variants/rollout_team_$name.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so $OBJS \
         build/variants/rollout_team_$name.o -ldl ) &
 done
