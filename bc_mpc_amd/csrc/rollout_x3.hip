@@ -73,6 +73,10 @@ namespace bcmpc {
 #ifndef X3_DIAG_NOBAR            // no workgroup barriers inside the step loop
 #define X3_DIAG_NOBAR 0
 #endif
+// widest hidden layer whose plain tanh split kernel takes the branch-free owner phase (v9, §6.4)
+#ifndef X3_BF_MAXHP
+#define X3_BF_MAXHP 512
+#endif
 #ifndef X3_STAMP                 // per-phase s_memtime totals, printed by two blocks at exit
 #define X3_STAMP 0
 #endif
@@ -851,7 +855,7 @@ void rollout_x3(const RolloutArgs a) {
         if (owner && !X3_DIAG_NOOWNER) {
             // ---- normalise the state (dynamics.py:109), cast to f32 (TF feed), column max ----
             const float* xr = xa + ((h % NCH) * CB + 16 * cw + m) * A;
-            if constexpr (PHP > 0 || AK != 0 || F1 || HP > 512) {
+            if constexpr (PHP > 0 || AK != 0 || F1 || HP > X3_BF_MAXHP) {
 #pragma unroll
                 for (int k = 0; k < NHV; ++k)
 #pragma unroll
@@ -1158,7 +1162,7 @@ void rollout_x3(const RolloutArgs a) {
             for (int c = 0; c < NC; ++c)
                 if (c == cw) foc = fo * fcol[c];
         }
-        if constexpr (PHP > 0 || AK != 0 || F1 || HP > 512) {
+        if constexpr (PHP > 0 || AK != 0 || F1 || HP > X3_BF_MAXHP) {
 #pragma unroll
             for (int k = 0; k < NHV; ++k) {
                 const f4 bv = *reinterpret_cast<const f4*>(Blv + LB * HP + 16 * (hv0 + k) + 4 * q);
