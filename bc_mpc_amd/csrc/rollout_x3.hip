@@ -73,7 +73,8 @@ namespace bcmpc {
 #ifndef X3_DIAG_NOBAR            // no workgroup barriers inside the step loop
 #define X3_DIAG_NOBAR 0
 #endif
-// widest hidden layer whose plain tanh split kernel takes the branch-free owner phase (v9, §6.4)
+// widest hidden layer whose plain tanh split kernel takes the branch-free owner phase (v9, §6.4; at 1024 it
+// measured +0.5% at cfg5, profiles/r04_bf1024_ab_rejected.jsonl)
 #ifndef X3_BF_MAXHP
 #define X3_BF_MAXHP 512
 #endif
