@@ -25,7 +25,7 @@ MAX_LAYERS = 8
 MAX_STATE = 32
 MAX_ACTION = 16
 COMM_ID_BYTES = 128
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_STATE, ERR_EMPTY = range(6)
 ACT_TANH, ACT_RELU = 0, 1
@@ -204,6 +204,7 @@ SIGNATURES = [
     ("bcmpc_mt19937_uniform_device", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), _DP, _DP, ctypes.c_int64,
       ctypes.c_int64, _DP]),
+    ("bcmpc_engine_layout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]),
     ("bcmpc_engine_info", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
       ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),

@@ -1130,6 +1130,12 @@ static int sync_step(bcmpc_engine* e, hipStream_t st) {
     return rc == BCMPC_OK ? BCMPC_OK : fail(rc, err);
 }
 
+// the engine a failed synchronous step reruns on: a team engine's fallback engine.  With a communicator
+// attached the failure is the OR over the ranks (step_failed), so a rank whose own kernel is not the team
+// kernel also sees it: that rank reruns the same call on its own engine, which joins the collective
+// rerun's exchange (it has no fallback engine and no host copies of its weights to build one from)
+static int rerun_engine(bcmpc_engine* e, bcmpc_engine** r);
+
 static int team_status(bcmpc_engine* e) {
     if (team_failed(e))
         return fail(BCMPC_ERR_HIP, "team kernel: a workgroup team did not meet (its grid was not resident -- "
@@ -1202,6 +1208,16 @@ static int team_fallback(bcmpc_engine* e, bool collective = false) {
     if (const int rc = bcmpc_set_action_bounds(f, lo, hi)) return rc;
     f->timing = e->timing;
     ++e->team_reruns;
+    return BCMPC_OK;
+}
+
+static int rerun_engine(bcmpc_engine* e, bcmpc_engine** r) {
+    if (e->comm && e->kernel != BCMPC_KERNEL_TEAM) {
+        *r = e;
+        return BCMPC_OK;
+    }
+    if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
+    *r = e->fb;
     return BCMPC_OK;
 }
 
@@ -1633,8 +1649,9 @@ int bcmpc_get_action(bcmpc_engine* e, const double* state, const double* actions
         if (const int sr = sync_step(e, e->stream)) return sr;
     }
     if (step_failed(e)) {
-        if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
-        return bcmpc_get_action(e->fb, state, actions, seed, cand_offset, out, costs_out);
+        bcmpc_engine* re = nullptr;
+        if (const int fr = rerun_engine(e, &re)) return fr;
+        return bcmpc_get_action(re, state, actions, seed, cand_offset, out, costs_out);
     }
     *out = lean ? *e->h_result_map : *e->h_result;
     return BCMPC_OK;
@@ -2169,8 +2186,9 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             e->pre.ready = false;
         }
         if (step_failed(e)) {                         // (NumPy's state not yet advanced)
-            if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
-            return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
+            bcmpc_engine* re = nullptr;
+            if (const int fr = rerun_engine(e, &re)) return fr;
+            return bcmpc_get_action_mt19937(re, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
                                             out, costs_out);
         }
         std::memcpy(mt_key, g.key, sizeof(g.key));
@@ -2263,8 +2281,9 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
             }
         }
         if (step_failed(e)) {                         // (NumPy's state not yet advanced)
-            if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
-            return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
+            bcmpc_engine* re = nullptr;
+            if (const int fr = rerun_engine(e, &re)) return fr;
+            return bcmpc_get_action_mt19937(re, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed,
                                             out, costs_out);
         }
         std::memcpy(mt_key, fin_h, kMtN * sizeof(uint32_t));
@@ -2352,8 +2371,9 @@ int bcmpc_get_action_mt19937(bcmpc_engine* e, const double* state, uint32_t* mt_
         if (se != hipSuccess) return fail(BCMPC_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
     }
     if (step_failed(e)) {
-        if (const int fr = team_fallback(e, e->comm != nullptr)) return fr;
-        return bcmpc_get_action_mt19937(e->fb, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed, out,
+        bcmpc_engine* re = nullptr;
+        if (const int fr = rerun_engine(e, &re)) return fr;
+        return bcmpc_get_action_mt19937(re, state, mt_key, mt_pos, low, high, k_global, cand_offset, seed, out,
                                         costs_out);
     }
     std::memcpy(mt_key, g.key, sizeof(g.key));      // NumPy's state advances only when the call succeeded
@@ -2543,6 +2563,27 @@ int bcmpc_last_kernel_ms(bcmpc_engine* e, float* rollout_ms, float* argmin_ms) {
     HIP_TRY(hipEventElapsedTime(&m, e->ev[1], e->ev[2]));
     if (rollout_ms) *rollout_ms = r;
     if (argmin_ms) *argmin_ms = m;
+    return BCMPC_OK;
+}
+
+int bcmpc_engine_layout(const bcmpc_engine* e, char* buf, int32_t cap) {
+    if (!e || !buf || cap <= 0) return fail(BCMPC_ERR_ARG, "null argument");
+    const char* prec = e->f16 ? "f16" : e->split ? "split" : "fp32";
+    char s[160];
+    switch (e->kernel) {
+        case BCMPC_KERNEL_SOLO: std::snprintf(s, sizeof(s), "rollout_fp32<%d> fp32", e->HP); break;
+        case BCMPC_KERNEL_GROUP2:
+        case BCMPC_KERNEL_GROUP4:
+        case BCMPC_KERNEL_GROUP8: std::snprintf(s, sizeof(s), "rollout_grp<%d,NW=%d> fp32", e->HP, e->nw); break;
+        case BCMPC_KERNEL_SPLITR: std::snprintf(s, sizeof(s), "rollout_rr<%d> split", e->HP); break;
+        case BCMPC_KERNEL_TEAM: std::snprintf(s, sizeof(s), "rollout_team<%d,kind=%d> split", e->HP, e->team_kind); break;
+        default:
+            if (e->pp)
+                std::snprintf(s, sizeof(s), "rollout_pp<%d> %s", e->HP, prec);
+            else
+                std::snprintf(s, sizeof(s), "rollout_x3<%d,NC=%d,NW=%d> %s", e->HP, e->nc, e->nw, prec);
+    }
+    std::snprintf(buf, (size_t)cap, "%s", s);
     return BCMPC_OK;
 }
 

@@ -21,7 +21,9 @@
 #include <stdint.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -107,14 +109,15 @@ static_assert(sizeof(WireRecord) % 16 == 0, "wire record");
 // one wave: the rank's record and its team error word (mapped host memory, written by the team
 // kernel earlier on this stream) into the send slot
 __global__ __launch_bounds__(64) void pack_wire_kernel(const bcmpc_result* __restrict__ res,
-                                                       const unsigned* team_err, WireRecord* __restrict__ wire) {
+                                                       const unsigned* team_err, unsigned force,
+                                                       WireRecord* __restrict__ wire) {
     const uint64_t* src = reinterpret_cast<const uint64_t*>(res);
     uint64_t* dst = reinterpret_cast<uint64_t*>(&wire->r);
     constexpr int kWords = sizeof(bcmpc_result) / sizeof(uint64_t);
     for (int w = threadIdx.x; w < kWords; w += 64) dst[w] = src[w];
     if (threadIdx.x == 0) {
         const unsigned f = team_err ? __hip_atomic_load(team_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-        wire->flags = f ? 1u : 0u;
+        wire->flags = (f || force) ? 1u : 0u;
         wire->pad[0] = wire->pad[1] = wire->pad[2] = 0u;
     }
 }
@@ -160,6 +163,8 @@ struct bcmpc_comm {
     unsigned* h_flags = nullptr;             // mapped: OR of every rank's flags of the last exchange
     unsigned* d_flags = nullptr;
     bool aborted = false;                    // ncclCommAbort'ed after a timed-out exchange
+    int force_flags = 0;                     // (test hook, BCMPC_COMM_FORCE_FLAGS=n: the first n exchanges carry
+                                             //  a set flag, as if another rank's team had given up)
 };
 
 namespace bcmpc {
@@ -173,7 +178,9 @@ int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream
         return BCMPC_ERR_STATE;
     }
     const Rccl& r = rccl();
-    hipLaunchKernelGGL(pack_wire_kernel, dim3(1), dim3(64), 0, st, d_result, d_team_err, c->d_send);
+    const unsigned force = c->force_flags > 0 ? 1u : 0u;
+    if (c->force_flags > 0) --c->force_flags;
+    hipLaunchKernelGGL(pack_wire_kernel, dim3(1), dim3(64), 0, st, d_result, d_team_err, force, c->d_send);
     if (hipGetLastError() != hipSuccess) {
         *err = "pack_wire_kernel launch failed";
         return BCMPC_ERR_HIP;
@@ -204,9 +211,13 @@ bool comm_any_flags(bcmpc_comm* c) {
 // hipStreamSynchronize forever: poll the stream and RCCL's asynchronous error, and after timeout_ms
 // abort the communicator (ncclCommAbort ends its pending collectives) and report.  The communicator is
 // unusable afterwards (every later exchange fails with BCMPC_ERR_STATE).
+// Polls back to back (yielding the core) for the first 2 ms, which covers every control step, then sleeps
+// 50 us between polls: a sleep request of a few microseconds already costs ~50-60 us of timer slack, so a
+// poll that slept would add up to that to the completion of any step longer than the tight-poll window.
 int comm_wait(bcmpc_comm* c, hipStream_t st, int64_t timeout_ms, std::string* err) {
     const Rccl& r = rccl();
     const auto t0 = std::chrono::steady_clock::now();
+    bool tight = true;
     for (uint32_t i = 0;; ++i) {
         const hipError_t q = hipStreamQuery(st);
         if (q == hipSuccess) return BCMPC_OK;
@@ -223,7 +234,9 @@ int comm_wait(bcmpc_comm* c, hipStream_t st, int64_t timeout_ms, std::string* er
                 c->aborted = true;
                 return BCMPC_ERR_HIP;
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+            const auto el = std::chrono::steady_clock::now() - t0;
+            tight = el < std::chrono::milliseconds(2);
+            if (el > std::chrono::milliseconds(timeout_ms)) {
                 (void)r.abort(c->nccl);
                 c->nccl = nullptr;
                 c->aborted = true;
@@ -233,7 +246,10 @@ int comm_wait(bcmpc_comm* c, hipStream_t st, int64_t timeout_ms, std::string* er
                 return BCMPC_ERR_HIP;
             }
         }
-        std::this_thread::sleep_for(std::chrono::microseconds(i < 1000 ? 0 : 50));
+        if (tight)
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
 
@@ -271,6 +287,7 @@ int bcmpc_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t dev
     if (hipSetDevice(device) != hipSuccess) return comm_fail(BCMPC_ERR_HIP, "hipSetDevice failed");
     bcmpc_comm* c = new bcmpc_comm();
     c->nranks = nranks; c->rank = rank; c->device = device;
+    if (const char* v = std::getenv("BCMPC_COMM_FORCE_FLAGS")) c->force_flags = std::max(0, std::atoi(v));
     auto release = [&]() {
         if (c->d_send) (void)hipFree(c->d_send);
         if (c->d_gather) (void)hipFree(c->d_gather);

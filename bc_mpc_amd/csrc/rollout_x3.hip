@@ -1613,14 +1613,18 @@ void rollout_pp(const RolloutArgs a) {
                     for (int i = 0; i < 8; ++i) bown[i] = (_Float16)(xin[i] * sc);
                     swrite(slab0 + wl * 64 + lane, bown);
                     if (q == 0) colf[16 * wl + m] = ldexpf(a.winv[0], -sh) * kTanhK;
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
+                // publish: a workgroup-scope release of this wave's LDS writes (slab0 / colf, and its reads of
+                // the partials), then the count; LDS only ("local"), so the weight loads stay in flight
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                 if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 X3_ST(0);
                 if (h < a.H) {
                     // the group's four layer-0 inputs published (and every partial of the slab read)
                     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (h + 1))
                         __builtin_amdgcn_s_sleep(1);
+                    // (acquire: the slab0 / colf reads below cannot move above the wait)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
                     X3_ST(1);
                     // layer 0 [S+A -> h]: this wave's 8 tiles x the group's 4 columns
                     h8 b0[NC];
@@ -1674,7 +1678,7 @@ void rollout_pp(const RolloutArgs a) {
                     } else {
                         // this wave's slab reads have returned: count it (the group's partials overwrite the
                         // slab only once all 4 waves have, below)
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                         if (lane == 0) __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
 #pragma unroll
@@ -1701,6 +1705,8 @@ void rollout_pp(const RolloutArgs a) {
                 // past their MFMAs)
                 while (__hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (h + 1))
                     __builtin_amdgcn_s_sleep(1);
+                // (acquire: the partial writes below cannot move above the wait)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
                 X3_ST(5);
 #pragma unroll
                 for (int v = 0; v < 2; ++v)

@@ -56,7 +56,9 @@ class LibraryComm:
             _lib.check(self._lib.bcmpc_comm_unique_id(buf))
         obj = [bytes(buf)]
         src = 0 if group is None else dist.get_global_rank(group, 0)
-        dist.broadcast_object_list(obj, src=src, group=group, device=torch.device("cuda", self.device))
+        # (the group's own backend carries the id: CUDA tensors under nccl, host tensors under gloo)
+        dev = torch.device("cuda", self.device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        dist.broadcast_object_list(obj, src=src, group=group, device=dev)
         ctypes.memmove(buf, obj[0], _lib.COMM_ID_BYTES)
         h = ctypes.c_void_p()
         _lib.check(self._lib.bcmpc_comm_init(buf, self.size, self.rank, self.device, ctypes.byref(h)))

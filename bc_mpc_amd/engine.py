@@ -590,10 +590,16 @@ class RolloutEngine:
         _lib.check(self._lib.bcmpc_engine_info(self._h, ctypes.byref(hp), ctypes.byref(wb), ctypes.byref(wpb),
                                                ctypes.byref(kn)))
         names = {v: k for k, v in _lib.KERNELS.items()}
+        buf = ctypes.create_string_buffer(160)
+        _lib.check(self._lib.bcmpc_engine_layout(self._h, buf, len(buf)))
         return dict(hidden_padded=hp.value, packed_weight_bytes=wb.value, waves_per_block=wpb.value,
-                    kernel=names.get(kn.value, str(kn.value)))
+                    kernel=names.get(kn.value, str(kn.value)), layout=buf.value.decode())
 
     def close(self) -> None:
+        # (the prepared ctypes arguments of the fast paths hold the handle: dropped with it, so a call after
+        #  close() passes NULL and gets the library's clean error instead of a freed engine)
+        self._ga_fast = None
+        self._mt_fast = None
         if getattr(self, "_h", None):
             self.comm = None
             self._lib.bcmpc_destroy(self._h)

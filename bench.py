@@ -107,10 +107,14 @@ def _cpu_model() -> str:
 
 
 def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explore=0.5, gamma=1.0, cem=None):
-    """The oracle (NumPy restatement of the reference path, kind "port") timed on the host
-    cores: at the workload's FULL K with the BLAS pool's threads (calls until ``budget_s``), and
-    at 1 thread (one full-K call when that fits the budget, else a K sample).  CEM workloads
-    (cfg5: ~3 min per full-size oracle call) are sampled at K=1024."""
+    """The oracle (NumPy restatement of the reference path, kind "port") timed on the host cores at the
+    workload's FULL K (CEM workloads -- cfg5: minutes per full-size oracle call -- at K=1024) twice: with
+    the BLAS pool's threads (calls until ``budget_s``) and with 1 thread (a K sample of about the same
+    wall time when a full-K call would not fit).  ``value`` / ``cores`` are the faster of the two per
+    candidate-step (at K=400 one thread beats the pool: NumPy's per-call overhead, not the GEMMs); the
+    other stays in the record.  The pool size is the process's BLAS setting (OMP_NUM_THREADS, which the
+    GPU box sets to its CPU share per GPU), not the machine's CPU count; the record names both and the
+    process's CPU affinity."""
     from oracle import mpc_oracle as orc
     from threadpoolctl import threadpool_info, threadpool_limits
     reward = isinstance(spec_w, orc.RewardMLPWeights)
@@ -150,15 +154,27 @@ def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explor
     Ks = min(1024, K_full) if cem else K_full
     v, calls, el = timed(Ks, budget_s)
     per_call = el / calls
-    # 1 thread: one full-K call unless it would take over ~6x the budget (assumed linear in the pool size)
-    K1 = Ks if per_call * threads <= 6 * budget_s else max(256, int(Ks * 6 * budget_s / (per_call * threads)))
+    # 1 thread: a K sample sized to take about the budget (assuming linear in the pool size, at most 1x
+    # the pool's per-call time per thread), never below 64 candidates, never above the line's K
+    K1 = int(min(Ks, max(64, Ks * budget_s / max(per_call * threads, 1e-9))))
     short = per_call * threads < 0.1 * budget_s          # (small K: many 1-thread calls, not one)
     with threadpool_limits(limits=1, user_api="blas"):
         v1, calls1, el1 = timed(K1, budget_s / 2 if short else 0.0, max_calls=(1 << 30) if short else 1)
-    return dict(value=v, unit="candidate-steps/s", cores=int(threads), kind="port", K_sampled=Ks,
+    best_pool = v >= v1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return dict(value=v if best_pool else v1, unit="candidate-steps/s", cores=int(threads) if best_pool else 1,
+                kind="port", K_sampled=Ks if best_pool else K1,
+                value_pool=v, pool_threads=int(threads), K_sampled_pool=Ks,
                 value_1thread=v1, K_sampled_1thread=K1, cpu_model=_cpu_model(), host_cpus=os.cpu_count(),
+                affinity_cpus=aff, omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
+                threads_note=("value/cores = the faster of the BLAS pool and 1 thread per candidate-step; the "
+                              "pool size is OMP_NUM_THREADS (the GPU box's CPU share per GPU), not host_cpus"),
                 sample=f"{calls} oracle get_action calls at K={Ks} (workload K={K_full}), H={H}, {net}, "
-                       f"OpenBLAS {threads} threads, {el:.1f} s; 1 thread: {calls1} call at K={K1}, {el1:.1f} s")
+                       f"OpenBLAS {threads} threads, {el:.1f} s; 1 thread: {calls1} call(s) at K={K1}, {el1:.1f} s"
+                       + (f"; CEM {cem['iterations']} iterations per call" if cem else ""))
 
 
 class _Space:
@@ -420,6 +436,112 @@ def cfg2_line(device, calls=100, warmup=10, cpu_seconds=4.0, dropin_calls=20, wi
     return row
 
 
+def workload_line(name, device, steps=20, warmup=3, cpu_seconds=4.0, with_cpu=True):
+    """Another BASELINE config timed on this GPU as the headline is (a complete get_action per step, HIP
+    events inside the timed region, precision "auto"): cfg4_shard (configs[3]'s per-GPU shard, K=32768,
+    H=20: the N=1 rank of the 8-GPU weak-scaling run) and cfg5 (configs[4]: K=65536, H=50, 3x1024 tanh,
+    CEM x4 on one GPU; one step = one CEMcontroller.get_action = 4 rollout passes + the device elite
+    select / refit, HIP events around the whole device-side call).  The oracle on the host beside it
+    (cfg5 sampled at K=1024: a full-size oracle CEM call takes minutes)."""
+    wl = WORKLOADS[name]
+    prob = synthetic_problem(wl)
+    K, H, cem = wl["K"], wl["H"], wl.get("cem")
+    iters = cem["iterations"] if cem else 1
+    eng = make_engine(wl, prob, device, "auto")
+    if cem:
+        n_elite = max(1, int(round(cem["elite_frac"] * K)))
+        mu0, sd0 = np.zeros((H, A_DIM)), np.full((H, A_DIM), 0.5)
+
+        def call(i):
+            return eng.cem_get_action(prob["state"], mu0, sd0, iters, n_elite, cem["alpha"], 0xC5 + i)[0]
+    else:
+        def call(i):
+            return eng.get_action(prob["state"], None, seed=0xC4 + i)
+    eng.set_timing(True)
+    for i in range(warmup):
+        call(i)
+    ts, ks = [], []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        call(warmup + i)
+        ts.append(time.perf_counter() - t0)
+        ks.append(eng.last_kernel_ms()[0])
+    fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
+    info = eng.info()
+    prec = eng.precision
+    key = f"{name}:{prec}:device"
+    row = {"K": K, "H": H, "net": net_label(wl, prob), "kernel": info["layout"], "precision": prec,
+           "value": K * H * iters / float(np.median(ts)), "unit": "candidate-steps/s", "steps": steps,
+           "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
+           "roofline": roofline_line(K, H, fpcs, float(np.mean(ks)), prec, iters=iters, traffic_key=key)}
+    if cem:
+        row["cem"] = dict(cem, n_elite=n_elite)
+        row["roofline"]["kernel_note"] = ("HIP events around the whole device-side CEM call: 4 rollout passes + "
+                                          "elite select + refit + argmin")
+    eng.close()
+    if with_cpu:
+        row["cpu_baseline"] = cpu_baseline(oracle_weights(prob, wl), prob["norm"], prob["state"], H, cpu_seconds, K,
+                                           net_label(wl, prob), cem=cem)
+    return row
+
+
+def library_comm_line(eng, state, offset, K, H, steps, warmup, world, local, backend):
+    """N > 1: the north_star's collective as the library owns it, timed beside the default line.  The same
+    engine gets libbcmpc's communicator (bcmpc_comm_init over RCCL, its id bootstrapped through
+    torch.distributed) attached, so every get_action ends with the device pack, ONE ncclAllGather of the
+    144-byte records over xGMI and the device np.argmin select (csrc/comm.hip) -- then the same timed loop
+    as the headline.  Guarded: a communicator that cannot be created (e.g. RCCL refusing two ranks on one
+    GPU in a rehearsal) or an exchange that fails / times out (BCMPC_COMM_TIMEOUT_MS, 20 s here) is
+    recorded, every rank agreeing on the outcome, and the bench goes on."""
+    import torch
+    import torch.distributed as dist
+    from bc_mpc_amd import distributed as bdist
+    os.environ.setdefault("BCMPC_COMM_TIMEOUT_MS", "20000")
+    tdev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
+
+    def agree(v, op):
+        t = torch.tensor([float(v)], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    comm, err = None, ""
+    try:
+        comm = bdist.LibraryComm(local)
+    except Exception as ex:                            # (RCCL: "Duplicate GPU detected" on one card)
+        err = str(ex)
+    if agree(1.0 if comm is not None else 0.0, dist.ReduceOp.MIN) < 1.0:
+        if comm is not None:
+            comm.close()
+        return {"status": "init-failed", "error": err or "another rank's bcmpc_comm_init failed"}
+    status, ts, el = "ok", [], float("nan")
+    eng.set_comm(comm)
+    try:
+        for i in range(warmup):
+            eng.get_action(state, None, seed=0xC0 + i, cand_offset=offset)
+        dist.barrier()
+        torch.cuda.synchronize(local)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            t1 = time.perf_counter()
+            eng.get_action(state, None, seed=0xC0 + warmup + i, cand_offset=offset)
+            ts.append(time.perf_counter() - t1)
+        torch.cuda.synchronize(local)
+        el = time.perf_counter() - t0
+    except Exception as ex:
+        status, err = "exchange-failed", str(ex)
+    finally:
+        eng.set_comm(None)
+        comm.close()
+    if agree(1.0 if status == "ok" else 0.0, dist.ReduceOp.MIN) < 1.0:
+        return {"status": "exchange-failed", "error": err or "another rank's exchange failed"}
+    dist.barrier()
+    el = agree(el, dist.ReduceOp.MAX)
+    return {"status": "ok", "value": K * world * H * steps / el, "unit": "candidate-steps/s",
+            "ms_per_step": el / steps * 1e3, "p50_ms": float(np.median(ts) * 1e3),
+            "collective": "libbcmpc RCCL all-gather of the 144-byte result records + device np.argmin select, "
+                          "in get_action (bcmpc_engine_set_comm)"}
+
+
 def small_k_lines(device, calls=200, warmup=20, cpu_seconds=3.0, with_cpu=True):
     """get_action p50 (host state in, device-drawn actions, host result out) and the rollout kernel's
     HIP-event time for the small-K workloads the reference actually runs (train_mpc_ppo.py:71,77: K=400;
@@ -556,6 +678,8 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cfg2", action="store_true", help="skip the cfg2 line (BASELINE configs[1], K=4096)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the cfg4_shard and cfg5 lines (BASELINE configs[3] per-GPU shard, configs[4] on 1 GPU)")
     ap.add_argument("--no-small-k", action="store_true",
                     help="skip the small-K get_action lines (ppo_defaults, runsh_recipe, cfg1: team vs slab kernel)")
     args = ap.parse_args()
@@ -683,6 +807,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    lib_line = None
+    if world > 1 and lib_comm is None and not cem and args.actions == "device":
+        lib_line = library_comm_line(eng, state, offset, K, H, args.steps, args.warmup, world, local, backend)
+
     dropin = None
     if args.dropin_calls > 0 and not (cem or policy or reward):
         dropin = dropin_parity_p50(K * world, H, hidden, L, act, ln, kernels, biases, ln_g, ln_b, norm, state,
@@ -748,6 +876,8 @@ def main():
         "cpu_baseline": None,
         "small_k": None,
     }
+    if lib_line is not None:
+        out["library_comm"] = lib_line
     # PMC HBM traffic per launch of THIS round's kernels (tools/r04_traffic.sh: rocprofv3 --pmc FETCH_SIZE /
     # WRITE_SIZE in separate passes, the gfx950 FETCH_SIZE x2 correction calibrated on the action tensor)
     prof = os.path.join(REPO, "profiles", TRAFFIC_FILE)
@@ -775,6 +905,10 @@ def main():
         out["small_k"] = small_k_lines(local, with_cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cfg2 and args.workload == "cfg3" and not args.no_small_k:
         out["cfg2"] = cfg2_line(local, with_cpu=not args.no_cpu_baseline)
+    if rank == 0 and world == 1 and not args.no_extra and args.workload == "cfg3":
+        out["cfg4_shard"] = workload_line("cfg4_shard", local, with_cpu=not args.no_cpu_baseline)
+        out["cfg5"] = workload_line("cfg5", local, steps=5, warmup=1, cpu_seconds=4.0,
+                                    with_cpu=not args.no_cpu_baseline)
     if (rank == 0 and world == 1 and not args.no_f16 and not (cem or policy or reward or ln) and act == "tanh"
             and eng.precision != "f16"):
         out["f16_single_pass"] = f16_line(wl, prob, local, name=args.workload)

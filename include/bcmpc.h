@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BCMPC_ABI_VERSION 3
+#define BCMPC_ABI_VERSION 4
 #define BCMPC_MAX_LAYERS 8      /* hidden layers supported (dynamics.py:66 n_layers) */
 #define BCMPC_MAX_STATE 32      /* S: observation dim (HalfCheetah: 20, cheetah_env.py:21-27) */
 #define BCMPC_MAX_INPUT 32      /* S + A (dynamics.py:26 concat) */
@@ -439,6 +439,10 @@ int bcmpc_last_kernel_ms(bcmpc_engine* eng, float* rollout_ms, float* argmin_ms)
 /* Static shape facts for tests: padded hidden size and packed weight bytes. */
 int bcmpc_engine_info(const bcmpc_engine* eng, int32_t* hidden_padded, int64_t* packed_weight_bytes,
                       int32_t* waves_per_block, int32_t* kernel);
+/* The device kernel instance the engine launches per rollout, as text (e.g. "rollout_pp<512> f16",
+ * "rollout_x3<512,NC=4,NW=8> split"), NUL-terminated and truncated to cap bytes: tests and the bench
+ * assert / report which layout the engine selected.  Round 5 (ABI 4). */
+int bcmpc_engine_layout(const bcmpc_engine* eng, char* buf, int32_t cap);
 
 #ifdef __cplusplus
 }

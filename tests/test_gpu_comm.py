@@ -115,6 +115,54 @@ def test_single_rank_exchange_team_giveup_reruns_collectively(monkeypatch):
     comm.close()
 
 
+def test_single_rank_non_team_engine_joins_a_collective_rerun(monkeypatch):
+    """With a communicator attached, a flag that ANOTHER rank's team raised (the exchange carries the OR
+    of every rank's flags) makes every rank rerun the step together.  A rank whose own kernel is not the
+    team kernel reruns the same call on its own engine -- joining the rerun's exchange -- instead of
+    building a fallback from host weight copies it does not keep.  The other rank's flag is
+    simulated with the test hook BCMPC_COMM_FORCE_FLAGS=n (the first n exchanges carry a set flag)."""
+    from bc_mpc_amd import _lib
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    lib = _lib.load()
+    w = orc.synthetic_weights(20, 6, 500, 2, "tanh", False)
+    norm = orc.synthetic_normalization(20, 6)
+    state = orc.synthetic_state(norm)
+
+    def make():
+        eng = RolloutEngine(20, 6, 500, 2, "tanh", False, 6, 3000, device=0, kernel="split4")
+        eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, 1)
+        return eng
+    idbuf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    _lib.check(lib.bcmpc_comm_unique_id(idbuf))
+    monkeypatch.setenv("BCMPC_COMM_FORCE_FLAGS", "2")
+    comm = _Comm(idbuf, 1, 0)
+    monkeypatch.delenv("BCMPC_COMM_FORCE_FLAGS")
+    assert comm.rc == 0, comm.err
+    plain, shared = make(), make()
+    assert shared.info()["kernel"] == "split4"
+    shared.set_comm(comm)
+    a = plain.get_action(state, None, seed=5, cand_offset=500)
+    b = shared.get_action(state, None, seed=5, cand_offset=500)    # flagged exchange -> rerun -> clean one
+    assert (a.best_index, a.best_cost) == (b.best_index, b.best_cost)
+    assert np.array_equal(a.first_action, b.first_action)
+    np.random.seed(4)
+    st = np.random.get_state()
+    a = plain.get_action_numpy_stream(state, -np.ones(6), np.ones(6), 3000)
+    after = np.random.get_state()
+    np.random.set_state(st)
+    b = shared.get_action_numpy_stream(state, -np.ones(6), np.ones(6), 3000)   # flagged again: rerun
+    assert (a.best_index, a.best_cost) == (b.best_index, b.best_cost)
+    assert np.array_equal(np.random.get_state()[1], after[1]) and np.random.get_state()[2] == after[2]
+    c = shared.get_action(state, None, seed=6, cand_offset=500)     # the hook is spent: plain exchange
+    d = plain.get_action(state, None, seed=6, cand_offset=500)
+    assert (c.best_index, c.best_cost) == (d.best_index, d.best_cost)
+    assert shared.team_reruns == 0
+    shared.set_comm(None)
+    plain.close(), shared.close()
+    comm.close()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -17,6 +17,8 @@ tolerance of test_gpu_parity.py (the bench's `value` never uses it).  The bar he
 
 F16_TOL_STEP is set from the measured worst case (printed) with headroom: a 2x regression fails.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -41,6 +43,10 @@ def _engine(S, A, w, H, K, norm, kernel="auto"):
     from bc_mpc_amd.engine import MLPSpec, RolloutEngine
     eng = RolloutEngine(S, A, w.hidden, w.n_layers, w.activation, False, H, K, kernel=kernel, precision="f16")
     eng.set_weights(MLPSpec(w.kernels, w.biases, w.activation), norm, version=1)
+    if os.environ.get("BCMPC_F16_PP") == "1" and K >= 128 and w.n_layers == 2 and 256 < w.hidden <= 512:
+        # (the pp_kernel tests: the pipelined kernel must really be the one that runs, not a silent
+        #  fallback to the single-group layouts)
+        assert eng.info()["layout"].startswith("rollout_pp<512>"), eng.info()["layout"]
     return eng
 
 

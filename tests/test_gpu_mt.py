@@ -307,9 +307,6 @@ def test_speculative_device_draw(hidden, L, act, ln, K, H, monkeypatch):
     from bc_mpc_amd.engine import MLPSpec, RolloutEngine
     from oracle import mpc_oracle as orc
     monkeypatch.setenv("BCMPC_MT_SPECULATE", "1")
-    # (team engines take draws up to 2^18 words on the host by default since round 4: cfg1's 180k words
-    #  would never reach the device path this test is about)
-    monkeypatch.setenv("BCMPC_MT_ZC_WORDS", str(1 << 16))
     S, A = 20, 6
     w = orc.synthetic_weights(S, A, hidden, L, act, ln)
     norm = orc.synthetic_normalization(S, A)
