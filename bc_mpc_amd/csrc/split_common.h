@@ -73,11 +73,27 @@ __device__ __forceinline__ void swrite(f4* p, h8 v) { *p = __builtin_bit_cast(f4
 // 4096 - 8192 / (1 + 2^z) (fma / add / fma as packed f32 ops, bit-identical to the scalar
 // form; exp / rcp per element), split.  The pair's accumulators are exactly one k-step B
 // fragment of the next layer (the host's k-order permutation, capi.cpp pack_x3_layer).
+#ifndef BCMPC_EPI_PK             // 0: scalar (default: rollout_pp 0.831 -> 0.822 ms, profiles/r05_epi_scalar_ab.txt), 1: packed f32 fma / add (v_pk_*_f32)
+#define BCMPC_EPI_PK 0
+#endif
 __device__ __forceinline__ void epi_pair_tanh(const f4& a0, const f4& a1, float f, const float* __restrict__ bias,
                                               int t0, int q, h8& hi, h8& lo) {
     const f4 b0 = *reinterpret_cast<const f4*>(bias + 16 * t0 + 4 * q);
     const f4 b1 = *reinterpret_cast<const f4*>(bias + 16 * (t0 + 1) + 4 * q);
     float v[8];
+    if constexpr (!BCMPC_EPI_PK) {
+        // (the same IEEE operations one element at a time: bit-identical)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float z0 = fmaf(a0[r], f, b0[r]), z1 = fmaf(a1[r], f, b1[r]);
+            const float r0 = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z0) + 1.0f);
+            const float r1 = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z1) + 1.0f);
+            v[r] = fmaf(-8192.0f, r0, 4096.0f);
+            v[4 + r] = fmaf(-8192.0f, r1, 4096.0f);
+        }
+        split8(v, hi, lo);
+        return;
+    }
     const f2 one = {1.0f, 1.0f}, m8k = {-8192.0f, -8192.0f}, p4k = {4096.0f, 4096.0f};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

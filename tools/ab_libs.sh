@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B several library builds (BCMPC_LIB) on one workload, alternating rounds; "tree" = the in-tree library.
-# usage: tools/ab_libs.sh workload steps lib1 lib2 ...   (env ROUNDS, default 2; KERNEL: BCMPC_KERNEL)
+# usage: tools/ab_libs.sh workload steps lib1 lib2 ...   (env ROUNDS, default 2; KERNEL: BCMPC_KERNEL;
+#        AB_ARGS: extra bench.py arguments, e.g. "--precision f16")
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -9,7 +10,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in "$@"; do
     if [ "$lib" = tree ]; then unset BCMPC_LIB; else export BCMPC_LIB=$PWD/$lib; fi
     env ${KERNEL:+BCMPC_KERNEL=$KERNEL} timeout -k 10 200 python bench.py --workload "$WL" --steps "$N" --warmup 10 \
-        --no-cpu-baseline --no-small-k --dropin-calls 0 > gpurun_out/ab_libs.log 2>&1 \
+        --no-cpu-baseline --no-small-k --no-cfg2 --no-f16 --no-extra --dropin-calls 0 ${AB_ARGS:-} > gpurun_out/ab_libs.log 2>&1 \
         || { echo "$lib failed"; tail -5 gpurun_out/ab_libs.log; exit 1; }
     python - "$lib" gpurun_out/ab_libs.log <<'PY'
 import json, sys

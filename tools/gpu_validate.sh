@@ -9,6 +9,7 @@
 #     traffic  PMC FETCH_SIZE / WRITE_SIZE passes per workload      -> $OUT/traffic_*/
 #     issue    PMC issue / wait / memory-path passes over $PMC_ARGS -> $OUT/pmc_*/
 #     rehearse 2-rank gloo rehearsal of bench.py on the one card    -> $OUT/rehearsal.json
+#     ab       tools/ab_libs.sh $AB_WL $AB_STEPS $AB_LIBS (AB_ARGS: extra bench arguments) -> $OUT/ab.txt
 #   TAG    output directory gpurun_out/$TAG
 # Every GPU step has its own time limit; the first failure (test failure included) stops the session.
 set -u
@@ -73,6 +74,10 @@ for step in $STEPS; do
           --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 \
           --no-cpu-baseline $BENCH_ARGS > "$OUT/rehearsal.json" 2> "$OUT/rehearsal.err" || stop rehearse $?
       tail -c 600 "$OUT/rehearsal.json" ;;
+    ab)
+      ROUNDS=${ROUNDS:-2} AB_ARGS=${AB_ARGS:-} bash tools/ab_libs.sh ${AB_WL:-cfg3} ${AB_STEPS:-30} $AB_LIBS \
+          > "$OUT/ab.txt" 2>&1 || { cat "$OUT/ab.txt"; stop ab 1; }
+      cat "$OUT/ab.txt" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
