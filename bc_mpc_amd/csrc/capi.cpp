@@ -146,6 +146,8 @@ int set_error(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace bcmpc
 
 static thread_local bool g_no_team = false;         // bcmpc_create: never pick the team kernel (fallbacks)
+// auto-selection bound of the multi-column team kernel (rollout_mc.hip; measured against rollout_x3)
+static constexpr int64_t kMcAutoMaxK = 8192;
 
 struct bcmpc_engine {
     bcmpc_config cfg{};
@@ -218,6 +220,10 @@ struct bcmpc_engine {
     // team kernel (rollout_team.hip): exchange granules, {ticket, generation}, mapped timeout flag
     unsigned long long* d_team = nullptr;
     int team_kind = 0;                  // 0 plain delta net, 1 + policy, 2 reward net (+ policy)
+    // multi-column team kernel (rollout_mc.hip; kernel == TEAM, mc): teams, columns per team, state scratch
+    bool mc = false;
+    int mc_nteam = 0, mc_ncol = 0;
+    double* d_mc_state = nullptr;
     unsigned* d_team_ctl = nullptr;
     unsigned* h_team_err = nullptr;
     unsigned* d_team_err = nullptr;
@@ -448,6 +454,22 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                             !(tkind == 2 && c.layer_norm && (c.state_dim > 23 || !team_rw_ln_built()));
     const bool team_fits = team_shape && c.num_paths > 0 && team_blocks(c.num_paths, e->HP, tkind) <= (int64_t)ncu;
     bool use_team = c.kernel == BCMPC_KERNEL_TEAM;
+    // multi-column team kernel (rollout_mc.hip): the plain 2-layer tanh delta net at hidden 512 in split
+    // precision, several columns per team of 4 CUs -- where the one-column team does not fit the chip.
+    // Auto for K up to kMcAutoMaxK (cfg2-size K); kernel "team" beyond the one-column team's reach takes it
+    // at any K; BCMPC_MC=1 forces it wherever the shape allows, =0 turns it off
+    const bool mc_shape = split && !f16 && tkind == 0 && c.activation == BCMPC_ACT_TANH && !c.layer_norm &&
+                          mc_shape_ok(e->HP, c.n_layers, c.state_dim, c.action_dim, c.horizon) && c.num_paths > 0 &&
+                          mc_teams(c.num_paths, ncu) >= 8 &&
+                          (c.cost == BCMPC_COST_CHEETAH || c.cost == BCMPC_COST_NONE);
+    bool use_mc = false;
+    if (mc_shape && !use_rr && !g_no_team) {
+        const char* ev = std::getenv("BCMPC_MC");
+        const bool on = ev && ev[0] == '1', off = ev && ev[0] == '0';
+        if (use_team && !team_fits) use_mc = !off;
+        else if (c.kernel == BCMPC_KERNEL_AUTO) use_mc = on || (!off && !team_fits && c.num_paths <= kMcAutoMaxK);
+    }
+    if (use_mc) use_team = false;
     if (use_team && !team_fits) {
         delete e;
         return fail(BCMPC_ERR_UNSUPPORTED, "team kernel: 2-layer net, hidden <= 512 (LayerNorm: <= 256; with a "
@@ -455,11 +477,21 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                                            "net: 512, tanh, LayerNorm with S <= 23), S + A <= 32, "
                                            "ceil(K / 128) * 8 * members workgroups <= the device's CUs");
     }
-    if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr && !g_no_team) {
+    if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr && !g_no_team && !use_mc) {
         const char* ev = std::getenv("BCMPC_TEAM");
         use_team = !(ev && ev[0] == '0');
     }
-    if (use_team) {
+    if (use_mc) {
+        e->split = true;
+        e->nc = 1;
+        e->kernel = BCMPC_KERNEL_TEAM;
+        e->mc = true;
+        e->nw = 4;
+        e->team_kind = 0;
+        e->mc_nteam = mc_teams(c.num_paths, ncu);
+        e->mc_ncol = mc_columns_per_team(c.num_paths, ncu);
+        kern = e->kernel;
+    } else if (use_team) {
         e->split = true;
         e->nc = 1;
         e->kernel = BCMPC_KERNEL_TEAM;
@@ -627,7 +659,9 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { g_last_error = "event create failed"; return cleanup(BCMPC_ERR_HIP); }
     if (e->kernel == BCMPC_KERNEL_TEAM) {
         const size_t tb = team_buf_bytes(c.num_paths, e->HP, e->team_kind);
-        if ((tb && hipMalloc(&e->d_team, tb) != hipSuccess) ||
+        const size_t mb = e->mc ? mc_state_bytes(c.num_paths, ncu) : 0;
+        if ((mb && hipMalloc(&e->d_mc_state, mb) != hipSuccess) ||
+            (tb && hipMalloc(&e->d_team, tb) != hipSuccess) ||
             (tb && hipMemset(e->d_team, 0, tb) != hipSuccess) ||
             hipMalloc(&e->d_team_ctl, 4 * sizeof(unsigned)) != hipSuccess ||
             hipMemset(e->d_team_ctl, 0, 4 * sizeof(unsigned)) != hipSuccess ||
@@ -695,7 +729,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
                     (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
                     (void*)e->d_count, (void*)e->d_amin_c, (void*)e->d_amin_i,
-                    (void*)e->d_amin_ticket, (void*)e->d_team, (void*)e->d_team_ctl, (void*)e->d_mt_io, (void*)e->d_mt_bounds, (void*)e->d_mt_xs,
+                    (void*)e->d_amin_ticket, (void*)e->d_team, (void*)e->d_team_ctl, (void*)e->d_mc_state, (void*)e->d_mt_io, (void*)e->d_mt_bounds, (void*)e->d_mt_xs,
                     (void*)e->d_mt_polys, (void*)e->d_mt_chunks, (void*)e->d_mt_part})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
@@ -1390,7 +1424,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         return !(v && v[0] == '0');
     }();
     const bool fused = d_result && !cem &&
-                       (e->kernel == BCMPC_KERNEL_TEAM ? team_fused
+                       (e->kernel == BCMPC_KERNEL_TEAM ? team_fused && !e->mc
                                                        : e->split && e->kernel != BCMPC_KERNEL_SPLITR && fa && fa[0] == '1');
     if (fused) {
         a.fused_argmin = 1;
@@ -1416,7 +1450,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         // diagnostics: TEAM_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_tst = nullptr;
         static size_t tst_n = 0;
-        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
+        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr && !e->mc;
         const size_t nwv = (size_t)(e->HP / 16 / team_layer0_tiles(e->HP, e->team_kind));
         const size_t blocks = (size_t)team_blocks(c.num_paths, e->HP, e->team_kind);
         if (stamps) {
@@ -1431,6 +1465,11 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         if (a.team_spins < 0) {
             __atomic_store_n(e->h_team_err, 1u, __ATOMIC_RELEASE);
             team_skipped = true;                      // (no tail ran: the argmin launch raises the done word)
+        } else if (e->mc) {
+            a.mc_state = e->d_mc_state;
+            a.mc_ncol = e->mc_ncol;
+            a.mc_nteam = e->mc_nteam;
+            HIP_TRY(launch_rollout_mc(a, st));
         } else {
             HIP_TRY(launch_rollout_team(a, e->HP, st));
         }
@@ -2576,7 +2615,13 @@ int bcmpc_engine_layout(const bcmpc_engine* e, char* buf, int32_t cap) {
         case BCMPC_KERNEL_GROUP4:
         case BCMPC_KERNEL_GROUP8: std::snprintf(s, sizeof(s), "rollout_grp<%d,NW=%d> fp32", e->HP, e->nw); break;
         case BCMPC_KERNEL_SPLITR: std::snprintf(s, sizeof(s), "rollout_rr<%d> split", e->HP); break;
-        case BCMPC_KERNEL_TEAM: std::snprintf(s, sizeof(s), "rollout_team<%d,kind=%d> split", e->HP, e->team_kind); break;
+        case BCMPC_KERNEL_TEAM:
+            if (e->mc)
+                std::snprintf(s, sizeof(s), "rollout_mc<%d,T=%d,teams=%d,cols=%d> split", e->HP, mc_members(),
+                              e->mc_nteam, e->mc_ncol);
+            else
+                std::snprintf(s, sizeof(s), "rollout_team<%d,kind=%d> split", e->HP, e->team_kind);
+            break;
         default:
             if (e->pp)
                 std::snprintf(s, sizeof(s), "rollout_pp<%d> %s", e->HP, prec);

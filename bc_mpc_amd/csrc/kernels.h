@@ -105,6 +105,10 @@ struct RolloutArgs {
     // (team kernel, the reward net with LayerNorm heads) [8 members][32 rows]: sum over member t's head
     // rows of the gamma-folded, scaled output weights (the centring correction, rollout_team.hip)
     const float* head_rs;
+    // (multi-column team kernel, rollout_mc.hip) per-member state scratch [columns][T][4 waves][3][64] f64,
+    // columns per team and teams
+    double* mc_state;
+    int32_t mc_ncol, mc_nteam;
 };
 
 struct SelectArgs {                          // top-E of (cost, index) pairs, NaN last, ties -> lower index
@@ -199,6 +203,13 @@ int64_t team_blocks(int64_t K, int hidden_padded, int kind);
 size_t team_buf_bytes(int64_t K, int hidden_padded, int kind);
 bool team_rw_ln_built();                                // the reward net's LayerNorm heads are in this build
 hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st);
+// rollout_mc.hip: the multi-column team kernel (plain tanh delta net, hidden 512, split precision)
+bool mc_shape_ok(int hidden_padded, int n_layers, int state_dim, int action_dim, int horizon);
+int mc_members();                                        // workgroups per team (T)
+int mc_teams(int64_t K, int n_cu);                       // teams launched (a multiple of 8)
+int mc_columns_per_team(int64_t K, int n_cu);
+size_t mc_state_bytes(int64_t K, int n_cu);
+hipError_t launch_rollout_mc(const RolloutArgs& a, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 hipError_t launch_select(const SelectArgs& a, hipStream_t st);
 hipError_t launch_refit(const RefitArgs& a, hipStream_t st);

@@ -420,7 +420,7 @@ def cfg2_line(device, calls=100, warmup=10, cpu_seconds=4.0, dropin_calls=20, wi
         eng.get_action(prob["state"], None, seed=0xC2 + i)
         ks.append(eng.last_kernel_ms()[0])
     fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
-    row = {"K": wl["K"], "H": wl["H"], "kernel": eng.info()["kernel"], "precision": eng.precision,
+    row = {"K": wl["K"], "H": wl["H"], "kernel": eng.info()["layout"], "precision": eng.precision,
            "value": wl["K"] * wl["H"] / float(np.median(ts)), "unit": "candidate-steps/s",
            "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
            "roofline": roofline_line(wl["K"], wl["H"], fpcs, float(np.mean(ks)), eng.precision,
@@ -722,6 +722,8 @@ def main():
                    "split4": "rollout_x3<NC=4>", "splitr": "rollout_rr (resident columns, LDS weight ring)",
                    "team": "rollout_team (weights in registers, one column per team of workgroups)"}.get(
         info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
+    if info["layout"].startswith(("rollout_mc", "rollout_pp")):
+        kernel_name = info["layout"] + f" (hidden padded {info['hidden_padded']}, {act})"
     lib_comm = None
     if (world > 1 and backend == "nccl" and not wl.get("cem") and args.actions == "device"
             and os.environ.get("BCMPC_LIBRARY_COMM", "0") == "1"):
