@@ -158,6 +158,8 @@ struct bcmpc_engine {
     bool split = false;                // BCMPC_PREC_SPLIT_F16 or F16 (rollout_x3)
     bool f16 = false;                  // BCMPC_PREC_F16: single MFMA pass
     bool pp = false;                   // BCMPC_PREC_F16 on the two-group pipelined kernel (rollout_pp)
+    bool pp_fold = false;              // ... with the folded operands (rollout_pp<, FOLD>; BCMPC_PP_FOLD=0: off)
+    bool pp_fold_w = false;            //     active for the current weights (|W| x 2 log2 e within f16's range)
     int nc = 0;                        // split kernel: 16-candidate columns per workgroup
     int nwl = 0;                       // packed weight layers (RolloutArgs.w entries)
     float winv[BCMPC_MAX_LAYERS + 1]{};  // split kernel: 1 / operand scales per layer
@@ -536,6 +538,8 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                 // the two-group pipelined kernel (rollout_pp): 128 candidates per workgroup, 4 waves per
                 // group own 8 hidden tiles each (weights packed 8 tiles per wave)
                 e->pp = true;
+                const char* ef = std::getenv("BCMPC_PP_FOLD");
+                e->pp_fold = !(ef && ef[0] == '0');
                 nc = 8;
                 nw = 8;
             }
@@ -891,9 +895,20 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         // same sizes as the f32 layout (4 bytes per weight: two halves)
         _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
         const int P = T / 2;
+        // rollout_pp's folded operands: the hidden-producing layers as f16(W x 2 log2 e), unscaled, when that
+        // stays well inside f16's range (else the scaled single-pass layout of the same kernel)
+        constexpr float kTanhKh = 2.8853900817779268f;     // 2 log2(e) (split_common.h kTanhK)
+        bool fold = e->pp && e->pp_fold;
+        for (int l = 0; l < L && fold; ++l) {
+            const int in = l == 0 ? S + A : h;
+            float mx = 0.f;
+            for (size_t i = 0; i < (size_t)in * h; ++i) mx = std::max(mx, std::fabs(w->kernels[l][i]));
+            fold = std::isfinite(mx) && mx * kTanhKh < 16384.0f;
+        }
+        e->pp_fold_w = fold;
         for (int l = 0; l <= L; ++l) {
             const int in = l == 0 ? S + A : h, out = l == L ? S : h;
-            const float sw = x3_scale(w->kernels[l], (size_t)in * out);
+            const float sw = fold && l < L ? kTanhKh : x3_scale(w->kernels[l], (size_t)in * out);
             // (team kernel: layer 0 in tb = team_layer0_tiles per wave, hidden layers in team_layer1_tiles)
             const int tbh = e->kernel == BCMPC_KERNEL_TEAM ? team_layer1_tiles(HP, e->team_kind) : tb;
             if (l == 0) pack_x3_layer(w->kernels[0], in, out, 1, T, tb, sw, hh + 2 * e->w_off[0]);
@@ -917,6 +932,7 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
             } else if (l > 0 && c.activation == BCMPC_ACT_RELU) {
                 in_scale = 1.0f;
             }
+            if (fold) in_scale = 1.0f;                     // (folded: hidden activations are tanh in [-1, 1])
             e->winv[l] = (1.0f / sw) * (l == 0 ? 1.0f : 1.0f / in_scale);
         }
         for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
@@ -1357,7 +1373,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
     }
     a.f16_single = e->f16 ? 1 : 0;
     a.x3_nw = e->nw;
-    a.x3_pp = e->pp ? 1 : 0;
+    a.x3_pp = e->pp ? (e->pp_fold_w ? 2 : 1) : 0;
     a.consts = e->d_consts;
     a.state = d_state; a.state_stride = stride;
     if (state_inline) {                       // the tiled state by value in the kernel arguments
@@ -1469,7 +1485,36 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             a.mc_state = e->d_mc_state;
             a.mc_ncol = e->mc_ncol;
             a.mc_nteam = e->mc_nteam;
+            // diagnostics: MC_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
+            static uint64_t* d_mst = nullptr;
+            static size_t mst_n = 0;
+            const bool mst = std::getenv("BCMPC_X3_STAMPS") != nullptr;
+            const size_t mblocks = (size_t)e->mc_nteam * mc_members();
+            if (mst) {
+                if (mst_n < mblocks * 40) {
+                    if (d_mst) (void)hipFree(d_mst);
+                    mst_n = mblocks * 40;
+                    HIP_TRY(hipMalloc(&d_mst, mst_n * sizeof(uint64_t)));
+                }
+                HIP_TRY(hipMemsetAsync(d_mst, 0, mst_n * sizeof(uint64_t), st));
+                a.stamps = d_mst;
+            }
             HIP_TRY(launch_rollout_mc(a, st));
+            if (mst) {
+                std::vector<uint64_t> hs(mblocks * 40);
+                HIP_TRY(hipMemcpyAsync(hs.data(), d_mst, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                const char* names[10] = {"loads+publish", "l0l1mm+c", "ccheck", "cstore", "l1epi", "barrier", "-", "-", "-",
+                                         "prologue"};
+                const double nint = (double)std::max(4, e->mc_ncol) * (c.horizon + 1) + 2;
+                std::fprintf(stderr, "mc stamps (per interval, s_memtime ticks; %.0f intervals):", nint);
+                for (int k = 0; k < 10; ++k) {
+                    double sm = 0;
+                    for (size_t i = 0; i < mblocks * 4; ++i) sm += (double)hs[i * 10 + k];
+                    std::fprintf(stderr, " %s=%.0f", names[k], sm / (mblocks * 4) / (k == 9 ? 1.0 : nint));
+                }
+                std::fprintf(stderr, "\n");
+            }
         } else {
             HIP_TRY(launch_rollout_team(a, e->HP, st));
         }
@@ -2624,7 +2669,7 @@ int bcmpc_engine_layout(const bcmpc_engine* e, char* buf, int32_t cap) {
             break;
         default:
             if (e->pp)
-                std::snprintf(s, sizeof(s), "rollout_pp<%d> %s", e->HP, prec);
+                std::snprintf(s, sizeof(s), "rollout_pp<%d%s> %s", e->HP, e->pp_fold_w ? ",fold" : "", prec);
             else
                 std::snprintf(s, sizeof(s), "rollout_x3<%d,NC=%d,NW=%d> %s", e->HP, e->nc, e->nw, prec);
     }

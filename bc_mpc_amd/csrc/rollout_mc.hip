@@ -42,6 +42,16 @@
 
 namespace bcmpc {
 
+// MC_STAMP 1 (timing diagnostic, variant builds only): per-phase s_memtime totals of every wave into
+// a.stamps ([blocks][4][10]: 0 C loads + publish, 1 L0 + L1 MFMAs with the C computation, 2 C epoch check
+// (and a late granule's poll), 3 C stores, 4 L1 epilogue + out, 5 barrier, 9 prologue)
+#ifndef MC_STAMP
+#define MC_STAMP 0
+#endif
+#if MC_STAMP && !defined(BCMPC_DIAG_VARIANT)
+#error "MC_STAMP is a timing diagnostic: build it with tools/build_variants.sh"
+#endif
+
 namespace {
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -141,6 +151,15 @@ void rollout_mc(const RolloutArgs a) {
     }
     __syncthreads();
 
+    uint64_t ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tp_ = MC_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) __attribute__((always_inline)) {
+        if constexpr (MC_STAMP) {
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();
+            ph_[k] += t_ - tp_;
+            tp_ = t_;
+        }
+    };
     // ---- this wave's resident weights: hidden tiles [2g, 2g + 2) over all k-steps, output k-step g ----
     const int voff = lane * 16;
     h8 w1h[kP][kTPW], w1l[kP][kTPW], woh[2], wol[2];
@@ -178,11 +197,45 @@ void rollout_mc(const RolloutArgs a) {
         return reinterpret_cast<f4*>(base + kOffParts + (k & 1) * kNWV * 2 * 1024);
     };
 
+    stamp(9);
+    // C-stage lanes: the D-fragment granule rows of dims e (k8 = e & 3) and e + 16 (4 + (e & 3)), lane lb
+    const int ka = (e & 3) * 64 + lb, kb = (4 + (e & 3)) * 64 + lb;
     for (int k = -1; k <= J; ++k) {
         // (an opaque zero keeps the per-interval LDS table reads in the loop instead of hoisted registers)
         int wz = 0;
         asm volatile("" : "+s"(wz));
         const double* const Cz = C + wz;
+
+        // ======== C (X_{k+1}): its global loads first -- state scratch, the T members' partials of the
+        //          column's previous step, the HBM action -- their latency passes under the MFMA block ========
+        const int jc = k + 1;
+        const bool c_act = jc >= 0 && jc < J;
+        const int cci = c_act ? jc % NCOLP : 0, ch = c_act ? jc / NCOLP : 0;
+        const int64_t ccol = c0 + cci;
+        const bool c_real = c_act && cci < ncol_t && ccol < ncol;
+        const int64_t lcol = c_real ? ccol : 0;                // (ghosts load a real column's memory, discarded)
+        const int64_t cand = lcol * 16 + cm;
+        const bool valid = c_real && cand < a.K;
+        double* const stp = a.mc_state + ((((size_t)lcol * kT + tm) * kNWV + w) * 3) * 64 + lane;
+        const gu64* const src = gb + ((size_t)lcol * 2 + ((ch - 1) & 1)) * kT * 512;
+        const unsigned epw = (gen << 10) + (unsigned)ch;      // epoch of the partials of step ch - 1
+        const bool gather = c_real && ch > 0;
+        const bool need1 = d1 < S;
+        unsigned long long xa[kT], xb[kT];
+        double st0 = 0.0, st1 = 0.0, stc = 0.0, av = 0.0;
+        const int aj = min(max(d1 - S, 0), A - 1);
+        if (gather) {
+            st0 = stp[0];
+            st1 = stp[64];
+            stc = stp[128];
+        }
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+            xa[t] = __hip_atomic_load(src + t * 512 + ka, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            xb[t] = __hip_atomic_load(src + t * 512 + kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (a.actions && valid && ch < H && d1 >= S && d1 < S + A)
+            av = a.actions[((int64_t)ch * a.K + cand) * A + aj];
 
         // ======== P: publish the member partial of X_{k-2} ========
         {
@@ -209,6 +262,55 @@ void rollout_mc(const RolloutArgs a) {
                 }
             }
         }
+        stamp(0);
+
+        // ---- the C computation of X_{k+1} from the loaded values (branch-free, so it interleaves with the
+        //      MFMAs below; garbage for ghosts and h == 0 is discarded by selects / guarded stores) ----
+        double s0, s1, cost;
+        float x0, x1;
+        int sh;
+        auto c_compute = [&]() __attribute__((always_inline)) {
+            float oa = __uint_as_float((unsigned)xa[0]), ob = __uint_as_float((unsigned)xb[0]);
+#pragma unroll
+            for (int t = 1; t < kT; ++t) {                 // member order (the same bits in every member)
+                oa += __uint_as_float((unsigned)xa[t]);
+                ob += __uint_as_float((unsigned)xb[t]);
+            }
+            const int64_t sc0 = valid ? cand : 0;           // (per-candidate initial states: no read past K)
+            const double i0 = e < S ? (a.state_inline ? a.state_v[e] : a.state[sc0 * a.state_stride + e]) : 0.0;
+            const double i1 = d1 < S ? (a.state_inline ? a.state_v[min(d1, S - 1)]
+                                                       : a.state[sc0 * a.state_stride + min(d1, S - 1)]) : 0.0;
+            // cheetah penalties on the state before the step (cost_functions.py:16-26): dims 5..7
+            const bool pen = (e == 5 && st0 >= 0.2) || ((e == 6 || e == 7) && st0 >= 0.0);
+            const unsigned long long bal = __ballot(pen);
+            const int npen = __popcll((bal >> (16 * (lane >> 4))) & 0xFFFFull);
+            // de-normalise + residual (dynamics.py:113,116), f64, no FMA (dims >= S: padded constants, unread)
+            const float dn0 = fmaf(oa, fo, Bout[e]);
+            const double u0 = __dadd_rn(st0, __dadd_rn(__dmul_rn((double)dn0, Cz[5 * 32 + e]), Cz[4 * 32 + e]));
+            const float dn1 = fmaf(ob, fo, Bout[d1]);
+            const double u1 = __dadd_rn(st1, __dadd_rn(__dmul_rn((double)dn1, Cz[5 * 32 + d1]), Cz[4 * 32 + d1]));
+            const double score = __dsub_rn(10.0 * (double)npen, div_rn(__dsub_rn(u1, st1), 0.01, 1.0 / 0.01));
+            const double uc = a.cost == BCMPC_COST_CHEETAH ? __dadd_rn(stc, score) : stc;
+            s0 = ch == 0 ? i0 : u0;
+            s1 = ch == 0 ? i1 : u1;
+            cost = ch == 0 ? 0.0 : uc;                       // trajectory_cost = 0 (cost_functions.py:60)
+            // the next layer-0 input: normalised state (dynamics.py:109) and action (:110), f32 (the TF feed),
+            // the candidate's power of two (max |x| -> [2^11, 2^12))
+            const double act = a.actions ? av : rng_action(a.seed, (uint64_t)(a.cand_offset + cand), ch, aj,
+                                                           Cz[6 * 32 + aj], Cz[7 * 32 + aj]);
+            const float xs0 = (float)div_rn(__dsub_rn(s0, Cz[0 * 32 + e]), Cz[1 * 32 + e], Cz[8 * 32 + e]);
+            const float xs1 = (float)div_rn(__dsub_rn(s1, Cz[0 * 32 + d1]), Cz[1 * 32 + d1], Cz[8 * 32 + d1]);
+            const float xa1 = (float)div_rn(__dsub_rn(act, Cz[2 * 32 + aj]), Cz[3 * 32 + aj], Cz[9 * 32 + aj]);
+            x0 = valid ? xs0 : 0.f;
+            x1 = !valid ? 0.f : d1 < S ? xs1 : d1 < S + A ? xa1 : 0.f;
+            float mx = fmaxf(fabsf(x0), fabsf(x1));
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+            int ex = 0;
+            (void)frexpf(mx, &ex);
+            sh = 12 - ex;
+            sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
+        };
 
         // ======== L0 (X_k) and L1 (X_{k-1}): unconditional (pipeline fill / drain and ghost columns compute on
         //          stale LDS; their outputs are only read by stages that are inactive too) ========
@@ -244,151 +346,82 @@ void rollout_mc(const RolloutArgs a) {
                     swrite(sw + ((kL0P * w + pp) * 2 + 0) * 64 + lane, xh);
                     swrite(sw + ((kL0P * w + pp) * 2 + 1) * 64 + lane, xl);
                 }
+                if (p == 9) c_compute();                   // (in the MFMA stream: its loads have landed by now)
             }
 #pragma unroll
             for (int j = 0; j < kTPW; ++j) acc1[j] += acc1b[j];
         }
+        stamp(1);
 
-        // ======== C: X_{k+1} ========
-        {
-            const int jc = k + 1;
-            if (jc >= 0 && jc < J) {
-                const int ci = jc % NCOLP, h = jc / NCOLP;
-                const int64_t col = c0 + ci;
-                if (ci < ncol_t && col < ncol) {
-                    const int64_t cand = col * 16 + cm;
-                    const bool valid = cand < a.K;
-                    double* const stp = a.mc_state + ((((size_t)col * kT + tm) * kNWV + w) * 3) * 64 + lane;
-                    const bool writer = tm == 0 && valid;
-                    double s0, s1, cost;
-                    if (h == 0) {
-                        s0 = valid && e < S ? (a.state_inline ? a.state_v[e] : a.state[cand * a.state_stride + e]) : 0.0;
-                        s1 = valid && d1 < S ? (a.state_inline ? a.state_v[d1] : a.state[cand * a.state_stride + d1]) : 0.0;
-                        cost = 0.0;                           // trajectory_cost = 0 (cost_functions.py:60)
-                    } else {
-                        s0 = stp[0];
-                        s1 = stp[64];
-                        cost = stp[128];
-                        // the T members' partials of (column, h - 1): rows e and e + 16 of candidate cm
-                        const unsigned epw = (gen << 10) + (unsigned)h;
-                        const gu64* const src = gb + ((size_t)col * 2 + ((h - 1) & 1)) * kT * 512;
-                        const bool need1 = d1 < S;
-                        float pa[kT], pb[kT];
-                        bool have = false;
-                        for (int spins = 0;; ++spins) {
-                            unsigned long long xa[kT], xb[kT];
+        // ======== C: the epoch check; a late granule (rare) -> poll, then recompute ========
+        if (gather) {
+            bool ok = true;
 #pragma unroll
-                            for (int t = 0; t < kT; ++t) {
-                                xa[t] = __hip_atomic_load(src + t * 512 + (e & 3) * 64 + lb, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                                xb[t] = __hip_atomic_load(src + t * 512 + (4 + (e & 3)) * 64 + lb, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                            }
-                            bool ok = true;
+            for (int t = 0; t < kT; ++t)
+                ok &= (unsigned)(xa[t] >> 32) == epw && (!need1 || (unsigned)(xb[t] >> 32) == epw);
+            if (!__all(ok) && !dead) {
+                for (int spins = 0;; ++spins) {
+                    __builtin_amdgcn_s_sleep(1);
+                    bool ok2 = true;
 #pragma unroll
-                            for (int t = 0; t < kT; ++t) {
-                                pa[t] = __uint_as_float((unsigned)xa[t]);
-                                pb[t] = __uint_as_float((unsigned)xb[t]);
-                                ok &= (unsigned)(xa[t] >> 32) == epw && (!need1 || (unsigned)(xb[t] >> 32) == epw);
-                            }
-                            have = __all(ok);
-                            if (have || dead) break;
-                            bool gone = *reinterpret_cast<volatile int*>(deadf) != 0;
-                            if ((spins & 31) == 31)
-#pragma unroll
-                                for (int t = 0; t < kT; ++t)
-                                    gone = gone || (unsigned)(__hip_atomic_load(src + t * 512 + lane, __ATOMIC_RELAXED,
-                                                                               __HIP_MEMORY_SCOPE_AGENT) >> 32) == dep;
-                            if (__any(gone) || spins >= spin_limit) {
-                                // give up: the mapped error word (the host reruns the call on its fallback
-                                // engine), this member's other waves (LDS), the team (dead tags in granule row 0
-                                // of both parities of every column of the team: every poller reads it)
-                                dead = true;
-                                *reinterpret_cast<volatile int*>(deadf) = 1;
-                                if (lane == 0 && a.team_err)
-                                    __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                                for (int c2 = 0; c2 < ncol_t && c0 + c2 < ncol; ++c2)
-                                    for (int par = 0; par < 2; ++par)
-                                        __hip_atomic_store(gb + (((size_t)(c0 + c2) * 2 + par) * kT + tm) * 512 + lane,
-                                                           (unsigned long long)dep << 32, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-                                break;
-                            }
-                            __builtin_amdgcn_s_sleep(1);
-                        }
-                        float oa = pa[0], ob = pb[0];
-#pragma unroll
-                        for (int t = 1; t < kT; ++t) {         // member order (the same bits in every member)
-                            oa += pa[t];
-                            ob += pb[t];
-                        }
-                        // cheetah penalties on the state before the step (cost_functions.py:16-26): dims 5..7
-                        const bool pen = (e == 5 && s0 >= 0.2) || ((e == 6 || e == 7) && s0 >= 0.0);
-                        const unsigned long long bal = __ballot(pen);
-                        const int npen = __popcll((bal >> (16 * (lane >> 4))) & 0xFFFFull);
-                        const double s17 = s1;                 // (lane e == 1: dim 17)
-                        // de-normalise + residual (dynamics.py:113,116), f64, no FMA; dims >= S carry the
-                        // padded constants (mean 0, std 0) and are never read
-                        {
-                            const float dn0 = fmaf(oa, fo, Bout[e]);
-                            s0 = __dadd_rn(s0, __dadd_rn(__dmul_rn((double)dn0, Cz[5 * 32 + e]), Cz[4 * 32 + e]));
-                            const float dn1 = fmaf(ob, fo, Bout[d1]);
-                            s1 = __dadd_rn(s1, __dadd_rn(__dmul_rn((double)dn1, Cz[5 * 32 + d1]), Cz[4 * 32 + d1]));
-                        }
-                        if (a.cost == BCMPC_COST_CHEETAH) {
-                            const double score = __dsub_rn(10.0 * (double)npen,
-                                                           div_rn(__dsub_rn(s1, s17), 0.01, 1.0 / 0.01));
-                            cost = __dadd_rn(cost, score);
-                        }
+                    for (int t = 0; t < kT; ++t) {
+                        xa[t] = __hip_atomic_load(src + t * 512 + ka, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        xb[t] = __hip_atomic_load(src + t * 512 + kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok2 &= (unsigned)(xa[t] >> 32) == epw && (!need1 || (unsigned)(xb[t] >> 32) == epw);
                     }
-                    if (writer && a.traj) {
-                        if (e < S) a.traj[((int64_t)h * a.K + cand) * S + e] = s0;
-                        if (d1 < S) a.traj[((int64_t)h * a.K + cand) * S + d1] = s1;
-                    }
-                    if (h == H) {
-                        if (writer && e == 1 && a.costs) a.costs[cand] = cost;
-                    } else {
-                        // ---- the next layer-0 input: normalised state (dynamics.py:109) and action (:110),
-                        //      f32 (the TF feed), the candidate's power of two (max |x| -> [2^11, 2^12)) ----
-                        float x0 = valid ? (float)div_rn(__dsub_rn(s0, Cz[0 * 32 + e]), Cz[1 * 32 + e], Cz[8 * 32 + e]) : 0.f;
-                        float x1 = 0.f;
-                        if (valid && d1 < S) {
-                            x1 = (float)div_rn(__dsub_rn(s1, Cz[0 * 32 + d1]), Cz[1 * 32 + d1], Cz[8 * 32 + d1]);
-                        } else if (valid && d1 < S + A) {
-                            const int j = d1 - S;
-                            const double av = a.actions ? a.actions[((int64_t)h * a.K + cand) * A + j]
-                                                        : rng_action(a.seed, (uint64_t)(a.cand_offset + cand), h, j,
-                                                                     Cz[6 * 32 + j], Cz[7 * 32 + j]);
-                            x1 = (float)div_rn(__dsub_rn(av, Cz[2 * 32 + j]), Cz[3 * 32 + j], Cz[9 * 32 + j]);
-                        }
-                        float mx = fmaxf(fabsf(x0), fabsf(x1));
+                    if (__all(ok2)) break;
+                    bool gone = *reinterpret_cast<volatile int*>(deadf) != 0;
+                    if ((spins & 31) == 31)
 #pragma unroll
-                        for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-                        int ex = 0;
-                        (void)frexpf(mx, &ex);
-                        int sh = 12 - ex;
-                        sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
-                        const float sc = ldexpf(1.0f, sh);
-                        x0 *= sc;
-                        x1 *= sc;
-                        const _Float16 h0 = (_Float16)x0, h1 = (_Float16)x1;
-                        const _Float16 l0 = (_Float16)(x0 - (float)h0), l1 = (_Float16)(x1 - (float)h1);
-                        _Float16* const b0w = reinterpret_cast<_Float16*>(base + kOffB0 + (jc & 1) * 2048);
-                        b0w[lb * 8 + (e & 3)] = h0;
-                        b0w[lb * 8 + 4 + (e & 3)] = h1;
-                        b0w[512 + lb * 8 + (e & 3)] = l0;
-                        b0w[512 + lb * 8 + 4 + (e & 3)] = l1;
-                        if (e == 0)
-                            reinterpret_cast<float*>(base + kOffColf)[(jc & 1) * 16 + cm] =
-                                ldexpf(a.winv[0], -sh) * kTanhK;
-                        stp[0] = s0;
-                        stp[64] = s1;
-                        stp[128] = cost;
+                        for (int t = 0; t < kT; ++t)
+                            gone = gone || (unsigned)(__hip_atomic_load(src + t * 512 + lane, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT) >> 32) == dep;
+                    if (__any(gone) || spins >= spin_limit) {
+                        // give up: the mapped error word (the host reruns the call on its fallback engine), this
+                        // member's other waves (LDS), the team (dead tags in granule row 0 of both parities of
+                        // every column of the team: every poller reads it)
+                        dead = true;
+                        *reinterpret_cast<volatile int*>(deadf) = 1;
+                        if (lane == 0 && a.team_err)
+                            __hip_atomic_store(a.team_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        for (int c2 = 0; c2 < ncol_t && c0 + c2 < ncol; ++c2)
+                            for (int par = 0; par < 2; ++par)
+                                __hip_atomic_store(gb + (((size_t)(c0 + c2) * 2 + par) * kT + tm) * 512 + lane,
+                                                   (unsigned long long)dep << 32, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        break;
                     }
                 }
+                c_compute();
             }
         }
-
+        stamp(2);
+        if (c_real) {
+            const bool writer = tm == 0 && valid;
+            if (writer && a.traj) {
+                if (e < S) a.traj[((int64_t)ch * a.K + cand) * S + e] = s0;
+                if (d1 < S) a.traj[((int64_t)ch * a.K + cand) * S + d1] = s1;
+            }
+            if (ch == H) {
+                if (writer && e == 1 && a.costs) a.costs[cand] = cost;
+            } else {
+                const float sc = ldexpf(1.0f, sh);
+                const float y0 = x0 * sc, y1 = x1 * sc;
+                const _Float16 h0 = (_Float16)y0, h1 = (_Float16)y1;
+                const _Float16 l0 = (_Float16)(y0 - (float)h0), l1 = (_Float16)(y1 - (float)h1);
+                _Float16* const b0w = reinterpret_cast<_Float16*>(base + kOffB0 + (jc & 1) * 2048);
+                b0w[lb * 8 + (e & 3)] = h0;
+                b0w[lb * 8 + 4 + (e & 3)] = h1;
+                b0w[512 + lb * 8 + (e & 3)] = l0;
+                b0w[512 + lb * 8 + 4 + (e & 3)] = l1;
+                if (e == 0)
+                    reinterpret_cast<float*>(base + kOffColf)[(jc & 1) * 16 + cm] = ldexpf(a.winv[0], -sh) * kTanhK;
+                stp[0] = s0;
+                stp[64] = s1;
+                stp[128] = cost;
+            }
+        }
+        stamp(3);
         // ======== L1 (X_{k-1}): epilogue, output layer k-step, the wave's partial ========
         {
             h8 oh, ol;
@@ -400,8 +433,14 @@ void rollout_mc(const RolloutArgs a) {
             pw[(w * 2 + 0) * 64 + lane] = po[0];
             pw[(w * 2 + 1) * 64 + lane] = po[1];
         }
+        stamp(4);
         lds_barrier();
         dead = dead || *reinterpret_cast<volatile int*>(deadf) != 0;
+        stamp(5);
+    }
+    if constexpr (MC_STAMP) {
+        if (a.stamps && lane == 0)
+            for (int k2 = 0; k2 < 10; ++k2) a.stamps[((size_t)blockIdx.x * 4 + w) * 10 + k2] = ph_[k2];
     }
 
     // the launch's last workgroup advances the generation (every workgroup read it at its start)

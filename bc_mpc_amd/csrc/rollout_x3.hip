@@ -1379,9 +1379,11 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 __device__ __forceinline__ constexpr int pp_unit_off(int j, int T0, int TW, int TWH) {
     return ((j / PP_G) / (TWH / PP_G)) * TW * 2048 + (T0 + ((j / PP_G) % (TWH / PP_G)) * PP_G + j % PP_G) * 2048;
 }
-template <int TW, int NC, int P, int PG, int PD, int TWH = TW, int T0 = 0>
+template <int TW, int NC, int P, int PG, int PD, int TWH = TW, int T0 = 0, bool BIAS = false>
 __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TWH][NC],
-                                      int lane, const h8 (&s0)[PD * PG]) {
+                                      int lane, const h8 (&s0)[PD * PG], const f4* bias = nullptr) {
+    // (BIAS: the first k-step's MFMAs take bias[tile] as their C operand -- the accumulators start from the
+    //  bias, no separate initialisation)
     // (TWH < TW: tiles [T0, T0 + TWH) of the wave's TW only)
     constexpr int NG = TWH / PG, NU = P * NG, NS = PD + 1;
     const int voff = lane * 16;
@@ -1407,11 +1409,18 @@ __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, cons
 #pragma unroll
         for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int j = 0; j < PG; ++j) acc[g * PG + j][c] = mfma16(sr[u % NS][j], bh[c], acc[g * PG + j][c]);
+            for (int j = 0; j < PG; ++j)
+                acc[g * PG + j][c] = mfma16(sr[u % NS][j], bh[c],
+                                            BIAS && u < NG ? bias[g * PG + j] : acc[g * PG + j][c]);
     }
 }
 
-template <int HP>
+// FOLD (the default, BCMPC_PP_FOLD=0 turns it off): the host packs both hidden-producing layers as
+// f16(W x 2 log2 e) with no power-of-two scales, the MFMAs start from the bias x 2 log2 e, so the
+// accumulators are z and the epilogue is epi_pair_fold (one VALU operation per element fewer); the
+// layer-0 input goes to f16 unscaled (|x| clamped below f16's overflow, NaN kept), no per-column power of
+// two; the hidden activations are tanh in [-1, 1] (the output layer's scale is 1 / its weight scale)
+template <int HP, bool FOLD>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void rollout_pp(const RolloutArgs a) {
     constexpr int NC = 4;                         // 16-candidate columns per group
@@ -1599,20 +1608,28 @@ void rollout_pp(const RolloutArgs a) {
                             else if (d < S + A) xv = xr[d - S];
                             xin[4 * v + r] = xv;
                         }
-                    float mx = 0.f;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fabsf(xin[i]));
-                    mx = max_rows32(max_rows16(mx));
-                    int e = 0;
-                    (void)frexpf(mx, &e);                      // column scale: max |x| -> [2^11, 2^12)
-                    int sh = 12 - e;
-                    sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
-                    const float sc = ldexpf(1.0f, sh);
                     h8 bown;                                   // (the k order of pack_x3_layer)
+                    if constexpr (FOLD) {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) bown[i] = (_Float16)(xin[i] * sc);
+                        for (int i = 0; i < 8; ++i) {          // |x| below f16's overflow, NaN kept
+                            const float xc = fminf(fmaxf(xin[i], -65504.0f), 65504.0f);
+                            bown[i] = (_Float16)(xin[i] == xin[i] ? xc : xin[i]);
+                        }
+                    } else {
+                        float mx = 0.f;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fabsf(xin[i]));
+                        mx = max_rows32(max_rows16(mx));
+                        int e = 0;
+                        (void)frexpf(mx, &e);                  // column scale: max |x| -> [2^11, 2^12)
+                        int sh = 12 - e;
+                        sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
+                        const float sc = ldexpf(1.0f, sh);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) bown[i] = (_Float16)(xin[i] * sc);
+                        if (q == 0) colf[16 * wl + m] = ldexpf(a.winv[0], -sh) * kTanhK;
+                    }
                     swrite(slab0 + wl * 64 + lane, bown);
-                    if (q == 0) colf[16 * wl + m] = ldexpf(a.winv[0], -sh) * kTanhK;
                 }
                 // publish: a workgroup-scope release of this wave's LDS writes (slab0 / colf, and its reads of
                 // the partials), then the count; LDS only ("local"), so the weight loads stay in flight
@@ -1630,11 +1647,15 @@ void rollout_pp(const RolloutArgs a) {
                     h8 b0[NC];
 #pragma unroll
                     for (int c = 0; c < NC; ++c) b0[c] = sread(slab0 + c * 64 + lane);
-                    const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+                    f4 z4[TW];
+#pragma unroll
+                    for (int j = 0; j < TW; ++j)
+                        z4[j] = FOLD ? *reinterpret_cast<const f4*>(Blz + 16 * (wl * TW + j) + 4 * q)
+                                     : (f4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int c = 0; c < NC; ++c)
 #pragma unroll
-                        for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0[j], b0[c], z4);
+                        for (int j = 0; j < TW; ++j) acc[j][c] = mfma16(a0[j], b0[c], z4[j]);
                     // ME's first operand units, in flight through the tanh below and the barrier
 #pragma unroll
                     for (int j = 0; j < PP_D * PP_G; ++j)          // (units 0..PP_D-1 of tile half 0)
@@ -1645,8 +1666,11 @@ void rollout_pp(const RolloutArgs a) {
 #pragma unroll
                         for (int c = 0; c < NC; ++c) {
                             h8 xh, xl;
-                            epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[16 * c + m], Blz, wl * TW + 2 * pp, q,
-                                     xh, xl);
+                            if constexpr (FOLD)
+                                xh = epi_pair_fold(acc[2 * pp][c], acc[2 * pp + 1][c]);
+                            else
+                                epi_pair(acc[2 * pp][c], acc[2 * pp + 1][c], colf[16 * c + m], Blz, wl * TW + 2 * pp,
+                                         q, xh, xl);
                             swrite(slab + ((wl * PW + pp) * NC + c) * 64 + lane, xh);
                         }
                 }
@@ -1666,11 +1690,19 @@ void rollout_pp(const RolloutArgs a) {
                     constexpr int hf = decltype(HFc)::value;
                     constexpr int TWH = TW / 2;
                     f4 ah[TWH][NC];
+                    if constexpr (FOLD) {
+                        f4 bias1[TWH];                          // (the accumulators start from the bias)
 #pragma unroll
-                    for (int j = 0; j < TWH; ++j)
+                        for (int j = 0; j < TWH; ++j)
+                            bias1[j] = *reinterpret_cast<const f4*>(Blz + HP + 16 * (wl * TW + hf * TWH + j) + 4 * q);
+                        mm_pp<TW, NC, P, PP_G, PP_D, TWH, hf * TWH, true>(rs1, wz + wbase1, slab, ah, lane, uh, bias1);
+                    } else {
 #pragma unroll
-                        for (int c = 0; c < NC; ++c) ah[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
-                    mm_pp<TW, NC, P, PP_G, PP_D, TWH, hf * TWH>(rs1, wz + wbase1, slab, ah, lane, uh);
+                        for (int j = 0; j < TWH; ++j)
+#pragma unroll
+                            for (int c = 0; c < NC; ++c) ah[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
+                        mm_pp<TW, NC, P, PP_G, PP_D, TWH, hf * TWH>(rs1, wz + wbase1, slab, ah, lane, uh);
+                    }
                     if constexpr (hf == 0) {
 #pragma unroll
                         for (int j = 0; j < PP_D * PP_G; ++j)      // half 1's first units
@@ -1691,7 +1723,10 @@ void rollout_pp(const RolloutArgs a) {
 #pragma unroll
                         for (int c = 0; c < NC; ++c) {
                             h8 xh, xl;
-                            epi_pair(ah[2 * pp2][c], ah[2 * pp2 + 1][c], f1, Blz + HP, wl * TW + 2 * pp, q, xh, xl);
+                            if constexpr (FOLD)
+                                xh = epi_pair_fold(ah[2 * pp2][c], ah[2 * pp2 + 1][c]);
+                            else
+                                epi_pair(ah[2 * pp2][c], ah[2 * pp2 + 1][c], f1, Blz + HP, wl * TW + 2 * pp, q, xh, xl);
 #pragma unroll
                             for (int v = 0; v < 2; ++v) po[v][c] = mfma16(oh[v], xh, po[v][c]);
                         }
@@ -1915,13 +1950,19 @@ hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc
             return hipErrorInvalidValue;
         static bool attr_set = false;
         if (!attr_set) {
-            const hipError_t e = hipFuncSetAttribute((const void*)rollout_pp<512>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
+            for (const void* f : {(const void*)rollout_pp<512, false>, (const void*)rollout_pp<512, true>}) {
+                const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                if (e != hipSuccess) return e;
+            }
             attr_set = true;
         }
         const int64_t blocks = (a.K + 127) / 128;
-        hipLaunchKernelGGL(rollout_pp<512>, dim3((unsigned)blocks), dim3(512), (size_t)pp_lds_total(512, a.A), st, a);
+        if (a.x3_pp == 2)
+            hipLaunchKernelGGL((rollout_pp<512, true>), dim3((unsigned)blocks), dim3(512), (size_t)pp_lds_total(512, a.A),
+                               st, a);
+        else
+            hipLaunchKernelGGL((rollout_pp<512, false>), dim3((unsigned)blocks), dim3(512), (size_t)pp_lds_total(512, a.A),
+                               st, a);
         return hipGetLastError();
     }
     const int nw = a.x3_nw ? a.x3_nw : x3_waves(hidden_padded);

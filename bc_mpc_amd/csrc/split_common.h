@@ -110,4 +110,25 @@ __device__ __forceinline__ void epi_pair_tanh(const f4& a0, const f4& a1, float 
     split8(v, hi, lo);
 }
 
+// Single-pass "folded" epilogue (rollout_pp with FOLD): the weights carry 2 log2(e) and the accumulators
+// start from the bias x 2 log2(e), so the MFMA result IS z = 2 log2(e) y; tanh(y) = 1 - 2 / (1 + 2^z) in
+// f32 (exp, add, rcp, fma), rounded once to f16 -- one VALU operation per element fewer than
+// epi_pair_tanh's, no power-of-two operand scales (the hidden activations are tanh in [-1, 1])
+__device__ __forceinline__ h8 epi_pair_fold(const f4& a0, const f4& a1) {
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        v[r] = fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(a0[r]) + 1.0f), 1.0f);
+        v[4 + r] = fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(a1[r]) + 1.0f), 1.0f);
+    }
+    h8 hi;
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        const h2 h = __builtin_convertvector((f2){v[i], v[i + 1]}, h2);
+        hi[i] = h[0];
+        hi[i + 1] = h[1];
+    }
+    return hi;
+}
+
 }  // namespace bcmpc

@@ -42,6 +42,10 @@ WORKLOADS = {
     "cfg3": dict(K=65536, H=20, hidden=500, L=2, act="tanh"),
     "cfg4_shard": dict(K=32768, H=20, hidden=500, L=2, act="tanh"),   # 262144 / 8 per GPU
     "cfg3_relu": dict(K=65536, H=20, hidden=500, L=2, act="relu"),    # diagnostic: no tanh
+    # diagnostics: cfg2's net at other K (the multi-column team kernel's auto bound)
+    "k2048": dict(K=2048, H=20, hidden=500, L=2, act="tanh"),
+    "k8192": dict(K=8192, H=20, hidden=500, L=2, act="tanh"),
+    "k16384": dict(K=16384, H=20, hidden=500, L=2, act="tanh"),
     "cfg3_h256": dict(K=65536, H=20, hidden=256, L=2, act="tanh"),    # diagnostic: a 256-wide tanh net
     "cfg5_pass": dict(K=65536, H=50, hidden=1024, L=3, act="tanh"),   # one random-shooting pass of cfg5
     # MPCcontrollerPolicyNet (controllers.py:160-237) at cfg3 dims: 20->128->128->6 tanh policy fused per step,
@@ -620,6 +624,7 @@ def f16_line(wl, prob, device, steps=50, warmup=5, name="cfg3"):
         ts.append(time.perf_counter() - t0)
         ks.append(eng.last_kernel_ms()[0])
     kern = eng.info()["kernel"]
+    layout_name = eng.info()["layout"]
     # argmin agreement with the f32-grade split engine (within the fp32 envelope of the oracle:
     # tests/test_gpu_parity.py; against the oracle itself: tests/test_gpu_f16.py) over 16 seeds
     split = make_engine(wl, prob, device, "split")
@@ -637,8 +642,8 @@ def f16_line(wl, prob, device, steps=50, warmup=5, name="cfg3"):
     pp = (os.environ.get("BCMPC_F16_PP", "") != "0" and not os.environ.get("BCMPC_F16_NC")
           and not os.environ.get("BCMPC_F16_NW") and wl["hidden"] in range(497, 513) and wl["L"] == 2
           and wl.get("act", "tanh") == "tanh" and K >= 2048 * 16)
-    layout = ("rollout_pp<512> (two 64-candidate groups per workgroup, software-pipelined)" if pp
-              else f"rollout_x3 single-pass ({kern})")
+    layout = (f"{layout_name} (two 64-candidate groups per workgroup, software-pipelined)" if pp
+              else f"{layout_name} single-pass")
     traffic = None
     try:
         tr = json.load(open(os.path.join(REPO, "profiles", TRAFFIC_FILE))).get(f"{name}:f16:device")

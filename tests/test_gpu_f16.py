@@ -46,7 +46,7 @@ def _engine(S, A, w, H, K, norm, kernel="auto"):
     if os.environ.get("BCMPC_F16_PP") == "1" and K >= 128 and w.n_layers == 2 and 256 < w.hidden <= 512:
         # (the pp_kernel tests: the pipelined kernel must really be the one that runs, not a silent
         #  fallback to the single-group layouts)
-        assert eng.info()["layout"].startswith("rollout_pp<512>"), eng.info()["layout"]
+        assert eng.info()["layout"].startswith("rollout_pp<512"), eng.info()["layout"]
     return eng
 
 

@@ -124,12 +124,18 @@ def test_team_trajectory_states():
 
 
 def test_team_auto_rule():
-    """Auto picks the team kernel for the reference's small configurations and the slab kernel
-    once the grid would not be resident."""
-    for K, hidden, act, ln, want in [(400, 256, "relu", True, "team"), (1000, 500, "tanh", False, "team"),
-                                     (1100, 500, "tanh", False, "split1"), (65536, 500, "tanh", False, "split4")]:
+    """Auto picks the one-column team kernel for the reference's small configurations, the multi-column
+    team kernel (rollout_mc, engine kernel "team") for the plain 2x500 tanh net once the one-column grid
+    would not be resident and up to capi.cpp's kMcAutoMaxK, and the slab kernel beyond (or for nets
+    the multi-column kernel does not take)."""
+    for K, hidden, act, ln, want, lay in [(400, 256, "relu", True, "team", "rollout_team"),
+                                          (1000, 500, "tanh", False, "team", "rollout_team"),
+                                          (1100, 500, "tanh", False, "team", "rollout_mc"),
+                                          (4096, 500, "tanh", False, "team", "rollout_mc"),
+                                          (65536, 500, "tanh", False, "split4", "rollout_x3")]:
         eng, _, _ = _engine(K, 3, hidden, act, ln, kernel="auto")
         assert eng.info()["kernel"] == want, (K, hidden, eng.info()["kernel"])
+        assert eng.info()["layout"].startswith(lay), (K, hidden, eng.info()["layout"])
         eng.close()
 
 

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build A/B or diagnostic variants of the multi-column team kernel (rollout_mc.hip) into
+# build/variants/libbcmpc_<name>.so (selected at run time via BCMPC_LIB).
+# usage: tools/mc_variants.sh "name:-DFLAG=1 ..." ...
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p build/variants
+H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -DBCMPC_DIAG_VARIANT"
+make -s -j8 ARCH=gfx950 >/dev/null
+OBJS="build/rollout.o build/rollout_grp.o build/rollout_x3.o build/rollout_x3_plain.o build/rollout_rr.o build/rollout_team.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o"
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  ( $H ${MCSCHED:--mllvm -amdgpu-sched-strategy=iterative-ilp} $flags -c bc_mpc_amd/csrc/rollout_mc.hip -o build/variants/rollout_mc_$name.o &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so $OBJS \
+        build/variants/rollout_mc_$name.o -ldl ) &
+done
+wait
+ls build/variants/*.so

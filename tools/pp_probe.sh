@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 f=$(mktemp /tmp/ppprobe_XXXX.hip)
 { echo '#define X3_PROBE 1'; echo '#include "'$PWD'/bc_mpc_amd/csrc/rollout_x3.hip"'
-  echo "template __global__ void bcmpc::rollout_pp<512>(const bcmpc::RolloutArgs);"; } > $f
+  echo "template __global__ void bcmpc::rollout_pp<512, ${PP_FOLD:-true}>(const bcmpc::RolloutArgs);"; } > $f
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize \
   ${X3SCHED:--mllvm -amdgpu-sched-strategy=max-ilp} "$@" --cuda-device-only -c $f -o /tmp/ppprobe.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs:|Spill|Occupancy" | \
