@@ -146,8 +146,10 @@ int set_error(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace bcmpc
 
 static thread_local bool g_no_team = false;         // bcmpc_create: never pick the team kernel (fallbacks)
-// auto-selection bound of the multi-column team kernel (rollout_mc.hip; measured against rollout_x3)
-static constexpr int64_t kMcAutoMaxK = 8192;
+// auto-selection bound of the multi-column team kernel (rollout_mc.hip): 0 -- it measured slower than
+// rollout_x3 at every K it takes (cfg2 0.370 vs 0.247 ms, cfg4 shard 2.67 vs 0.96 ms; DESIGN.md 6.8,
+// profiles/r05_mc_ab.txt), so it is opt-in (BCMPC_MC=1, or kernel "team" beyond the one-column team's reach)
+static constexpr int64_t kMcAutoMaxK = 0;
 
 struct bcmpc_engine {
     bcmpc_config cfg{};

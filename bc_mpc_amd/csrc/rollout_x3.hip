@@ -1364,6 +1364,9 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 #ifndef PP_D
 #define PP_D 2
 #endif
+#ifndef PP_BPRE
+#define PP_BPRE 0
+#endif
 // wave priority per segment (s_setprio).  Without it the arbiter's age order favours group 0 in both of its
 // segments (stamps: group 1's C segment 20k ticks, group 0's 13.7k; profiles/r04_pp_stamps.log).  C ahead
 // of ME evens the groups out (profiles/r04_ppprio_stamps.log) but the interval stays bound by ME; ME ahead
@@ -1392,6 +1395,12 @@ __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     for (int d = 0; d < PD; ++d)
 #pragma unroll
         for (int j = 0; j < PG; ++j) sr[d][j] = s0[d * PG + j];
+    // (PP_BPRE: the next k-step's B fragments are read one k-step ahead, a second register set)
+    h8 bn[PP_BPRE ? NC : 1];
+    if constexpr (PP_BPRE) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) bn[c] = sread(slab + sidx<NC, true>(0, c, 0, lane));
+    }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         if (u + PD < NU) {
@@ -1402,8 +1411,16 @@ __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, cons
             __builtin_amdgcn_sched_barrier(0);
         }
         if (u % NG == 0) {
+            if constexpr (PP_BPRE) {
 #pragma unroll
-            for (int c = 0; c < NC; ++c) bh[c] = sread(slab + sidx<NC, true>(u / NG, c, 0, lane));
+                for (int c = 0; c < NC; ++c) bh[c] = bn[c];
+                if (u / NG + 1 < P)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) bn[c] = sread(slab + sidx<NC, true>(u / NG + 1, c, 0, lane));
+            } else {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) bh[c] = sread(slab + sidx<NC, true>(u / NG, c, 0, lane));
+            }
         }
         const int g = u % NG;
 #pragma unroll

@@ -54,13 +54,14 @@ def test_mc_bitwise_equal_to_one_column_team(K, H, monkeypatch):
 
 
 def test_mc_cfg2_reference_fixture():
-    """BASELINE configs[1] (K = 4096, H = 20, 2x500 tanh) through the reference-run fixture: the auto
-    kernel at this K is the multi-column team; the fp32 bar, argmin and first action exact."""
+    """BASELINE configs[1] (K = 4096, H = 20, 2x500 tanh) through the reference-run fixture on the
+    multi-column team kernel (kernel "team" beyond the one-column team's reach takes it): the fp32 bar,
+    argmin and first action exact."""
     from test_gpu_parity import argmin_is_decidable, assert_costs_close
     g = Golden("cfg2_2x500_tanh")
     from bc_mpc_amd.engine import MLPSpec, RolloutEngine
     wt = g.weights
-    eng = RolloutEngine(g.S, g.A, wt.hidden, wt.n_layers, wt.activation, False, g.H, g.K, device=0)
+    eng = RolloutEngine(g.S, g.A, wt.hidden, wt.n_layers, wt.activation, False, g.H, g.K, device=0, kernel="team")
     eng.set_weights(MLPSpec(wt.kernels, wt.biases, wt.activation), g.norm, version=1)
     assert eng.info()["layout"].startswith("rollout_mc"), eng.info()["layout"]
     res = eng.get_action(g.state, g.actions(), return_costs=True)

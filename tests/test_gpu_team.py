@@ -124,14 +124,12 @@ def test_team_trajectory_states():
 
 
 def test_team_auto_rule():
-    """Auto picks the one-column team kernel for the reference's small configurations, the multi-column
-    team kernel (rollout_mc, engine kernel "team") for the plain 2x500 tanh net once the one-column grid
-    would not be resident and up to capi.cpp's kMcAutoMaxK, and the slab kernel beyond (or for nets
-    the multi-column kernel does not take)."""
+    """Auto picks the one-column team kernel for the reference's small configurations and the slab kernel
+    once the grid would not be resident (the multi-column team kernel is opt-in: capi.cpp kMcAutoMaxK)."""
     for K, hidden, act, ln, want, lay in [(400, 256, "relu", True, "team", "rollout_team"),
                                           (1000, 500, "tanh", False, "team", "rollout_team"),
-                                          (1100, 500, "tanh", False, "team", "rollout_mc"),
-                                          (4096, 500, "tanh", False, "team", "rollout_mc"),
+                                          (1100, 500, "tanh", False, "split1", "rollout_x3"),
+                                          (4096, 500, "tanh", False, "split1", "rollout_x3"),
                                           (65536, 500, "tanh", False, "split4", "rollout_x3")]:
         eng, _, _ = _engine(K, 3, hidden, act, ln, kernel="auto")
         assert eng.info()["kernel"] == want, (K, hidden, eng.info()["kernel"])

@@ -57,7 +57,10 @@ for step in $STEPS; do
         w=${wl%%:*}; p=${wl##*:}
         pmc_pass "traffic_${w}_${p}_fetch" "--workload $w --precision $p" FETCH_SIZE
         pmc_pass "traffic_${w}_${p}_write" "--workload $w --precision $p" WRITE_SIZE
-      done ;;
+      done
+      # (the FETCH_SIZE calibration: cfg3 with its f64 action tensor read from HBM)
+      pmc_pass "traffic_cfg3_split_hbm_fetch" "--workload cfg3 --precision split --actions hbm" FETCH_SIZE
+      python3 "$R/tools/traffic_json.py" "$OUT" "$OUT/traffic_per_launch.json" ;;
     issue)
       pmc_pass pmc_a "$PMC_ARGS" GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY \
           SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC
