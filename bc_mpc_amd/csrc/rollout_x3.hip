@@ -1358,11 +1358,14 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 // k-steps, fully unrolled (no loop-carried operand sets: fixed accumulator registers).  Weights in units of
 // PG tiles through PD + 1 register sets, PD units in flight ahead of the MFMAs (the wave is alone on its
 // SIMD's matrix pipe in this segment: nothing else hides its L2 latency); s0 holds units 0..PD-1.
+// (round 5, folded operands: PP_G 1 x PP_D 4 -- the same 4 KiB in flight per wave, one tile per unit --
+//  measured 0.78 vs 0.785 ms, G2 x D2 / G1 x D6 / + a one-k-step B prefetch within +-0.5%: the segment is not
+//  bound by its weight loads' latency; profiles/r05_pp_prefetch_ab.txt, profiles/r05_pp_prio_ab.txt)
 #ifndef PP_G
-#define PP_G 2
+#define PP_G 1
 #endif
 #ifndef PP_D
-#define PP_D 2
+#define PP_D 4
 #endif
 #ifndef PP_BPRE
 #define PP_BPRE 0
@@ -1370,7 +1373,9 @@ __host__ __device__ constexpr int pp_lds_total(int HP, int A) { return pp_lds_by
 // wave priority per segment (s_setprio).  Without it the arbiter's age order favours group 0 in both of its
 // segments (stamps: group 1's C segment 20k ticks, group 0's 13.7k; profiles/r04_pp_stamps.log).  C ahead
 // of ME evens the groups out (profiles/r04_ppprio_stamps.log) but the interval stays bound by ME; ME ahead
-// measured best by 1-2% (profiles/r04_ppprio_ab.jsonl: 0.860-0.867 vs 0.876-0.887 ms C-first, 0.867-0.873 none)
+// measured best by 1-2% (profiles/r04_ppprio_ab.jsonl: 0.860-0.867 vs 0.876-0.887 ms C-first, 0.867-0.873 none);
+// round 5 with the folded operands (C and ME now ~18k ticks each): ME-first 0.785 ms, equal 0.811, C-first 0.835
+// (profiles/r05_pp_prio_ab.txt)
 #ifndef PP_PRIO_C
 #define PP_PRIO_C 0
 #endif
