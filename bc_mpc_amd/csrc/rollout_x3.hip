@@ -84,8 +84,11 @@ namespace bcmpc {
 // The knobs above exist only for A/B timing builds: they are refused unless the build is a
 // tools/build_variants.sh variant (which defines BCMPC_DIAG_VARIANT and writes build/variants/,
 // loaded only through BCMPC_LIB); `make` / __graft_entry__.build() can never produce them.
+#ifndef PP_DIAG_MFMA32          // rollout_pp's hidden layer as v_mfma_f32_32x32x16_f16 on the same operand bytes
+#define PP_DIAG_MFMA32 0         // (wrong results: the timing of half the MFMA issue slots)
+#endif
 #if (X3_DIAG_NOTANH || X3_DIAG_SMALLW || X3_DIAG_NOOWNER || X3_DIAG_NOMFMA || X3_DIAG_ONEPASS || \
-     X3_DIAG_LOADS || X3_DIAG_NOBAR || X3_STAMP) && !defined(BCMPC_DIAG_VARIANT)
+     X3_DIAG_LOADS || X3_DIAG_NOBAR || X3_STAMP || PP_DIAG_MFMA32) && !defined(BCMPC_DIAG_VARIANT)
 #error "X3_DIAG_* / X3_STAMP are timing-only diagnostics (wrong results): build them with tools/build_variants.sh"
 #endif
 #define X3_ST(k)                                                        \
@@ -1400,6 +1403,12 @@ __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     for (int d = 0; d < PD; ++d)
 #pragma unroll
         for (int j = 0; j < PG; ++j) sr[d][j] = s0[d * PG + j];
+    if constexpr (PP_DIAG_MFMA32 && BIAS) {
+#pragma unroll
+        for (int j = 0; j < TWH; ++j)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[j][c] = bias[j];
+    }
     // (PP_BPRE: the next k-step's B fragments are read one k-step ahead, a second register set)
     h8 bn[PP_BPRE ? NC : 1];
     if constexpr (PP_BPRE) {
@@ -1428,6 +1437,38 @@ __device__ __forceinline__ void mm_pp(__amdgpu_buffer_rsrc_t rs, int wbase, cons
             }
         }
         const int g = u % NG;
+        if constexpr (PP_DIAG_MFMA32) {
+            // tile unit t = g*PG + j as (row tile t/2, sub-step t%2); B fragment c as (column tile c/2,
+            // sub-step c%2); accumulators [TWH][NC] f4 reinterpreted as [TWH/2][NC/2] f16-vectors
+            typedef float f16v __attribute__((ext_vector_type(16)));
+            static_assert(TWH % 2 == 0 && NC % 2 == 0, "pairs");
+#pragma unroll
+            for (int j = 0; j < PG; ++j) {
+                const int t = g * PG + j;
+#pragma unroll
+                for (int ct = 0; ct < NC / 2; ++ct) {
+                    f16v* av = reinterpret_cast<f16v*>(&acc[(t / 2) * 2][ct * 2]);
+                    (void)av;
+                    f16v x;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        x[e] = acc[(t / 2) * 2][ct * 2][e];
+                        x[4 + e] = acc[(t / 2) * 2][ct * 2 + 1][e];
+                        x[8 + e] = acc[(t / 2) * 2 + 1][ct * 2][e];
+                        x[12 + e] = acc[(t / 2) * 2 + 1][ct * 2 + 1][e];
+                    }
+                    x = __builtin_amdgcn_mfma_f32_32x32x16_f16(sr[u % NS][j], bh[ct * 2 + (t & 1)], x, 0, 0, 0);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        acc[(t / 2) * 2][ct * 2][e] = x[e];
+                        acc[(t / 2) * 2][ct * 2 + 1][e] = x[4 + e];
+                        acc[(t / 2) * 2 + 1][ct * 2][e] = x[8 + e];
+                        acc[(t / 2) * 2 + 1][ct * 2 + 1][e] = x[12 + e];
+                    }
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int c = 0; c < NC; ++c)
 #pragma unroll

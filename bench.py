@@ -83,7 +83,7 @@ F16_MFMA_PEAK_TFLOPS = 2516.6     # dense f16/bf16 MFMA: 512 MAC/clk/SIMD x 1024
 # f32-equivalent (algorithmic) ceiling is a third of the f16 peak
 SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
-TRAFFIC_FILE = "r04_traffic_per_launch.json"
+TRAFFIC_FILE = "r05_traffic_per_launch.json"
 
 
 def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None, reward=False):
@@ -386,8 +386,10 @@ def roofline_line(K, H, fpcs, kernel_ms, precision, iters=1, traffic_key=None):
     out = {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s", "frac": tf / peak,
            "flop_per_launch": K * H * iters * fpcs}
     if traffic_key:
-        out["traffic"] = pmc_traffic(traffic_key)
-        out["traffic_source"] = f"profiles/{TRAFFIC_FILE} [{traffic_key}]"
+        t = pmc_traffic(traffic_key)
+        # (the PMC passes measure one rollout launch; a CEM call is `iters` of them)
+        out["traffic"] = t * iters if t is not None else None
+        out["traffic_source"] = f"profiles/{TRAFFIC_FILE} [{traffic_key}]" + (f" x {iters} passes" if iters > 1 else "")
     return out
 
 
@@ -885,7 +887,7 @@ def main():
     }
     if lib_line is not None:
         out["library_comm"] = lib_line
-    # PMC HBM traffic per launch of THIS round's kernels (tools/r04_traffic.sh: rocprofv3 --pmc FETCH_SIZE /
+    # PMC HBM traffic per launch of THIS round's kernels (tools/gpu_validate.sh traffic: rocprofv3 --pmc FETCH_SIZE /
     # WRITE_SIZE in separate passes, the gfx950 FETCH_SIZE x2 correction calibrated on the action tensor)
     prof = os.path.join(REPO, "profiles", TRAFFIC_FILE)
     out["roofline"]["traffic_source"] = f"profiles/{TRAFFIC_FILE}"

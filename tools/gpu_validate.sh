@@ -53,7 +53,7 @@ for step in $STEPS; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_timed" -o run -- \
           python3 bench.py --steps 50 --warmup 5 $LITE $BENCH_ARGS > "$OUT/trace_timed.json" 2>&1 || stop timed $? ;;
     traffic)
-      for wl in ${TRAFFIC_WL:-"cfg3:split cfg3:f16 cfg2:split cfg4_shard:split cfg5:split"}; do
+      for wl in ${TRAFFIC_WL:-cfg3:split cfg3:f16 cfg2:split cfg4_shard:split cfg5:split}; do
         w=${wl%%:*}; p=${wl##*:}
         pmc_pass "traffic_${w}_${p}_fetch" "--workload $w --precision $p" FETCH_SIZE
         pmc_pass "traffic_${w}_${p}_write" "--workload $w --precision $p" WRITE_SIZE

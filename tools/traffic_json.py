@@ -23,6 +23,13 @@ SHAPES = {"cfg3": (65536, 20, 512, 2), "cfg2": (4096, 20, 512, 2), "cfg4_shard":
           "cfg5": (65536, 50, 1024, 3)}
 
 
+READING = {
+    "cfg3": "device-RNG actions: the packed weights (each XCD misses them into its own L2) + the cost vector",
+    "cfg5": ("the packed weights (9.2 MB split) exceed an XCD's 4 MiB L2, so every column step re-streams them "
+             "from the Infinity Cache (FETCH_SIZE counts its hits: MI355X_MICROARCH.md HBM section); one rollout "
+             "pass of the CEM call")}
+
+
 def weight_bytes(hp, L, precision):
     """Packed fragment bytes (capi.cpp pack_x3_layer): layer 0 one k-step, hidden layers P k-steps, the
     output layer 2 tiles; 2 KiB per (tile, k-step) as hi | lo, 1 KiB hi only for the single pass."""
@@ -73,7 +80,7 @@ def main():
         res[f"{wl}:{prec}:device"] = {
             "hbm_bytes_per_launch": hbm, "fetch_size_kb": f_kb, "write_size_kb": w_kb, "dispatches": n,
             "correction": cal, "algorithmic_bytes_per_launch": alg, "kernel": kern[:160],
-            "reading": "device-RNG actions: the packed weights (each XCD misses them into its own L2) + the cost vector",
+            "reading": READING.get(wl, READING["cfg3"]),
             "source": f"{os.path.relpath(SRC, REPO)}/traffic_{name}_{{fetch,write}} (tools/gpu_validate.sh traffic)"}
     json.dump(res, open(DST, "w"), indent=1)
     for k, v in res.items():
