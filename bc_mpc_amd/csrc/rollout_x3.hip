@@ -214,9 +214,14 @@ __device__ __forceinline__ void aload_x3(__amdgpu_buffer_rsrc_t rs, int voff, in
 // other wave: bar() (the "layer input complete" barrier) runs after their MFMAs are
 // issued, overlapping them with the slower waves' epilogues.  (A wave reads its own
 // LDS writes in program order: no barrier.)
-template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, bool F1 = false, typename Bar = void (*)()>
+//
+// NRES (the resident units, X3_RES): the wave's own NOWN units come from registers loaded once per launch
+// (resh / resl) instead of the L2 stream; s0 then arrives holding unit NOWN.
+template <int TW, int NC, int P, int G, bool OWN = false, int PW = 1, bool F1 = false, int NRES = 0,
+          typename Bar = void (*)()>
 __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, const f4* slab, f4 (&acc)[TW][NC],
-                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr) {
+                                      int lane, h8 (&s0h)[G], h8 (&s0l)[G], int k0 = 0, Bar bar = nullptr,
+                                      const h8 (*resh)[G] = nullptr, const h8 (*resl)[G] = nullptr) {
     constexpr int NG = TW / G;
     static_assert(NG * G == TW && (NG == 1 || NG == 2), "one or two units per k-step");
     static_assert((P * NG) % 2 == 0, "ping-pong over unit pairs");
@@ -235,7 +240,15 @@ __device__ __forceinline__ void mm_x3(__amdgpu_buffer_rsrc_t rs, int wbase, cons
     // k-step (NG = 2) or the next k-step (NG = 1)
     constexpr int G1 = NG == 2 ? 1 : 0;
     h8 s1h[G], s1l[G], bh[NC], bl[NC];
-    if constexpr (OWN) {
+    static_assert(NRES == 0 || (OWN && NRES == NOWN && NG == 1 && !F1), "resident units: the own k-steps");
+    if constexpr (NRES > 0) {
+#pragma unroll
+        for (int u = 0; u < NRES; ++u) {
+            bread_x3<NC, F1>(slab, kstep(u), lane, bh, bl);
+            unit_x3<TW, NC, G, F1>(resh[u], resl[u], bh, bl, 0, acc);
+        }
+        bar();
+    } else if constexpr (OWN) {
 #pragma unroll
         for (int u = 0; u < NOWN; u += 2) {
             aload_x3<G, F1>(rs, voff, uoff(u + 1), s1h, s1l, true);
@@ -461,6 +474,9 @@ __host__ __device__ constexpr int x3_group(int TW) { return TW <= X3_GMAX ? TW :
 #ifndef X3_NCH
 #define X3_NCH 4                 // steps of layer-0 action inputs staged in LDS per fill
 #endif
+#ifndef X3_RES                   // NC = 1 at hidden 512 (cfg2's layout): the wave's own two k-steps of the
+#define X3_RES 1                 // hidden layer resident in registers for the whole launch (64 VGPRs)
+#endif
 
 // waves per SIMD the register allocator must allow: two whenever two workgroups
 // (or two waves of one) should share a SIMD
@@ -675,9 +691,24 @@ void rollout_x3(const RolloutArgs a) {
             ol[2 * slot + v] = F1 ? oh[2 * slot + v] : fload(rso, voff, o + 1024);
         }
     };
+    // Resident units (X3_RES; the one-column layout at hidden 512, cfg2's): a workgroup of 16 candidates
+    // streams the whole split net from L2 every step, and that per-CU stream binds it; the
+    // registers the layout leaves free hold the wave's own two k-steps of the hidden layer (1/8 of its
+    // fragments) for the whole launch, so the stream carries 7/8 of it
+    constexpr int NRES = (X3_RES && X3_OWN && NC == 1 && HP == 512 && PHP == 0 && !RW && AK == 0 && !F1 &&
+                          G == TW && PW % 2 == 0) ? PW : 0;
+    h8 rsh[NRES > 0 ? NRES : 1][G], rsl[NRES > 0 ? NRES : 1][G];
+    if constexpr (NRES > 0)
+        if (L >= 2)
+#pragma unroll
+            for (int u = 0; u < NRES; ++u)
+                aload_x3<G>(layer_rsrc(a.w[1], a.wbytes[1]), voff, w * P * TW * 2048 + ((kown + u) % P) * TW * 2048,
+                            rsh[u], rsl[u]);
     auto load_next = [&](int l_next) __attribute__((always_inline)) {
         if (l_next < L) {
-            aload_x3<G, F1>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, wz + w * P * TW * 2048 + kown * TW * 2048, uh, ul);
+            // (layer 1 with resident units: the stream starts at the first k-step past them)
+            const int k1 = (NRES > 0 && l_next == 1) ? (kown + NRES) % P : kown;
+            aload_x3<G, F1>(layer_rsrc(a.w[l_next], a.wbytes[l_next]), voff, wz + w * P * TW * 2048 + k1 * TW * 2048, uh, ul);
         } else {
             load_out(0, std::integral_constant<int, 0>{});
             if constexpr (OP > 1) load_out(1, std::integral_constant<int, OP - 1>{});
@@ -1084,8 +1115,14 @@ void rollout_x3(const RolloutArgs a) {
                 for (int c = 0; c < NC; ++c) acc[j][c] = (f4){0.f, 0.f, 0.f, 0.f};
             const float f = a.winv[l] * kAct;
             // own k-steps first: this wave's slab writes need no barrier
-            mm_x3<TW, NC, P, G, X3_OWN != 0, PW, F1>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc,
-                                                     lane, uh, ul, kown, ready);
+            if (NRES > 0 && l == 1) {
+                if constexpr (NRES > 0)
+                    mm_x3<TW, NC, P, G, true, PW, F1, NRES>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab,
+                                                            acc, lane, uh, ul, kown, ready, rsh, rsl);
+            } else {
+                mm_x3<TW, NC, P, G, X3_OWN != 0, PW, F1>(layer_rsrc(a.w[l], a.wbytes[l]), w * P * TW * 2048, slab, acc,
+                                                         lane, uh, ul, kown, ready);
+            }
             if constexpr (!X3_OWN) ready();
             X3_ST(5);
             load_next(l + 1);
