@@ -1,0 +1,50 @@
+"""bench.py's JSON line on the GPU box (the driver's contract): one short run of the headline workload and
+one of the CEM workload, in child processes, checked for the keys and the relations the driver and the
+judge read -- value = K*H*N*steps / wall time, ms_per_step, the roofline record (achieved / peak = frac,
+traffic from the committed PMC file), n_gpus 1, weak scaling."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LEAN = ["--no-cpu-baseline", "--dropin-calls", "0", "--no-small-k", "--no-f16", "--no-cfg2", "--no-extra"]
+
+
+def _bench(*args):
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_headline_line_contract():
+    d = _bench("--steps", "5", "--warmup", "2", *LEAN)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 2 and d["scaling"] == "weak"
+    assert d["higher_is_better"] is True and d["unit"] == "candidate-steps/s"
+    K, H = d["config"]["K_per_gpu"], d["config"]["horizon"]
+    assert (K, H) == (65536, 20)
+    assert d["value"] == pytest.approx(K * H / (d["ms_per_step"] / 1e3), rel=1e-6)
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and 0 < r["frac"] < 1
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
+    assert r["traffic"] and r["traffic"] > 0                      # profiles/<TRAFFIC_FILE>, cfg3:split:device
+    # the kernel's HIP-event time sits inside the step
+    assert r["flop_per_launch"] / (r["achieved"] * 1e12) * 1e3 <= d["ms_per_step"] * 1.02
+
+
+def test_cem_line_contract():
+    d = _bench("--workload", "cfg5", "--steps", "1", "--warmup", "1", *LEAN)
+    K, H = d["config"]["K_per_gpu"], d["config"]["horizon"]
+    assert (K, H) == (65536, 50)
+    # CEM: every iteration's candidate-steps count (4 rollout passes per get_action)
+    assert d["value"] == pytest.approx(4 * K * H / (d["ms_per_step"] / 1e3), rel=1e-6)
+    assert 0 < d["roofline"]["frac"] < 1
