@@ -19,6 +19,9 @@ DELTA = [  # (K, H, hidden, L, kernel)
     (1, 1, 64, 1, "split1"), (17, 3, 64, 2, "split2"), (65, 2, 100, 2, "split1"), (200, 4, 128, 3, "split4"),
     (129, 5, 200, 2, "split2"), (300, 3, 256, 2, "split4"), (97, 2, 300, 1, "split1"), (257, 4, 500, 2, "split4"),
     (130, 3, 512, 3, "split2"), (70, 2, 600, 2, "split1"), (150, 2, 768, 2, "split2"), (90, 2, 1000, 3, "split2"),
+    # the one-column layout at hidden 512 keeps its own layer-1 k-steps resident (X3_RES): L = 1 (no hidden
+    # layer, nothing resident), L = 2, L = 3 (layer 2 streamed from k-step kown as before)
+    (33, 2, 480, 1, "split1"), (70, 4, 500, 2, "split1"), (130, 3, 512, 3, "split1"),
 ]
 
 
