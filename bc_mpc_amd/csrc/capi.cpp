@@ -944,6 +944,32 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
                 std::memcpy(hln.data() + (size_t)l * HP, w->ln_gamma[l], sizeof(float) * h);
                 std::memcpy(hln.data() + (size_t)(L + l) * HP, w->ln_beta[l], sizeof(float) * h);
             }
+        // the team kernel's deferred last LayerNorm (rollout_team.hip DEFER; relu + LN, T = 1): the output
+        // kernel as dense_2 diag(gamma_1), scaled by its own power of two, its inputs the activations centred
+        // on each wave's column mean (no hsc); bias row b + dense_2^T beta_1 (f64 sum, one rounding); in
+        // gamma_1's slot the per-wave row sums c_w[n] = so sum_{k in wave w} (dense_2 diag(gamma_1))[k][n]
+        if (TEAM_DEFER && e->kernel == BCMPC_KERNEL_TEAM && e->team_kind == 0 && c.layer_norm &&
+            c.activation == BCMPC_ACT_RELU && L == 2 && team_members(HP, e->team_kind) == 1) {
+            const int tpw = team_layer1_tiles(HP, e->team_kind), nwv = HP / 16 / tpw;
+            std::vector<float> wg((size_t)h * S);
+            for (int k = 0; k < h; ++k)
+                for (int n = 0; n < S; ++n) wg[(size_t)k * S + n] = w->kernels[L][(size_t)k * S + n] * w->ln_gamma[L - 1][k];
+            const float so = x3_scale(wg.data(), (size_t)h * S);
+            pack_x3_layer(wg.data(), h, S, P, 2, 2, so, hh + 2 * e->w_off[L]);
+            e->winv[L] = 1.0f / so;
+            for (int n = 0; n < S; ++n) {
+                double acc = w->biases[L][n];
+                for (int k = 0; k < h; ++k) acc += (double)w->kernels[L][(size_t)k * S + n] * (double)w->ln_beta[L - 1][k];
+                hb[e->b_off[L] + n] = (float)acc;
+            }
+            std::fill(hln.begin() + HP, hln.begin() + 2 * HP, 0.f);
+            for (int x = 0; x < nwv; ++x)
+                for (int n = 0; n < S; ++n) {
+                    double acc = 0.0;
+                    for (int k = 16 * tpw * x; k < std::min(h, 16 * tpw * (x + 1)); ++k) acc += (double)wg[(size_t)k * S + n];
+                    hln[(size_t)HP + x * 32 + n] = (float)(acc * so);
+                }
+        }
     } else {
     pack_layer(w->kernels[0], S + A, h, 2, T, tb, hw.data() + e->w_off[0]);
     if (rw) {

@@ -197,6 +197,11 @@ int rr_candidates_per_block();
 hipError_t launch_rollout_rr(const RolloutArgs& a, int hidden_padded, hipStream_t st);
 // rollout_team.hip; kind: 0 the plain delta net, 1 + fused policy, 2 the reward net (+ policy)
 int team_members(int hidden_padded, int kind);          // workgroups per candidate column (0: unsupported)
+// the team kernel's deferred last LayerNorm (relu + LN delta net at T = 1; rollout_team.hip DEFER): the host
+// packs the output layer for it whenever the kernel takes it -- one switch for both sides
+#ifndef TEAM_DEFER
+#define TEAM_DEFER 1
+#endif
 int team_layer0_tiles(int hidden_padded, int kind);     // layer-0 tiles per wave (weight packing)
 int team_layer1_tiles(int hidden_padded, int kind);     // hidden-layer (head) tiles per wave
 int64_t team_blocks(int64_t K, int hidden_padded, int kind);

@@ -141,6 +141,65 @@ __device__ __forceinline__ const double* team_opaque_lds(const double* C) {
 // this kernel goes through LDS; cross-workgroup data travels in atomic granules.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Chan et al.'s merge of the NWV waves' per-column (mean, M2) in wave order (xch: [NWV][16][2]; lane column m)
+template <int NTL, int NWV, bool CLOSED>
+__device__ __forceinline__ void ln_merge(const float* xch, int m, int hidden, float& mean, float& m2) {
+    mean = 0.f;
+    m2 = 0.f;
+    if (hidden == 16 * NTL * NWV) {
+        // every wave full (no padded rows): the merge weights nb / nn and n nb / nn are the same
+        // f32 quotients as below, folded at compile time -- a chain of 2 NWV dependent divisions
+        // per LayerNorm off the step's critical path (bit-identical)
+#pragma unroll
+        for (int v = 0; v < NWV; ++v) {
+            const float nb = (float)(16 * NTL), n = (float)(16 * NTL * v), nn = n + nb;
+            const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
+            const float d = st[0] - mean;
+            mean = mean + d * (nb / nn);
+            m2 = m2 + st[1] + d * d * (n * nb / nn);
+        }
+    } else if constexpr (CLOSED) {
+        // (padded rows: the merge weights from the closed form n_v = min(hidden, 16 NTL v) -- the same
+        //  quotients as the running count gave, now independent of each other instead of a chain of
+        //  2 NWV dependent divisions on the step's critical path)
+        //  (an opaque copy of hidden keeps them in the step: hoisted, their registers spilled elsewhere)
+        int hid = hidden;
+        asm volatile("" : "+s"(hid));
+        float wq0[NWV], wq1[NWV];
+#pragma unroll
+        for (int v = 0; v < NWV; ++v) {
+            const float nb = (float)min(max(hid - 16 * NTL * v, 0), 16 * NTL);
+            const float n = (float)min(max(hid, 0), 16 * NTL * v), nn = n + nb;
+            wq0[v] = nb > 0.f ? nb / nn : 0.f;
+            wq1[v] = nb > 0.f ? n * nb / nn : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < NWV; ++v) {
+            if (hidden - 16 * NTL * v > 0) {
+                const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
+                const float d = st[0] - mean;
+                mean = mean + d * wq0[v];
+                m2 = m2 + st[1] + d * d * wq1[v];
+            }
+        }
+    } else {
+        // (the running count: kept where the closed form measured slower -- ppo_defaults +0.9 us
+        //  although its rows are never padded)
+        float n = 0.f;
+#pragma unroll
+        for (int v = 0; v < NWV; ++v) {
+            const float nb = (float)min(max(hidden - 16 * NTL * v, 0), 16 * NTL);
+            if (nb > 0.f) {
+                const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
+                const float nn = n + nb, d = st[0] - mean;
+                mean = mean + d * (nb / nn);
+                m2 = m2 + st[1] + d * d * (n * nb / nn);
+                n = nn;
+            }
+        }
+    }
+}
+
 // relu / LayerNorm epilogue of one wave's NTL tiles (tile x * NTL + j of the layer), one candidate
 // column per lane column m: BiasAdd + activation in f32, then
 //   XCH (LN, or relu's column max across the member): one exchange of per-column statistics
@@ -148,7 +207,10 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 //     M2 / hidden; x * inv + (beta - mean * inv), inv = rsqrt(var + eps) * gamma, x hsc);
 //   !XCH (relu without LN, layer 1): this wave's own column max picks the power of two;
 // then the split into the next layer's B fragments.  fcol: 2^-sh of relu's column scale.
-template <int AK, int NTL, int NWV, bool XCH, bool CLOSED = false>
+//   DEFER (LN, the last hidden layer at T = 1): no barrier and no normalisation here -- the activations
+//     are left centred on this wave's own column mean, the statistics published for the output layer's
+//     partials barrier, and the normalisation applied to the summed output rows (rollout_team's DEFER)
+template <int AK, int NTL, int NWV, bool XCH, bool CLOSED = false, bool DEFER = false>
 __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* __restrict__ bias,
                                          const float* __restrict__ lg, const float* __restrict__ lb, float hsc,
                                          int hidden, float* xch, int x, int w, int lane, float& fcol) {
@@ -176,7 +238,9 @@ __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* _
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float d = acc[j][r] - s0;
-                s1 += (16 * (x * NTL + j) + 4 * q + r < hidden) ? d * d : 0.f;
+                const bool in = 16 * (x * NTL + j) + 4 * q + r < hidden;
+                s1 += in ? d * d : 0.f;
+                if constexpr (DEFER) acc[j][r] = in ? d : 0.f;
             }
         s1 = add_rows(s1);
     } else {
@@ -188,62 +252,12 @@ __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* _
     }
     if constexpr (XCH) {
         if (q == 0) *reinterpret_cast<f2*>(xch + (w * 16 + m) * 2) = (f2){s0, s1};
+        if constexpr (DEFER) return;                                        // (published with the partials)
         lds_barrier();                                                      // every wave's statistics published
     }
     if constexpr (LNK) {
         float mean = 0.f, m2 = 0.f;
-        if (hidden == 16 * NTL * NWV) {
-            // every wave full (no padded rows): the merge weights nb / nn and n nb / nn are the same
-            // f32 quotients as below, folded at compile time -- a chain of 2 NWV dependent divisions
-            // per LayerNorm off the step's critical path (bit-identical)
-#pragma unroll
-            for (int v = 0; v < NWV; ++v) {
-                const float nb = (float)(16 * NTL), n = (float)(16 * NTL * v), nn = n + nb;
-                const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
-                const float d = st[0] - mean;
-                mean = mean + d * (nb / nn);
-                m2 = m2 + st[1] + d * d * (n * nb / nn);
-            }
-        } else if constexpr (CLOSED) {
-            // (padded rows: the merge weights from the closed form n_v = min(hidden, 16 NTL v) -- the same
-            //  quotients as the running count gave, now independent of each other instead of a chain of
-            //  2 NWV dependent divisions on the step's critical path)
-            //  (an opaque copy of hidden keeps them in the step: hoisted, their registers spilled elsewhere)
-            int hid = hidden;
-            asm volatile("" : "+s"(hid));
-            float wq0[NWV], wq1[NWV];
-#pragma unroll
-            for (int v = 0; v < NWV; ++v) {
-                const float nb = (float)min(max(hid - 16 * NTL * v, 0), 16 * NTL);
-                const float n = (float)min(max(hid, 0), 16 * NTL * v), nn = n + nb;
-                wq0[v] = nb > 0.f ? nb / nn : 0.f;
-                wq1[v] = nb > 0.f ? n * nb / nn : 0.f;
-            }
-#pragma unroll
-            for (int v = 0; v < NWV; ++v) {
-                if (hidden - 16 * NTL * v > 0) {
-                    const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
-                    const float d = st[0] - mean;
-                    mean = mean + d * wq0[v];
-                    m2 = m2 + st[1] + d * d * wq1[v];
-                }
-            }
-        } else {
-            // (the running count: kept where the closed form measured slower -- ppo_defaults +0.9 us
-            //  although its rows are never padded)
-            float n = 0.f;
-#pragma unroll
-            for (int v = 0; v < NWV; ++v) {
-                const float nb = (float)min(max(hidden - 16 * NTL * v, 0), 16 * NTL);
-                if (nb > 0.f) {
-                    const f2 st = *reinterpret_cast<const f2*>(xch + (v * 16 + m) * 2);
-                    const float nn = n + nb, d = st[0] - mean;
-                    mean = mean + d * (nb / nn);
-                    m2 = m2 + st[1] + d * d * (n * nb / nn);
-                    n = nn;
-                }
-            }
-        }
+        ln_merge<NTL, NWV, CLOSED>(xch, m, hidden, mean, m2);
         const float eps = RELU ? 1e-12f : 1e-12f * 16777216.0f;        // tanh: activations carry x 2^12
         const float rs = __builtin_amdgcn_rsqf(m2 * (1.0f / (float)hidden) + eps);    // v_rsq_f32 (~1 ulp)
 #pragma unroll
@@ -325,6 +339,15 @@ void rollout_team(const RolloutArgs a) {
     // whose per-member statistics ride along with the output partials (below)
     static_assert(!LNK || T == 1 || RW, "LayerNorm geometry");
     constexpr bool HLN = RW && LNK;                     // the reward net's LayerNorm heads (dynamics.py:165-177)
+    // DEFER (relu + LayerNorm delta net at T = 1, TEAM_DEFER): the second LayerNorm moves behind the output
+    // layer.  The output kernel is packed as dense_2 diag(gamma_1) (its bias + dense_2^T beta_1 in the bias
+    // row, capi.cpp), each wave feeds it its activations centred on its own column mean, and after the
+    // partials barrier -- which now also publishes the statistics -- the summed rows become
+    // rsqrt(var + eps) (sum + sum_w (mean_w - mean) c_w), c_w = the wave's rows of the scaled, folded output
+    // kernel summed (lnp + HP, [NWV][32]): one barrier and the normalisation pass fewer per step
+    // (not with a fused policy: ppo_mpc_default's kernel spilled 8 VGPRs with it, +0.8 us)
+    constexpr bool DEFER = TEAM_DEFER && T == 1 && AK == 3 && !RW && PHP == 0;     // (kernels.h)
+    static_assert(!DEFER || NWV * 32 <= HP, "the deferred LayerNorm's per-wave row sums fit gamma_1's LDS slot");
     constexpr bool OPQ_PTR = RW || (PHP > 0 && HP > 256);   // (team_opaque_lds)
     // fused policy (MPCcontrollerPolicyNet, ppo_bc_policy.py:54-88): each wave owns one policy tile
     // pair; it shares the dynamics slab (free once the step's partials barrier has passed) and, when
@@ -1077,7 +1100,7 @@ void rollout_team(const RolloutArgs a) {
                     epi_cols<AK, TPW, NWV, false>(acc1, f1, Bl + HP, lnp, lnp, 1.f, a.hidden, nullptr, g, w, lane,
                                                   fcol1);
                 } else {
-                    epi_cols<AK, TPW, NWV, true>(acc1, f1, Bl + HP, lnp + HP, lnp + 3 * HP, a.hsc[1], a.hidden,
+                    epi_cols<AK, TPW, NWV, true, false, DEFER>(acc1, f1, Bl + HP, lnp + HP, lnp + 3 * HP, a.hsc[1], a.hidden,
                                                  xch + NWV * 32, g, w, lane, fcol1);
                 }
                 split_tiles<TPW>(acc1, g & 1, oh, ol);
@@ -1107,6 +1130,30 @@ void rollout_team(const RolloutArgs a) {
                     ot[v] = parts[(0 * 2 + v) * 64 + lane];
 #pragma unroll
                     for (int x = 1; x < NWV; ++x) ot[v] += parts[(x * 2 + v) * 64 + lane];
+                }
+                if constexpr (DEFER) {
+                    // the deferred LayerNorm of the last hidden layer (its statistics published before the
+                    // partials barrier): rows 16 v + 4 q + r of this lane's candidate
+                    const float* const hx = xch + NWV * 32;
+                    float mean, m2;
+                    ln_merge<TPW, NWV, false>(hx, m, a.hidden, mean, m2);
+                    const float rs = __builtin_amdgcn_rsqf(m2 * (1.0f / (float)a.hidden) + 1e-12f);
+                    const float* const cw = lnp + HP;
+                    f4 corr[2] = {(f4){0.f, 0.f, 0.f, 0.f}, (f4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                    for (int x = 0; x < NWV; ++x) {
+                        const float dm = hx[(x * 16 + m) * 2] - mean;
+#pragma unroll
+                        for (int v = 0; v < 2; ++v) {
+                            const f4 c4 = *reinterpret_cast<const f4*>(cw + x * 32 + 16 * v + 4 * q);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) corr[v][r] = fmaf(dm, c4[r], corr[v][r]);
+                        }
+                    }
+#pragma unroll
+                    for (int v = 0; v < 2; ++v)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) ot[v][r] = rs * (ot[v][r] + corr[v][r]);
                 }
             } else {
                 // member partial: every wave sums the parts in wave order (the same bits in each)
