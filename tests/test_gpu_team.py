@@ -25,6 +25,9 @@ SHAPES = [  # (K, H, hidden, activation, layer_norm)
     (400, 7, 256, "relu", True), (257, 4, 256, "tanh", False), (150, 3, 200, "relu", False),
     (1000, 15, 500, "tanh", False), (33, 30, 500, "tanh", False), (500, 4, 400, "relu", False),
     (1024, 2, 512, "tanh", False), (4096, 3, 256, "tanh", True),
+    # relu + LN with padded rows through the deferred last LayerNorm (round 5, DEFER): the last wave holds
+    # 8 valid rows (hidden 200), no valid row at all (hidden 150)
+    (77, 5, 200, "relu", True), (40, 3, 150, "relu", True),
 ]
 
 
