@@ -224,6 +224,7 @@ struct bcmpc_engine {
     // team kernel (rollout_team.hip): exchange granules, {ticket, generation}, mapped timeout flag
     unsigned long long* d_team = nullptr;
     int team_kind = 0;                  // 0 plain delta net, 1 + policy, 2 reward net (+ policy)
+    bool team_defer = false;            // the weights are packed for rollout_team's deferred last LayerNorm
     // multi-column team kernel (rollout_mc.hip; kernel == TEAM, mc): teams, columns per team, state scratch
     bool mc = false;
     int mc_nteam = 0, mc_ncol = 0;
@@ -948,8 +949,9 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         // kernel as dense_2 diag(gamma_1), scaled by its own power of two, its inputs the activations centred
         // on each wave's column mean (no hsc); bias row b + dense_2^T beta_1 (f64 sum, one rounding); in
         // gamma_1's slot the per-wave row sums c_w[n] = so sum_{k in wave w} (dense_2 diag(gamma_1))[k][n]
-        if (TEAM_DEFER && e->kernel == BCMPC_KERNEL_TEAM && e->team_kind == 0 && c.layer_norm &&
-            c.activation == BCMPC_ACT_RELU && L == 2 && team_members(HP, e->team_kind) == 1) {
+        e->team_defer = TEAM_DEFER && e->kernel == BCMPC_KERNEL_TEAM && e->team_kind == 0 && c.layer_norm &&
+                        c.activation == BCMPC_ACT_RELU && L == 2 && team_members(HP, e->team_kind) == 1;
+        if (e->team_defer) {
             const int tpw = team_layer1_tiles(HP, e->team_kind), nwv = HP / 16 / tpw;
             std::vector<float> wg((size_t)h * S);
             for (int k = 0; k < h; ++k)
@@ -2693,7 +2695,8 @@ int bcmpc_engine_layout(const bcmpc_engine* e, char* buf, int32_t cap) {
                 std::snprintf(s, sizeof(s), "rollout_mc<%d,T=%d,teams=%d,cols=%d> split", e->HP, mc_members(),
                               e->mc_nteam, e->mc_ncol);
             else
-                std::snprintf(s, sizeof(s), "rollout_team<%d,kind=%d> split", e->HP, e->team_kind);
+                std::snprintf(s, sizeof(s), "rollout_team<%d,kind=%d%s> split", e->HP, e->team_kind,
+                              e->team_defer ? ",deferLN" : "");
             break;
         default:
             if (e->pp)

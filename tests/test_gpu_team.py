@@ -137,6 +137,8 @@ def test_team_auto_rule():
         eng, _, _ = _engine(K, 3, hidden, act, ln, kernel="auto")
         assert eng.info()["kernel"] == want, (K, hidden, eng.info()["kernel"])
         assert eng.info()["layout"].startswith(lay), (K, hidden, eng.info()["layout"])
+        # train_mpc_ppo's relu + LN net at T = 1 takes the deferred last LayerNorm (round 5)
+        assert ("deferLN" in eng.info()["layout"]) == (ln and act == "relu"), eng.info()["layout"]
         eng.close()
 
 
