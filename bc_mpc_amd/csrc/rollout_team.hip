@@ -252,7 +252,29 @@ __device__ __forceinline__ void epi_cols(f4 (&acc)[NTL], float f, const float* _
     }
     if constexpr (XCH) {
         if (q == 0) *reinterpret_cast<f2*>(xch + (w * 16 + m) * 2) = (f2){s0, s1};
-        if constexpr (DEFER) return;                                        // (published with the partials)
+        if constexpr (DEFER) {
+            // (published with the partials) the centred activations go into the split operands scaled by
+            // this wave's column power of two, |d| max in [2^11, 2^12) as the relu path's below: the lo
+            // half stays out of f16's subnormals (and hi below its overflow) whatever the weights' scale;
+            // the wave's output partial is multiplied back by fcol = 2^-sh (exact) before the partials sum
+            float mx = 0.f;
+#pragma unroll
+            for (int j = 0; j < NTL; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, fabsf(acc[j][r]));
+            mx = max_rows32(max_rows16(mx));
+            int e = 0;
+            (void)frexpf(mx, &e);
+            int sh = 12 - e;
+            sh = mx > 0.f ? (sh < -100 ? -100 : (sh > 100 ? 100 : sh)) : 0;
+            const float sc = ldexpf(1.0f, sh);
+            fcol = ldexpf(1.0f, -sh);
+#pragma unroll
+            for (int j = 0; j < NTL; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[j][r] *= sc;
+            return;
+        }
         lds_barrier();                                                      // every wave's statistics published
     }
     if constexpr (LNK) {
@@ -1114,7 +1136,7 @@ void rollout_team(const RolloutArgs a) {
             for (int pp = 0; pp < PPW; ++pp)
 #pragma unroll
                 for (int v = 0; v < 2; ++v) po[v] = mm3(woh[pp][v], wol[pp][v], oh[pp], ol[pp], po[v]);
-            if constexpr (DYN) {
+            if constexpr (DYN || DEFER) {
                 po[0] *= fcol1;                           // exact: undo this wave's column power of two
                 po[1] *= fcol1;
             }

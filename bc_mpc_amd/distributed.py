@@ -164,6 +164,70 @@ def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optiona
     return float(best[1]), int(best[2]), best[3:].copy()
 
 
+class RecordExchange:
+    """The torch-carried exchange with the selection on the device (the bench's N > 1 default; the
+    per-step cost against the host-staged forms: DESIGN.md §7).  Per control step:
+
+    1. this rank's ``bcmpc_result`` (144 bytes) is written into ``d_result`` by the argmin launch;
+    2. ONE ``all_gather_into_tensor`` of the records (RCCL over xGMI under nccl; under gloo through
+       host memory), stream-ordered after that launch on torch's current stream;
+    3. ``bcmpc_select_results_async`` (the library's np.argmin / np.argmax rule, comm.hip) reduces
+       the ``world`` records on the same stream;
+    4. one D2H of the 144-byte winner into pinned memory, one stream synchronisation.
+
+    No host round trip sits between the argmin and the collective, and the host never walks the
+    records.  Every rank must hold >= 1 candidate."""
+
+    def __init__(self, device: int, maximize: bool = False, group=None):
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        self._lib = _lib.load()
+        self.rank, self.size = world(group)
+        self.group = group
+        self.maximize = int(bool(maximize))
+        self.device = torch.device("cuda", int(device))
+        self.backend = dist.get_backend(group) if self.size > 1 else "none"
+        nb = ctypes_sizeof_result()
+        self.d_result = torch.zeros(nb, dtype=torch.uint8, device=self.device)
+        self.d_all = torch.zeros(max(1, self.size) * nb, dtype=torch.uint8, device=self.device)
+        self.d_best = torch.zeros(nb, dtype=torch.uint8, device=self.device)
+        self.h_best = torch.zeros(nb, dtype=torch.uint8).pin_memory()
+        self._nb = nb
+
+    def exchange(self, stream) -> Tuple[float, int, np.ndarray]:
+        """Steps 2-4 on ``stream`` (a torch.cuda.Stream: the one the argmin was launched on)."""
+        import ctypes
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        with torch.cuda.stream(stream):
+            if self.size > 1:
+                if self.backend == "nccl":
+                    dist.all_gather_into_tensor(self.d_all, self.d_result, group=self.group)
+                else:                                  # gloo: host tensors
+                    out = torch.empty(self.size * self._nb, dtype=torch.uint8)
+                    dist.all_gather_into_tensor(out, self.d_result.cpu(), group=self.group)
+                    self.d_all.copy_(out)
+            else:
+                self.d_all.copy_(self.d_result)
+            _lib.check(self._lib.bcmpc_select_results_async(
+                ctypes.c_void_p(self.d_all.data_ptr()), max(1, self.size), self.maximize,
+                ctypes.c_void_p(self.d_best.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
+            self.h_best.copy_(self.d_best, non_blocking=True)
+        stream.synchronize()
+        raw = self.h_best.numpy()
+        index = int(raw[:8].view(np.int64)[0])
+        cost = float(raw[8:16].view(np.float64)[0])
+        return cost, index, raw[16:].view(np.float64).copy()
+
+
+def ctypes_sizeof_result() -> int:
+    import ctypes
+    from . import _lib
+    return ctypes.sizeof(_lib.Result)
+
+
 def allgather_result(d_result, action_dim: int, maximize: bool = False, group=None) -> Tuple[float, int, np.ndarray]:
     """The torch-side form of the exchange (gloo rehearsals; nccl without the library communicator):
     ``d_result`` is this rank's ``bcmpc_result``

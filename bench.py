@@ -17,10 +17,17 @@ reference's RNG contract (rng="numpy": exactly the np.random.uniform(size=
 the first action taken from that array) at the same K and H -- the
 drop-in's latency including the draw.
 
-Multi-GPU (driver: torch.distributed.run, one rank per GPU): weak scaling --
-each rank owns K candidates of its own (global K = N*K); per step every rank
-runs its shard and the ranks agree on the global argmin through one
-all-gather of the 144-byte result records.  Rank 0 prints ONE JSON line.
+Multi-GPU: ``--gpus N`` runs N ranks, one per GPU -- started by the driver's
+torch.distributed.run (WORLD_SIZE must equal N), or, without WORLD_SIZE, by
+this script itself (a child torch.distributed.run, before any GPU call).
+Strong scaling on the north_star point by default: the workload's K is the
+GLOBAL K (cfg3: K = 65,536, H = 20, split contiguously, 65,536 / N per GPU);
+per step every rank runs its shard and the ranks agree on the global argmin
+through ONE all-gather of the 144-byte result records, reduced on the device
+(distributed.RecordExchange).  ``scale`` adds BASELINE's other global configs
+at the same N (cfg4: K = 262,144; cfg5: K = 65,536 with CEM x4) and cfg3
+weak-scaled.  Rank 0 prints ONE JSON line; its ``summary`` key (last) holds
+every line's value / p50 / roofline fraction.
 """
 from __future__ import annotations
 
@@ -41,6 +48,7 @@ WORKLOADS = {
     "cfg2": dict(K=4096, H=20, hidden=500, L=2, act="tanh"),
     "cfg3": dict(K=65536, H=20, hidden=500, L=2, act="tanh"),
     "cfg4_shard": dict(K=32768, H=20, hidden=500, L=2, act="tanh"),   # 262144 / 8 per GPU
+    "ns_shard": dict(K=8192, H=20, hidden=500, L=2, act="tanh"),      # the north_star's per-GPU shard: 65536 / 8
     "cfg3_relu": dict(K=65536, H=20, hidden=500, L=2, act="relu"),    # diagnostic: no tanh
     # diagnostics: cfg2's net at other K (the multi-column team kernel's auto bound)
     "k2048": dict(K=2048, H=20, hidden=500, L=2, act="tanh"),
@@ -164,7 +172,9 @@ def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explor
     short = per_call * threads < 0.1 * budget_s          # (small K: many 1-thread calls, not one)
     with threadpool_limits(limits=1, user_api="blas"):
         v1, calls1, el1 = timed(K1, budget_s / 2 if short else 0.0, max_calls=(1 << 30) if short else 1)
-    best_pool = v >= v1
+    # the 1-thread figure replaces the pool's only when it was measured at the same K (an extrapolation from
+    # a smaller K sample is kept in the record, never promoted to `value`)
+    best_pool = v >= v1 or K1 < Ks
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -172,9 +182,10 @@ def cpu_baseline(spec_w, norm, state, H, budget_s, K_full, net, pol=None, explor
     return dict(value=v if best_pool else v1, unit="candidate-steps/s", cores=int(threads) if best_pool else 1,
                 kind="port", K_sampled=Ks if best_pool else K1,
                 value_pool=v, pool_threads=int(threads), K_sampled_pool=Ks,
-                value_1thread=v1, K_sampled_1thread=K1, cpu_model=_cpu_model(), host_cpus=os.cpu_count(),
+                value_1thread=v1, K_sampled_1thread=K1, value_1thread_extrapolated=K1 < Ks, cpu_model=_cpu_model(), host_cpus=os.cpu_count(),
                 affinity_cpus=aff, omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
-                threads_note=("value/cores = the faster of the BLAS pool and 1 thread per candidate-step; the "
+                threads_note=("value/cores = the faster of the BLAS pool and 1 thread per candidate-step, the 1-thread "
+                              "figure only when sampled at the same K (value_1thread_extrapolated otherwise); the "
                               "pool size is OMP_NUM_THREADS (the GPU box's CPU share per GPU), not host_cpus"),
                 sample=f"{calls} oracle get_action calls at K={Ks} (workload K={K_full}), H={H}, {net}, "
                        f"OpenBLAS {threads} threads, {el:.1f} s; 1 thread: {calls1} call(s) at K={K1}, {el1:.1f} s"
@@ -344,9 +355,11 @@ def synthetic_problem(wl):
                 gamma=float(wl.get("gamma", 1.0)), policy=policy, pol_arrays=pol_arrays)
 
 
-def make_engine(wl, prob, device, precision):
+def make_engine(wl, prob, device, precision, K=None):
+    """The workload's engine; ``K``: this rank's shard size (default: the workload's K)."""
     from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
-    K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
+    H, hidden, L, act = wl["H"], wl["hidden"], wl["L"], wl["act"]
+    K = wl["K"] if K is None else int(K)
     if prob["policy"]:
         ph, pl = prob["policy"]
         eng = RolloutEngine(S_DIM, A_DIM, hidden, L, act, prob["ln"], H, K, device=device, policy_hidden=ph,
@@ -664,12 +677,338 @@ def f16_line(wl, prob, device, steps=50, warmup=5, name="cfg3"):
                                  "regret_unit": "split-engine cost of the f16 choice minus its minimum"}}
 
 
+def launch_plan(gpus, environ):
+    """How this invocation gets its ranks (the driver's ``--gpus N`` contract):
+
+    * ``"ranks"``  -- WORLD_SIZE is set (torch.distributed.run started this process): it must equal
+      ``--gpus`` (a mismatch exits non-zero before anything is measured);
+    * ``"single"`` -- ``--gpus 1`` and no WORLD_SIZE: one rank, no process group;
+    * ``"spawn"``  -- ``--gpus N > 1`` and no WORLD_SIZE: this process starts the N ranks itself as a
+      child ``torch.distributed.run`` (127.0.0.1, a free port) before it touches the GPU, waits for it
+      and exits with its status (never an exec of this process)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    ws = environ.get("WORLD_SIZE", "")
+    if ws != "":
+        if int(ws) != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}: the launcher and the flag disagree")
+        return "ranks"
+    return "single" if gpus == 1 else "spawn"
+
+
+def spawn_command(n, argv, port):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(n, argv):
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, BCMPC_BENCH_LAUNCHER="bench.py --gpus (child torch.distributed.run)")
+    return subprocess.run(spawn_command(n, argv, port), env=env).returncode
+
+
+def workload_shard(K_wl, rank, world, scaling):
+    """This rank's contiguous global candidate range (lo, hi) and the global K.
+    strong: the workload's K is the GLOBAL K, split as distributed.shard_range splits it (the first K % N
+    ranks one more; the north_star point: K = 65,536 over N GPUs); weak: every rank owns K_wl candidates
+    of its own (global N * K_wl)."""
+    if scaling == "weak":
+        return rank * K_wl, (rank + 1) * K_wl, K_wl * world
+    base, rem = divmod(int(K_wl), int(world))
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0), int(K_wl)
+
+
+class RankCtx:
+    """One rank's view: world / rank / device, the process group's backend, and the two primitives the
+    timed loops need (barrier; max over ranks)."""
+
+    def __init__(self, world, rank, local, backend):
+        import torch
+        self.world, self.rank, self.local, self.backend = world, rank, local, backend
+        self.dev = torch.device("cuda", local)
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def allreduce(self, v, op="max"):
+        if self.world == 1:
+            return float(v)
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.dev if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+        return float(t.item())
+
+    def ranks(self):
+        if self.world == 1:
+            return 1
+        import torch.distributed as dist
+        return dist.get_world_size()
+
+
+def timed_loop(ctx, step, steps, warmup, kernel_ms=None):
+    """W untimed steps, then EXACTLY ``steps`` steps bracketed by a barrier + device synchronisation on
+    both sides; the wall time is the max over ranks.  ``kernel_ms``: read after each step (HIP events of
+    the rollout launch on its stream)."""
+    import torch
+    for i in range(warmup):
+        step(i)
+    ctx.barrier()
+    torch.cuda.synchronize(ctx.dev)
+    ts, ks = [], []
+    t0 = time.perf_counter()
+    for i in range(steps):
+        t1 = time.perf_counter()
+        step(warmup + i)
+        ts.append(time.perf_counter() - t1)
+        if kernel_ms is not None:
+            ks.append(kernel_ms())
+    torch.cuda.synchronize(ctx.dev)
+    ctx.barrier()
+    elapsed = ctx.allreduce(time.perf_counter() - t0, "max")
+    return elapsed, ts, ks
+
+
+def rollout_stepper(ctx, eng, state, lo, maximize, lib_comm=None):
+    """One complete control step of a plain random-shooting workload on this rank's shard [lo, lo + K):
+    1 rank -- bcmpc_get_action (state in the kernel arguments, in-kernel Philox actions, rollout + argmin,
+    the result in mapped host memory, one synchronisation); N ranks -- the state H2D, bcmpc_rollout_async
+    (result record on the device), then distributed.RecordExchange: one torch all-gather of the 144-byte
+    records (RCCL over xGMI) + the library's device select + one D2H (or, with the library communicator
+    attached -- BCMPC_LIBRARY_COMM=1 -- bcmpc_get_action with the exchange inside the library).
+    Returns (step(i) -> (cost, index, first_action), carrier description)."""
+    import torch
+    if ctx.world == 1 or lib_comm is not None:
+        def step(i):
+            res = eng.get_action(state, None, seed=0xB0B + i, cand_offset=lo)
+            return res.best_cost, res.best_index, res.first_action
+        return step, ("none (1 rank)" if ctx.world == 1 else
+                      "libbcmpc RCCL all-gather of the 144-byte result records + device np.argmin select, in "
+                      "get_action (bcmpc_engine_set_comm)")
+    from bc_mpc_amd import distributed as bdist
+    ex = bdist.RecordExchange(ctx.local, maximize=maximize)
+    h_state = torch.zeros(len(state), dtype=torch.float64).pin_memory()
+    hs = h_state.numpy()
+    d_state = torch.zeros(len(state), dtype=torch.float64, device=ctx.dev)
+    d_costs = torch.empty(max(1, eng.num_paths), dtype=torch.float64, device=ctx.dev)
+    stream = torch.cuda.current_stream(ctx.dev)
+
+    def step(i):
+        np.copyto(hs, state)
+        with torch.cuda.stream(stream):
+            d_state.copy_(h_state, non_blocking=True)
+        eng.rollout_async(d_state.data_ptr(), 0, None, 0xB0B + i, lo, d_costs.data_ptr(), None,
+                          ex.d_result.data_ptr(), stream.cuda_stream)
+        return ex.exchange(stream)
+    carrier = (f"torch {ctx.backend} all_gather_into_tensor of the 144-byte bcmpc_result records "
+               f"({'RCCL over xGMI' if ctx.backend == 'nccl' else 'host memory'}) + bcmpc_select_results_async "
+               "(device np.argmin select) + one D2H (distributed.RecordExchange)")
+    return step, carrier
+
+
+def cem_stepper(ctx, eng, wl, prob, lo, hi, K_global):
+    """One CEMcontroller.get_action (cfg5): 1 rank -- bcmpc_cem_get_action (all iterations on the device);
+    N ranks -- cem.cem_multi_rank over this rank's shard (per iteration one all-gather of the local top-E
+    records, then the same global elite select + refit on every rank; one final min-loc)."""
+    import torch
+    from bc_mpc_amd.cem import cem_multi_rank
+    cem = wl["cem"]
+    H = wl["H"]
+    iters = cem["iterations"]
+    n_elite = max(1, int(round(cem["elite_frac"] * K_global)))
+    mu0, sd0 = np.zeros((H, A_DIM)), np.full((H, A_DIM), 0.5)
+    stream = torch.cuda.current_stream(ctx.dev)
+
+    class _Shard:                                       # cem._EngineShard around this engine
+        device = ctx.dev
+
+        def rollout(self, d_state, d_mu, d_sigma, seed, it, lo_, k_global, d_costs, d_res, merge):
+            eng.cem_rollout_async(d_state.data_ptr(), d_mu.data_ptr(), d_sigma.data_ptr(), seed, it, lo_,
+                                  k_global, d_costs.data_ptr(), d_res.data_ptr(), merge, stream.cuda_stream)
+
+        def check_status(self):
+            eng.check_status()
+
+        def select(self, d_pairs, d_costs, m, index_base, n, d_out, d_count):
+            eng.select_async(d_pairs.data_ptr() if d_pairs is not None else None,
+                             d_costs.data_ptr() if d_costs is not None else None, m, index_base, n,
+                             d_out.data_ptr(), d_count.data_ptr(), stream.cuda_stream)
+
+        def refit(self, d_elite, d_count, seed, it, alpha, d_mu, d_sigma):
+            eng.cem_refit_async(d_elite.data_ptr(), d_count.data_ptr(), seed, it, alpha, d_mu.data_ptr(),
+                                d_sigma.data_ptr(), stream.cuda_stream)
+
+    def step(i):
+        if ctx.world == 1:
+            res, _, _ = eng.cem_get_action(prob["state"], mu0, sd0, iters, n_elite, cem["alpha"], 0xB0B + i)
+            return res.best_cost, res.best_index, res.first_action
+        return cem_multi_rank(_Shard(), prob["state"], mu0, sd0, iters, n_elite, cem["alpha"], 0xB0B + i, lo, hi,
+                              K_global, A_DIM, prob["reward"])[:3]
+    carrier = ("none (1 rank)" if ctx.world == 1 else
+               f"torch {ctx.backend} all_gather of the local top-{n_elite} (cost, index) records per CEM iteration "
+               "+ one final min-loc all-gather")
+    return step, n_elite, carrier
+
+
+def scale_line(ctx, name, K_global, steps, warmup, precision="auto", scaling="strong"):
+    """A BASELINE config at this run's N (every rank takes part; rank 0 keeps the record): the global K split
+    over the ranks (strong) or K per rank (weak), the same timed loop as the headline, value = the
+    candidate-steps ALL ranks processed / the max-over-ranks wall time."""
+    wl = dict(WORKLOADS[name], K=K_global)
+    prob = synthetic_problem(wl)
+    lo, hi, Kg = workload_shard(K_global, ctx.rank, ctx.world, scaling)
+    eng = make_engine(wl, prob, ctx.local, precision, K=hi - lo)
+    eng.set_timing(True)
+    cem = wl.get("cem")
+    iters = cem["iterations"] if cem else 1
+    if cem:
+        step, n_elite, carrier = cem_stepper(ctx, eng, wl, prob, lo, hi, Kg)
+        kms = (lambda: eng.last_kernel_ms()[0]) if ctx.world == 1 else None
+    else:
+        step, carrier = rollout_stepper(ctx, eng, prob["state"], lo, prob["reward"])
+        kms = lambda: eng.last_kernel_ms()[0]          # noqa: E731
+    el, ts, ks = timed_loop(ctx, step, steps, warmup, kms)
+    H = wl["H"]
+    fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
+    # (multi-rank CEM: the HIP events see one pass at a time; the per-rank device share is the step's wall)
+    kern = float(np.mean(ks)) if ks else float(np.median(ts) * 1e3)
+    kern = ctx.allreduce(kern, "max")
+    row = {"K_global": Kg, "K_per_gpu": hi - lo, "H": H, "scaling": scaling, "ranks": ctx.ranks(),
+           "value": Kg * H * iters * steps / el, "unit": "candidate-steps/s", "steps": steps,
+           "ms_per_step": el / steps * 1e3, "p50_ms": float(np.median(ts) * 1e3),
+           "kernel": eng.info()["layout"], "precision": eng.precision,
+           "kernel_ms": kern, "collective": carrier,
+           "roofline": roofline_line(hi - lo, H, fpcs, kern, eng.precision, iters=iters)}
+    row["roofline"]["per"] = "the slowest rank's shard launch (max over ranks)"
+    if cem:
+        row["cem"] = dict(cem, n_elite=n_elite)
+    eng.close()
+    return row
+
+
+def exchange_cost(device, K=8192, H=20, calls=200, warmup=20, n_rec=8):
+    """The N > 1 exchange's cost on ONE card at the north_star shard (K = 8192 per GPU of K = 65,536 over 8,
+    H = 20, 2x500 tanh), the wire itself excepted (one GPU cannot all-gather with itself; the 144-byte
+    all-gather over xGMI is the part SCALE measures): per control step p50, for
+    * ``get_action``: the 1-rank step (bcmpc_get_action, result in mapped host memory);
+    * ``host_staged``: the controller's default N > 1 tail (distributed.allgather_minloc): the result on
+      the host, its record up to the device, ``n_rec`` records back down (the gathered buffer's D2H) and
+      the host select (bcmpc_select_results);
+    * ``device_select``: the bench's N > 1 tail (distributed.RecordExchange): state H2D, rollout_async with
+      the record on the device, the ``n_rec`` records (a device copy standing in for the gather) reduced by
+      bcmpc_select_results_async, one D2H.
+    The overheads are the p50 differences to ``get_action``."""
+    import ctypes
+    import torch
+    from bc_mpc_amd import _lib
+    from bc_mpc_amd import distributed as bdist
+    wl = dict(WORKLOADS["ns_shard"], K=K, H=H)
+    prob = synthetic_problem(wl)
+    state = prob["state"]
+    eng = make_engine(wl, prob, device, "auto")
+    dev = torch.device("cuda", device)
+    stream = torch.cuda.current_stream(dev)
+    lib = _lib.load()
+    nb = ctypes.sizeof(_lib.Result)
+
+    def p50(fn):
+        for i in range(warmup):
+            fn(i)
+        ts = []
+        for i in range(calls):
+            t0 = time.perf_counter()
+            fn(warmup + i)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts) * 1e3)
+
+    def ga(i):
+        return eng.get_action(state, None, seed=0xE0 + i)
+
+    def host_staged(i):
+        r = eng.get_action(state, None, seed=0xE0 + i)
+        rec = np.zeros(3 + A_DIM)
+        rec[0], rec[1], rec[2], rec[3:] = 1.0, r.best_cost, float(r.best_index), r.first_action
+        t = torch.from_numpy(rec).to(dev)
+        out = t.repeat(n_rec)                           # (the gathered buffer: n_rec records on the device)
+        recs = out.view(n_rec, rec.size).cpu().numpy()
+        return bdist.select(recs)
+
+    d_state = torch.zeros(S_DIM, dtype=torch.float64, device=dev)
+    h_state = torch.zeros(S_DIM, dtype=torch.float64).pin_memory()
+    d_costs = torch.empty(K, dtype=torch.float64, device=dev)
+    d_res = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    d_all = torch.zeros(n_rec * nb, dtype=torch.uint8, device=dev)
+    d_best = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    h_best = torch.zeros(nb, dtype=torch.uint8).pin_memory()
+
+    def device_select(i):
+        np.copyto(h_state.numpy(), state)
+        d_state.copy_(h_state, non_blocking=True)
+        eng.rollout_async(d_state.data_ptr(), 0, None, 0xE0 + i, 0, d_costs.data_ptr(), None, d_res.data_ptr(),
+                          stream.cuda_stream)
+        d_all.view(n_rec, nb).copy_(d_res.view(1, nb).expand(n_rec, nb))
+        _lib.check(lib.bcmpc_select_results_async(ctypes.c_void_p(d_all.data_ptr()), n_rec, 0,
+                                                  ctypes.c_void_p(d_best.data_ptr()),
+                                                  ctypes.c_void_p(stream.cuda_stream)))
+        h_best.copy_(d_best, non_blocking=True)
+        stream.synchronize()
+        return int(h_best.numpy()[:8].view(np.int64)[0])
+
+    # the three tails pick the same winner
+    assert device_select(7) == ga(7).best_index == int(host_staged(7)[2])
+    out = {"K": K, "H": H, "records": n_rec, "get_action_p50_ms": p50(ga), "host_staged_p50_ms": p50(host_staged),
+           "device_select_p50_ms": p50(device_select), "calls": calls}
+    out["host_staged_overhead_us"] = (out["host_staged_p50_ms"] - out["get_action_p50_ms"]) * 1e3
+    out["device_select_overhead_us"] = (out["device_select_p50_ms"] - out["get_action_p50_ms"]) * 1e3
+    out["note"] = ("one card: the all-gather's wire time is not included (SCALE's N > 1 lines carry it); "
+                   "host_staged = distributed.allgather_minloc's tail, device_select = distributed.RecordExchange")
+    eng.close()
+    return out
+
+
+def summary_of(out):
+    """value / p50_ms / roofline.frac of every line, compact, printed LAST in the JSON line so the driver's
+    stdout tail keeps it."""
+    def pick(d):
+        if not isinstance(d, dict):
+            return None
+        r = {k: d[k] for k in ("value", "p50_ms", "ms_per_step") if isinstance(d.get(k), (int, float))}
+        if isinstance(d.get("roofline"), dict) and "frac" in d["roofline"]:
+            r["frac"] = round(float(d["roofline"]["frac"]), 4)
+        for k in ("value", "p50_ms", "ms_per_step"):
+            if k in r:
+                r[k] = float(f"{r[k]:.4g}")
+        return r or None
+    s = {"headline": pick(out)}
+    for key in ("cfg2", "ns_shard", "cfg4_shard", "cfg5", "f16_single_pass"):
+        if out.get(key):
+            s[key] = pick(out[key])
+    for key, row in (out.get("scale") or {}).items():
+        s["scale." + key] = pick(row)
+    for key, row in (out.get("small_k") or {}).items():
+        s["small_k." + key] = pick(row)
+    if out.get("library_comm"):
+        s["library_comm"] = pick(out["library_comm"]) or out["library_comm"].get("status")
+    return s
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE, N > 1 starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default): the workload's K is the GLOBAL K split over the ranks (cfg3: the "
+                         "north_star point, K=65536 over N GPUs); weak: K per rank")
     ap.add_argument("--actions", default="device", choices=["hbm", "device"],
                     help="device: a complete get_action with in-kernel Philox actions (host state in, host result "
                          "out); hbm: the rollout alone on a [H,K,A] f64 action array resident in HBM (A/B)")
@@ -686,10 +1025,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cfg2", action="store_true", help="skip the cfg2 line (BASELINE configs[1], K=4096)")
     ap.add_argument("--no-extra", action="store_true",
-                    help="skip the cfg4_shard and cfg5 lines (BASELINE configs[3] per-GPU shard, configs[4] on 1 GPU)")
+                    help="skip the ns_shard, cfg4_shard and cfg5 lines (the north_star's and configs[3]'s per-GPU "
+                         "shards, configs[4] on 1 GPU)")
+    ap.add_argument("--no-scale", action="store_true",
+                    help="skip the `scale` lines (cfg4 at K_global=262144, cfg5 at K_global=65536, cfg3 weak) "
+                         "that every N measures over all its ranks")
     ap.add_argument("--no-small-k", action="store_true",
                     help="skip the small-K get_action lines (ppo_defaults, runsh_recipe, cfg1: team vs slab kernel)")
     args = ap.parse_args()
+
+    plan = launch_plan(args.gpus, os.environ)
+    if plan == "spawn":                                # before any GPU call: N ranks in a child launcher
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -706,22 +1053,22 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    ctx = RankCtx(world, rank, local, backend)
 
     from bc_mpc_amd import distributed as bdist
-    from bc_mpc_amd.engine import MLPSpec, PolicySpec, RolloutEngine
-    import bc_mpc_amd._lib as L_
 
     wl = WORKLOADS[args.workload]
-    K, H, hidden, L, act = wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"]
-    offset = rank * K                                  # (precision "auto": the engine's rule, engine.py)
+    H, hidden, L, act = wl["H"], wl["hidden"], wl["L"], wl["act"]
+    lo, hi, K_global = workload_shard(wl["K"], rank, world, args.scaling)
+    K = hi - lo                                        # this rank's shard (precision "auto": engine.py's rule)
 
     prob = synthetic_problem(wl)
     kernels, biases, ln_g, ln_b, norm, state = (prob[k] for k in ("kernels", "biases", "ln_g", "ln_b", "norm", "state"))
-    reward, ln, model, cost, gamma, policy, pol_arrays = (prob[k] for k in ("reward", "ln", "model", "cost", "gamma",
-                                                                            "policy", "pol_arrays"))
-    eng = make_engine(wl, prob, local, args.precision)
+    reward, ln, gamma, policy, pol_arrays = (prob[k] for k in ("reward", "ln", "gamma", "policy", "pol_arrays"))
+    eng = make_engine(wl, prob, local, args.precision, K=K)
     eng.set_timing(True)                               # the roofline's HIP events inside the timed region
     info = eng.info()
     kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
@@ -736,103 +1083,61 @@ def main():
             and os.environ.get("BCMPC_LIBRARY_COMM", "0") == "1"):
         # opt-in (BCMPC_LIBRARY_COMM=1): the library's own communicator -- get_action all-gathers the ranks'
         # result records over RCCL and selects on the device (csrc/comm.hip); torch.distributed only carried
-        # its RCCL id.  Default: the torch all-gather of the records (allgather_minloc)
+        # its RCCL id.  Default: distributed.RecordExchange (torch all-gather + device select)
         lib_comm = bdist.LibraryComm(local)
         eng.set_comm(lib_comm)
-    d_state = torch.from_numpy(state).to(dev)
-    d_actions = None
-    if args.actions == "hbm":
+    cem = wl.get("cem")
+    iters = cem["iterations"] if cem else 1
+    n_elite = None
+    if cem:
+        step, n_elite, carrier = cem_stepper(ctx, eng, wl, prob, lo, hi, K_global)
+    elif args.actions == "device":
+        step, carrier = rollout_stepper(ctx, eng, state, lo, reward, lib_comm)
+    else:
+        # A/B: the rollout alone on a resident [H, K, A] f64 action array, the exchange as above
+        d_state = torch.from_numpy(state).to(dev)
         host = np.random.RandomState(1234 + rank).uniform(-1, 1, (H, K, A_DIM))
         d_actions = torch.from_numpy(host).to(dev)
         del host
-    d_costs = torch.empty(K, dtype=torch.float64, device=dev)
-    d_res = torch.zeros(__import__("ctypes").sizeof(L_.Result), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    cem = wl.get("cem")
-    iters = cem["iterations"] if cem else 1
-    if cem:
-        from bc_mpc_amd.cem import cem_multi_rank
-        n_elite = max(1, int(round(cem["elite_frac"] * K * world)))
-        mu0, sd0 = np.zeros((H, A_DIM)), np.full((H, A_DIM), 0.5)
+        d_costs = torch.empty(K, dtype=torch.float64, device=dev)
+        ex = bdist.RecordExchange(local, maximize=reward)
+        stream = torch.cuda.current_stream(dev)
 
-        class _Shard:                                   # cem._EngineShard around this engine
-            device = dev
+        def step(i):
+            eng.rollout_async(d_state.data_ptr(), 0, d_actions.data_ptr(), 0xB0B + i, lo, d_costs.data_ptr(), None,
+                              ex.d_result.data_ptr(), stream.cuda_stream)
+            return ex.exchange(stream)
+        carrier = "none (1 rank)" if world == 1 else f"torch {backend} all-gather + device select"
 
-            def rollout(self, d_state, d_mu, d_sigma, seed, it, lo, k_global, d_costs, d_res, merge):
-                eng.cem_rollout_async(d_state.data_ptr(), d_mu.data_ptr(), d_sigma.data_ptr(), seed, it, lo,
-                                      k_global, d_costs.data_ptr(), d_res.data_ptr(), merge, stream.cuda_stream)
+    kms = (lambda: eng.last_kernel_ms()[0]) if not (cem and world > 1) else None
+    elapsed, step_s, kern_ms = timed_loop(ctx, step, args.steps, args.warmup, kms)
 
-            def select(self, d_pairs, d_costs, m, index_base, n, d_out, d_count):
-                eng.select_async(d_pairs.data_ptr() if d_pairs is not None else None,
-                                 d_costs.data_ptr() if d_costs is not None else None, m, index_base, n,
-                                 d_out.data_ptr(), d_count.data_ptr(), stream.cuda_stream)
-
-            def refit(self, d_elite, d_count, seed, it, alpha, d_mu, d_sigma):
-                eng.cem_refit_async(d_elite.data_ptr(), d_count.data_ptr(), seed, it, alpha, d_mu.data_ptr(),
-                                    d_sigma.data_ptr(), stream.cuda_stream)
-
-    def cem_step(i):
-        if world == 1:
-            res, _, _ = eng.cem_get_action(state, mu0, sd0, iters, n_elite, cem["alpha"], 0xB0B + i)
-            return res
-        return cem_multi_rank(_Shard(), state, mu0, sd0, iters, n_elite, cem["alpha"], 0xB0B + i, offset,
-                              offset + K, K * world, A_DIM, reward)
-
-    def step(i):
-        if cem:
-            return cem_step(i)
-        if d_actions is None:
-            # the complete control step: state H2D, device-drawn actions, rollout, argmin, result D2H
-            res = eng.get_action(state, None, seed=0xB0B + i, cand_offset=offset)
-            if world == 1 or lib_comm is not None:     # (with the communicator: already the global best)
-                return res.best_cost, res.best_index, res.first_action
-            sign = -1.0 if reward else 1.0              # learned reward: argmax == argmin of -r
-            return bdist.allgather_minloc(True, sign * res.best_cost, res.best_index, res.first_action, A_DIM,
-                                          device=local)
-        eng.rollout_async(d_state.data_ptr(), 0, d_actions.data_ptr(), 0xB0B + i, offset, d_costs.data_ptr(), None,
-                          d_res.data_ptr(), stream.cuda_stream)
-        # the min-loc exchange straight from the device result (stream-ordered after the argmin
-        # launch), then one D2H of the gathered records (argmax for the learned reward)
-        return bdist.allgather_result(d_res, A_DIM, maximize=reward)
-
-    for i in range(args.warmup):
-        step(i)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    kern_ms, step_s = [], []
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ts = time.perf_counter()
-        step(args.warmup + i)
-        step_s.append(time.perf_counter() - ts)
-        kern_ms.append(eng.last_kernel_ms()[0] if not (cem and world > 1) else float("nan"))
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    scale = None
+    if not args.no_scale and args.workload == "cfg3" and args.scaling == "strong":
+        # BASELINE's global configs at this N (every rank takes part): configs[3] K=262144, configs[4]
+        # K=65536 CEM x4, and cfg3 weak-scaled (65536 per GPU; at N=1 the headline itself)
+        scale = {"cfg4": scale_line(ctx, "cfg4_shard", 262144, steps=10, warmup=2),
+                 "cfg5": scale_line(ctx, "cfg5", 65536, steps=3, warmup=1)}
+        scale["cfg3_weak"] = (scale_line(ctx, "cfg3", 65536, steps=20, warmup=3, scaling="weak") if world > 1 else
+                              "= the headline (N=1)")
 
     lib_line = None
     if world > 1 and lib_comm is None and not cem and args.actions == "device":
-        lib_line = library_comm_line(eng, state, offset, K, H, args.steps, args.warmup, world, local, backend)
+        lib_line = library_comm_line(eng, state, lo, K, H, args.steps, args.warmup, world, local, backend)
 
     dropin = None
     if args.dropin_calls > 0 and not (cem or policy or reward):
-        dropin = dropin_parity_p50(K * world, H, hidden, L, act, ln, kernels, biases, ln_g, ln_b, norm, state,
+        dropin = dropin_parity_p50(K_global, H, hidden, L, act, ln, kernels, biases, ln_g, ln_b, norm, state,
                                    local, args.dropin_calls, world)
 
-    total_cand_steps = K * world * H * iters * args.steps
-    value = total_cand_steps / elapsed
+    value = K_global * H * iters * args.steps / elapsed
     fpcs = flop_per_cand_step(hidden, L, policy=policy, reward=reward)
     if cem and world > 1:                              # per-launch device time: the wall-clock share
         kern_ms = [t * 1e3 for t in step_s]
-    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    kern_avg_s = ctx.allreduce(float(np.mean(kern_ms)), "max") / 1e3
     peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16": F16_MFMA_PEAK_TFLOPS}.get(eng.precision, SPLIT_PEAK_TFLOPS)
     achieved_tflops = K * H * iters * fpcs / kern_avg_s / 1e12
+    ns = args.workload == "cfg3" and args.scaling == "strong"
     out = {
         "metric": "candidate-steps/sec (K x H per get_action), HalfCheetah dims",
         # CEM workloads count every iteration's K x H candidate-steps (iterations x K x H per get_action)
@@ -843,13 +1148,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": {"fp32": "f32", "f16": "f16 (one MFMA pass, f32 accumulate; not the fp32 tolerance)"}.get(
             eng.precision, "f32 (hi/lo f16 split operands, 3 MFMA passes, f32 accumulate)"),
         "data": f"synthetic (HalfCheetah dims s=20,a=6; random-init {'two-head reward net' if reward else 'dynamics MLP'}; "
                 f"actions {'resident in HBM as [H,K,6] f64, rollout only' if args.actions == 'hbm' else 'drawn in-kernel (Philox); step = complete get_action, host state in, host result out'})",
-        "config": {"workload": f"{args.workload}: K={K}/GPU (global {K * world}), H={H}, "
+        "config": {"workload": ("north_star: " if ns else "") + f"{args.workload}: K_global={K_global} "
+                               + (f"({K} per GPU)" if args.scaling == "weak" else f"over {world} GPU(s), {K} on rank 0")
+                               + f", H={H}, "
                                + (f"reward net {hidden} trunk + 2x{hidden} heads tanh, argmax sum r*{gamma}^h"
                                   if reward else f"{L}x{hidden} {act}" + (" + LayerNorm" if ln else ""))
                                + (f" + fused policy {policy[1]}x{policy[0]} tanh "
@@ -860,12 +1167,11 @@ def main():
                                + (f", {world} ranks: 1 all-gather min-loc per step"
                                   + (" (+1 all-gather of the local top-E per CEM iteration)" if cem else "")
                                   if world > 1 else ", 1 GPU (no collective)"),
-                   "K_per_gpu": K, "K_global": K * world, "horizon": H, "hidden": hidden, "n_layers": L,
+                   "K_per_gpu": K, "K_global": K_global, "horizon": H, "hidden": hidden, "n_layers": L,
                    "activation": act, "actions": args.actions, "parallelism": f"candidate-shard x{world}",
-                   "collective": ("libbcmpc RCCL all-gather of the 144-byte result records + device np.argmin "
-                                  "select, in get_action (bcmpc_engine_set_comm)" if lib_comm is not None else
-                                  f"torch {backend} all_gather min-loc, {3 + A_DIM} f64 per rank per step")
-                   if world > 1 else "none (1 rank)"},
+                   "ranks": ctx.ranks(), "launcher": os.environ.get("BCMPC_BENCH_LAUNCHER", "external" if world > 1
+                                                                    else "none (1 rank)"),
+                   "collective": carrier},
         "p50_ms": float(np.percentile(step_s, 50) * 1e3),
         "dropin_parity_p50_ms": dropin["p50_ms"] if dropin else None,
         "dropin_parity": dropin if dropin else "n/a (MPCcontroller drop-in is timed for the plain delta-net "
@@ -881,19 +1187,22 @@ def main():
                      "kernel": kernel_name + (" x CEM iterations + select/refit (HIP events around the "
                                               "whole device-side CEM call)" if cem else ""),
                      "flop_per_launch": K * H * fpcs,
-                     "flop_per_cand_step": fpcs},
+                     "flop_per_cand_step": fpcs,
+                     "per": "one rank's shard launch (the slowest rank's, max over ranks)"},
         "cpu_baseline": None,
         "small_k": None,
     }
+    if scale is not None:
+        out["scale"] = scale
     if lib_line is not None:
         out["library_comm"] = lib_line
     # PMC HBM traffic per launch of THIS round's kernels (tools/gpu_validate.sh traffic: rocprofv3 --pmc FETCH_SIZE /
-    # WRITE_SIZE in separate passes, the gfx950 FETCH_SIZE x2 correction calibrated on the action tensor)
+    # WRITE_SIZE in separate passes, the gfx950 FETCH_SIZE x2 correction calibrated on the action tensor); the
+    # measured launch is the 1-GPU one, so the N > 1 shard (a smaller K) has none
     prof = os.path.join(REPO, "profiles", TRAFFIC_FILE)
     out["roofline"]["traffic_source"] = f"profiles/{TRAFFIC_FILE}"
-    if os.path.exists(prof):
+    if os.path.exists(prof) and world == 1:
         try:
-            # PMC traffic of this kernel in this action mode (device: Philox actions in-kernel, hbm: read)
             key = args.workload + {"fp32": "", "f16": ":f16"}.get(eng.precision, ":split") + \
                 (":device" if args.actions == "device" else "")
             tr = json.load(open(prof)).get(key)
@@ -904,23 +1213,22 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import mpc_oracle as orc
         w = orc.RewardMLPWeights(kernels, biases, ln_g, ln_b) if reward else orc.MLPWeights(kernels, biases, act, ln_g, ln_b)
-        net = (f"reward net {hidden}" if reward else f"{L}x{hidden} {act}" + (" + LN" if ln else "")) + \
-            (f" + policy {policy}" if policy else "")
-        if policy and wl.get("policy_mode") == "stochastic":
-            net += " (oracle policy in its deterministic explore branch: TF's sampler is not restatable)"
-        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, net,
+        out["cpu_baseline"] = cpu_baseline(w, norm, state, H, args.cpu_baseline_seconds, K, net_label(wl, prob),
                                            pol_arrays, wl.get("explore", 0.5), gamma, cem)
     if rank == 0 and world == 1 and not args.no_small_k:
         out["small_k"] = small_k_lines(local, with_cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cfg2 and args.workload == "cfg3" and not args.no_small_k:
         out["cfg2"] = cfg2_line(local, with_cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_extra and args.workload == "cfg3":
+        out["ns_shard"] = workload_line("ns_shard", local, steps=50, warmup=5, with_cpu=not args.no_cpu_baseline)
+        out["ns_shard"]["exchange_cost"] = exchange_cost(local)
         out["cfg4_shard"] = workload_line("cfg4_shard", local, with_cpu=not args.no_cpu_baseline)
         out["cfg5"] = workload_line("cfg5", local, steps=5, warmup=1, cpu_seconds=4.0,
                                     with_cpu=not args.no_cpu_baseline)
     if (rank == 0 and world == 1 and not args.no_f16 and not (cem or policy or reward or ln) and act == "tanh"
             and eng.precision != "f16"):
         out["f16_single_pass"] = f16_line(wl, prob, local, name=args.workload)
+    out["summary"] = summary_of(out)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if lib_comm is not None:

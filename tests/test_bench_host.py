@@ -77,3 +77,64 @@ def test_cpu_baseline_record_and_thread_choice():
     assert rec["host_cpus"] == os.cpu_count()
     assert "OpenBLAS" in rec["sample"] and "1 thread" in rec["sample"]
     assert np.isfinite(rec["value"]) and rec["value"] > 0
+
+
+def test_launch_plan_follows_gpus_and_world_size():
+    # the driver's N=1 form and the self-launch form (no WORLD_SIZE)
+    assert bench.launch_plan(1, {}) == "single"
+    assert bench.launch_plan(8, {}) == "spawn"
+    assert bench.launch_plan(2, {"WORLD_SIZE": ""}) == "spawn"
+    # torch.distributed.run started us: WORLD_SIZE must equal --gpus
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}) == "ranks"
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}) == "ranks"
+    with pytest.raises(SystemExit, match="WORLD_SIZE=4 but --gpus 8"):
+        bench.launch_plan(8, {"WORLD_SIZE": "4"})
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {})
+
+
+def test_spawn_command_is_a_child_torchrun_on_loopback():
+    cmd = bench.spawn_command(4, ["--gpus", "4", "--steps", "3"], 29123)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29123" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
+def test_workload_shard_strong_splits_the_global_k(n):
+    """north_star: K = 65,536 GLOBAL over N ranks, contiguous, covering [0, K) once (distributed.shard_range);
+    configs[3]: 262,144 -> 32,768 per GPU at N = 8."""
+    from bc_mpc_amd.distributed import shard_range
+    for K in (65536, 262144, 1000):
+        parts = [bench.workload_shard(K, r, n, "strong") for r in range(n)]
+        assert parts[0][0] == 0 and parts[-1][1] == K
+        assert all(p[1] == q[0] for p, q in zip(parts, parts[1:]))
+        assert all(p[2] == K for p in parts)
+        assert [p[:2] for p in parts] == [shard_range(K, r, n) for r in range(n)]
+    assert bench.workload_shard(65536, 7, 8, "strong") == (57344, 65536, 65536)
+    assert bench.workload_shard(262144, 3, 8, "strong")[1] - bench.workload_shard(262144, 3, 8, "strong")[0] == 32768
+
+
+def test_workload_shard_weak_keeps_k_per_rank():
+    assert bench.workload_shard(65536, 0, 8, "weak") == (0, 65536, 524288)
+    assert bench.workload_shard(65536, 5, 8, "weak") == (5 * 65536, 6 * 65536, 524288)
+
+
+def test_summary_key_is_compact_and_covers_every_line():
+    out = {"value": 6.9e8, "p50_ms": 1.88, "ms_per_step": 1.9, "roofline": {"frac": 0.4591234},
+           "cfg2": {"value": 3.3e8, "p50_ms": 0.25, "roofline": {"frac": 0.25}},
+           "ns_shard": {"value": 5e8, "p50_ms": 0.33, "roofline": {"frac": 0.3}},
+           "scale": {"cfg4": {"value": 1e9, "ms_per_step": 5.0, "roofline": {"frac": 0.4}}, "cfg3_weak": "= the headline"},
+           "small_k": {"ppo_defaults": {"p50_ms": 0.047, "roofline": {"frac": 0.01}}}}
+    s = bench.summary_of(out)
+    assert s["headline"] == {"value": 6.9e8, "p50_ms": 1.88, "ms_per_step": 1.9, "frac": 0.4591}
+    assert s["small_k.ppo_defaults"]["p50_ms"] == 0.047
+    assert s["scale.cfg4"]["frac"] == 0.4 and s["scale.cfg3_weak"] is None
+    assert list(s)[0] == "headline" and "ns_shard" in s and "cfg2" in s
+
+
+def test_ns_shard_is_the_north_star_per_gpu_shard():
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    assert "K=65536" in base["north_star"] and "8" in base["north_star"]
+    ns = bench.WORKLOADS["ns_shard"]
+    assert ns["K"] * 8 == 65536 and ns["H"] == 20 and (ns["hidden"], ns["L"], ns["act"]) == (500, 2, "tanh")

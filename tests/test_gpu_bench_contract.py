@@ -1,7 +1,9 @@
 """bench.py's JSON line on the GPU box (the driver's contract): one short run of the headline workload and
 one of the CEM workload, in child processes, checked for the keys and the relations the driver and the
-judge read -- value = K*H*N*steps / wall time, ms_per_step, the roofline record (achieved / peak = frac,
-traffic from the committed PMC file), n_gpus 1, weak scaling."""
+judge read -- value = K*H*steps / wall time, ms_per_step, the roofline record (achieved / peak = frac,
+traffic from the committed PMC file), n_gpus 1, strong scaling on the north_star's global K -- and the
+self-launched 2-rank form (``--gpus 2`` without WORLD_SIZE: bench.py starts its own torch.distributed.run; gloo
+ranks sharing the one card) with the global K split over the ranks."""
 import json
 import os
 import subprocess
@@ -11,12 +13,16 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LEAN = ["--no-cpu-baseline", "--dropin-calls", "0", "--no-small-k", "--no-f16", "--no-cfg2", "--no-extra"]
+LEAN = ["--no-cpu-baseline", "--dropin-calls", "0", "--no-small-k", "--no-f16", "--no-cfg2", "--no-extra",
+        "--no-scale"]
 
 
-def _bench(*args):
+def _bench(*args, env=None):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
-                       timeout=240, cwd=REPO)
+                       timeout=240, cwd=REPO, env=e)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
@@ -28,11 +34,12 @@ def test_headline_line_contract():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 2 and d["scaling"] == "weak"
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 2 and d["scaling"] == "strong"
     assert d["higher_is_better"] is True and d["unit"] == "candidate-steps/s"
     K, H = d["config"]["K_per_gpu"], d["config"]["horizon"]
-    assert (K, H) == (65536, 20)
+    assert (K, H) == (65536, 20) and d["config"]["K_global"] == 65536 and d["config"]["ranks"] == 1
     assert d["value"] == pytest.approx(K * H / (d["ms_per_step"] / 1e3), rel=1e-6)
+    assert d["summary"]["headline"]["frac"] == pytest.approx(d["roofline"]["frac"], abs=1e-4)
     r = d["roofline"]
     assert r["bound"] == "mfma" and 0 < r["frac"] < 1
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
@@ -48,3 +55,20 @@ def test_cem_line_contract():
     # CEM: every iteration's candidate-steps count (4 rollout passes per get_action)
     assert d["value"] == pytest.approx(4 * K * H / (d["ms_per_step"] / 1e3), rel=1e-6)
     assert 0 < d["roofline"]["frac"] < 1
+
+
+def test_self_launched_two_ranks_split_the_global_k():
+    """``bench.py --gpus 2`` with no WORLD_SIZE starts the two ranks itself (gloo, both on this card): the
+    north_star's K = 65,536 is split 32,768 per rank, the record exchange ran over 2 ranks, and the scale
+    line's cfg4 is K_global = 262,144 over the same 2 ranks."""
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", *[a for a in LEAN if a != "--no-scale"],
+               env={"BCMPC_DIST_BACKEND": "gloo", "BCMPC_BENCH_DEVICE": "0"})
+    assert d["n_gpus"] == 2 and d["config"]["ranks"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["K_global"] == 65536 and d["config"]["K_per_gpu"] == 32768
+    assert "bench.py --gpus" in d["config"]["launcher"] and "RecordExchange" in d["config"]["collective"]
+    assert d["value"] == pytest.approx(65536 * 20 / (d["ms_per_step"] / 1e3), rel=1e-6)
+    c4 = d["scale"]["cfg4"]
+    assert c4["K_global"] == 262144 and c4["K_per_gpu"] == 131072 and c4["ranks"] == 2
+    c5 = d["scale"]["cfg5"]
+    assert c5["K_global"] == 65536 and c5["cem"]["n_elite"] == 6554 and c5["ranks"] == 2
+    assert d["scale"]["cfg3_weak"]["K_global"] == 131072
