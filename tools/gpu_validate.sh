@@ -8,13 +8,14 @@
 #     timed    kernel trace of the headline's timed launches only   -> $OUT/trace_timed/
 #     traffic  PMC FETCH_SIZE / WRITE_SIZE passes per workload      -> $OUT/traffic_*/
 #     issue    PMC issue / wait / memory-path passes over $PMC_ARGS -> $OUT/pmc_*/
-#     rehearse 2-rank gloo rehearsal of bench.py on the one card    -> $OUT/rehearsal.json
+#     rehearse 2-rank gloo rehearsal of bench.py on the one card, the ranks started by bench.py --gpus 2
+#              itself (no WORLD_SIZE: its child torch.distributed.run)  -> $OUT/rehearsal.json
 #     ab       tools/ab_libs.sh $AB_WL $AB_STEPS $AB_LIBS (AB_ARGS: extra bench arguments) -> $OUT/ab.txt
 #   TAG    output directory gpurun_out/$TAG
 # Every GPU step has its own time limit; the first failure (test failure included) stops the session.
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 OUT=$R/gpurun_out/$TAG
 STEPS=${STEPS:-"tests smoke bench trace"}
 TESTS=${TESTS:-tests}
@@ -25,7 +26,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 cd "$R"
 stop() { echo "stopping after $1 (rc=$2)"; exit "$2"; }
-LITE="--no-cpu-baseline --dropin-calls 0 --no-small-k --no-f16 --no-cfg2 --no-extra"
+LITE="--no-cpu-baseline --dropin-calls 0 --no-small-k --no-f16 --no-cfg2 --no-extra --no-scale"
 
 pmc_pass() {  # name, bench args, counters...
   local name=$1 args=$2; shift 2
@@ -53,7 +54,7 @@ for step in $STEPS; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_timed" -o run -- \
           python3 bench.py --steps 50 --warmup 5 $LITE $BENCH_ARGS > "$OUT/trace_timed.json" 2>&1 || stop timed $? ;;
     traffic)
-      for wl in ${TRAFFIC_WL:-cfg3:split cfg3:f16 cfg2:split cfg4_shard:split cfg5:split}; do
+      for wl in ${TRAFFIC_WL:-cfg3:split cfg3:f16 cfg2:split ns_shard:split cfg4_shard:split cfg5:split}; do
         w=${wl%%:*}; p=${wl##*:}
         pmc_pass "traffic_${w}_${p}_fetch" "--workload $w --precision $p" FETCH_SIZE
         pmc_pass "traffic_${w}_${p}_write" "--workload $w --precision $p" WRITE_SIZE
@@ -73,8 +74,7 @@ for step in $STEPS; do
       python3 "$R/tools/pmc_issue.py" "$OUT" "$PMC_KERNEL" ${PMC_CANDSTEPS:-1310720} > "$OUT/pmc_summary.txt" 2>&1 || true
       cat "$OUT/pmc_summary.txt" ;;
     rehearse)
-      BCMPC_DIST_BACKEND=gloo BCMPC_BENCH_DEVICE=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
-          --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 \
+      BCMPC_DIST_BACKEND=gloo BCMPC_BENCH_DEVICE=0 timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 1 \
           --no-cpu-baseline $BENCH_ARGS > "$OUT/rehearsal.json" 2> "$OUT/rehearsal.err" || stop rehearse $?
       tail -c 600 "$OUT/rehearsal.json" ;;
     ab)

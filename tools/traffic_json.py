@@ -16,10 +16,10 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = sys.argv[1]
-DST = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "profiles", "r05_traffic_per_launch.json")
+DST = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "profiles", "r06_traffic_per_launch.json")
 
 # (K, H, padded hidden, hidden layers) of the bench workloads
-SHAPES = {"cfg3": (65536, 20, 512, 2), "cfg2": (4096, 20, 512, 2), "cfg4_shard": (32768, 20, 512, 2),
+SHAPES = {"cfg3": (65536, 20, 512, 2), "cfg2": (4096, 20, 512, 2), "ns_shard": (8192, 20, 512, 2), "cfg4_shard": (32768, 20, 512, 2),
           "cfg5": (65536, 50, 1024, 3)}
 
 
