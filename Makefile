@@ -4,7 +4,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function
 SRC      := bc_mpc_amd/csrc
 LIB      := bc_mpc_amd/libbcmpc.so
-OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/rollout_x3_plain.o build/rollout_rr.o build/rollout_team.o build/rollout_mc.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o
+OBJ      := build/rollout.o build/rollout_grp.o build/rollout_x3.o build/rollout_x3_plain.o build/rollout_team.o build/cem.o build/fit.o build/capi.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o
 HDR      := include/bcmpc.h $(SRC)/kernels.h $(SRC)/device_common.h $(SRC)/argmin_common.h
 
 all: $(LIB)
@@ -32,19 +32,11 @@ build/rollout_x3_plain.o: $(SRC)/rollout_x3.hip $(HDR) $(SRC)/split_common.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) $(X3ILP) -DX3_PART=1 -c $< -o $@
 
-build/rollout_rr.o: $(SRC)/rollout_rr.hip $(HDR) $(SRC)/split_common.h
-	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-
 # the team kernels with the iterative ILP scheduler: ppo_defaults -2.4 us, ppo_mpc_default -5.5 us, run.sh
 # recipe -4.8 us per call against the default (max-ilp +2.5..+21 us, iterative-minreg +0..+24 us;
 # profiles/r04_team_sched_ab.jsonl)
 TEAMSCHED ?= -mllvm -amdgpu-sched-strategy=iterative-ilp
 build/rollout_team.o: $(SRC)/rollout_team.hip $(HDR) $(SRC)/split_common.h
-	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) $(TEAMSCHED) -c $< -o $@
-
-build/rollout_mc.o: $(SRC)/rollout_mc.hip $(HDR) $(SRC)/split_common.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) $(TEAMSCHED) -c $< -o $@
 

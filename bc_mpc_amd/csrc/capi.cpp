@@ -118,38 +118,38 @@ float x3_scale(const float* W, size_t n) {
     return std::ldexp(1.0f, std::max(-100, std::min(100, 12 - e)));
 }
 
-// Weight image of the resident-column split kernel (rollout_rr.hip RrGeom): NS = 2 + T slots per
-// step of 2P + 4 1-KiB pieces (P = HP / 32 k-steps, T = HP / 16 tiles, one piece = 512 halves):
-// slot 0 = layer-0 tiles [0, P) (x3 fragment pairs, hi | lo) + output tile 0 hi, lo, tile 1 hi,
-// lo at k-step P-1; slot 1 = layer-0 tiles [P, 2P) + four zero pieces; slot 2 + t = layer-1 tile
-// t (P k-steps, hi | lo) + output tile t & 1 (hi, lo) at k-step t/2 - 1 (zero for t < 2) + two
-// zero pieces.  l0 / l1 / lo are pack_x3_layer outputs with TWp = 1 ([tile][k-step][hi|lo][lane][8]).
-void pack_rr_image(const _Float16* l0, const _Float16* l1, const _Float16* lo, int HP, _Float16* img) {
-    const int P = HP / 32, T = HP / 16, SLOTH = (2 * P + 4) * 512;
-    auto out_frag = [&](int v, int p) { return lo + ((size_t)v * P + p) * 1024; };     // hi | lo, 1024 halves
-    std::memset(img, 0, sizeof(_Float16) * (size_t)(2 + T) * SLOTH);
-    for (int half = 0; half < 2; ++half)
-        std::memcpy(img + (size_t)half * SLOTH, l0 + (size_t)half * P * 1024, sizeof(_Float16) * P * 1024);
-    std::memcpy(img + (size_t)2 * P * 512, out_frag(0, P - 1), sizeof(_Float16) * 1024);
-    std::memcpy(img + (size_t)(2 * P + 2) * 512, out_frag(1, P - 1), sizeof(_Float16) * 1024);
-    for (int t = 0; t < T; ++t) {
-        _Float16* d = img + (size_t)(2 + t) * SLOTH;
-        std::memcpy(d, l1 + (size_t)t * P * 1024, sizeof(_Float16) * P * 1024);
-        if (t >= 2) std::memcpy(d + (size_t)2 * P * 512, out_frag(t & 1, t / 2 - 1), sizeof(_Float16) * 1024);
-    }
-}
-
 }  // namespace
 
 namespace bcmpc {
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace bcmpc
 
+// Diagnostic hooks: the per-phase stamps of STAMP variant kernels (BCMPC_X3_STAMPS, BCMPC_STAMP_DUMP) are read
+// only by a diagnostic build (-DBCMPC_DIAG_VARIANT: tools/build_variants.sh, tools/team_variants.sh); the
+// production library never consults them.
+static const char* diag_env(const char* name) {
+#ifdef BCMPC_DIAG_VARIANT
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+// Fault-injection hooks the GPU tests use (BCMPC_TEAM_SPINS=-1: every team gives up; comm.hip's
+// BCMPC_COMM_FORCE_FLAGS): read in every build, and announced on stderr once per process when set, so a stray
+// variable on a production run is visible.
+namespace bcmpc {
+void announce_test_hook(const char* name, const char* value) {
+    static std::atomic<unsigned> said{0};
+    const unsigned bit = name[6] == 'C' ? 1u : 2u;      // BCMPC_COMM_* / BCMPC_TEAM_*
+    if (!(said.fetch_or(bit) & bit))
+        std::fprintf(stderr, "libbcmpc: test hook %s=%s is active (fault injection; unset it for real runs)\n",
+                     name, value);
+}
+}  // namespace bcmpc
+
 static thread_local bool g_no_team = false;         // bcmpc_create: never pick the team kernel (fallbacks)
-// auto-selection bound of the multi-column team kernel (rollout_mc.hip): 0 -- it measured slower than
-// rollout_x3 at every K it takes (cfg2 0.370 vs 0.247 ms, cfg4 shard 2.67 vs 0.96 ms; DESIGN.md 6.8,
-// profiles/r05_mc_ab.txt), so it is opt-in (BCMPC_MC=1, or kernel "team" beyond the one-column team's reach)
-static constexpr int64_t kMcAutoMaxK = 0;
 
 struct bcmpc_engine {
     bcmpc_config cfg{};
@@ -225,10 +225,6 @@ struct bcmpc_engine {
     unsigned long long* d_team = nullptr;
     int team_kind = 0;                  // 0 plain delta net, 1 + policy, 2 reward net (+ policy)
     bool team_defer = false;            // the weights are packed for rollout_team's deferred last LayerNorm
-    // multi-column team kernel (rollout_mc.hip; kernel == TEAM, mc): teams, columns per team, state scratch
-    bool mc = false;
-    int mc_nteam = 0, mc_ncol = 0;
-    double* d_mc_state = nullptr;
     unsigned* d_team_ctl = nullptr;
     unsigned* h_team_err = nullptr;
     unsigned* d_team_err = nullptr;
@@ -379,7 +375,10 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (reward && c.state_dim < 16)
             return fail(BCMPC_ERR_UNSUPPORTED, "split reward engines need state_dim >= 16 (reward row in tile 1)");
         if (c.kernel != BCMPC_KERNEL_AUTO && (c.kernel < BCMPC_KERNEL_SPLIT1 || c.kernel > BCMPC_KERNEL_TEAM))
-            return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4/splitr/team kernels");
+            return fail(BCMPC_ERR_ARG, "SPLIT_F16 precision runs on the split1/split2/split4/team kernels");
+        if (c.kernel == BCMPC_KERNEL_SPLITR)
+            return fail(BCMPC_ERR_UNSUPPORTED, "the splitr (resident-column) kernel was retired: slower than the "
+                                               "split slab kernel at every K (DESIGN.md 6.5); use auto or split4");
     } else if (c.kernel >= BCMPC_KERNEL_SPLIT1) {
         return fail(BCMPC_ERR_ARG, "split kernels need precision SPLIT_F16");
     }
@@ -425,21 +424,6 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->TP = 8;
         e->PL = c.policy_layers;
     }
-    // resident-column split kernel (rollout_rr.hip): the 2-layer tanh delta net at hidden <= 512.
-    // Opt-in (kernel = splitr, or BCMPC_SPLITR=1 under auto): measured 2.03 ms at cfg3 against the
-    // slab kernel's 1.90 ms -- LDS-read-bound at one column per wave
-    const bool rr_ok = split && !f16 && !reward && e->PL == 0 && c.activation == BCMPC_ACT_TANH && !c.layer_norm &&
-                       c.n_layers == 2 && e->HP <= 512 && c.state_dim + c.action_dim <= 32;
-    bool use_rr = c.kernel == BCMPC_KERNEL_SPLITR;
-    if (use_rr && !rr_ok) {
-        delete e;
-        return fail(BCMPC_ERR_UNSUPPORTED, "splitr kernel: 2-layer tanh NNDynamicsModel, hidden <= 512, no "
-                                           "LayerNorm / policy / reward net");
-    }
-    if (c.kernel == BCMPC_KERNEL_AUTO && rr_ok) {
-        const char* ev = std::getenv("BCMPC_SPLITR");
-        use_rr = ev && *ev && ev[0] == '1';
-    }
     // small-K team kernel (rollout_team.hip): the 2-layer delta net at hidden <= 512 (LayerNorm: <=
     // 256), or at hidden 512 (tanh) with a fused policy of <= 2 layers and / or the reward net (the
     // run.sh recipe), when the whole grid fits one workgroup per CU (the team members of a column wait
@@ -459,22 +443,6 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                             !(tkind == 2 && c.layer_norm && (c.state_dim > 23 || !team_rw_ln_built()));
     const bool team_fits = team_shape && c.num_paths > 0 && team_blocks(c.num_paths, e->HP, tkind) <= (int64_t)ncu;
     bool use_team = c.kernel == BCMPC_KERNEL_TEAM;
-    // multi-column team kernel (rollout_mc.hip): the plain 2-layer tanh delta net at hidden 512 in split
-    // precision, several columns per team of 4 CUs -- where the one-column team does not fit the chip.
-    // Auto for K up to kMcAutoMaxK (cfg2-size K); kernel "team" beyond the one-column team's reach takes it
-    // at any K; BCMPC_MC=1 forces it wherever the shape allows, =0 turns it off
-    const bool mc_shape = split && !f16 && tkind == 0 && c.activation == BCMPC_ACT_TANH && !c.layer_norm &&
-                          mc_shape_ok(e->HP, c.n_layers, c.state_dim, c.action_dim, c.horizon) && c.num_paths > 0 &&
-                          mc_teams(c.num_paths, ncu) >= 8 &&
-                          (c.cost == BCMPC_COST_CHEETAH || c.cost == BCMPC_COST_NONE);
-    bool use_mc = false;
-    if (mc_shape && !use_rr && !g_no_team) {
-        const char* ev = std::getenv("BCMPC_MC");
-        const bool on = ev && ev[0] == '1', off = ev && ev[0] == '0';
-        if (use_team && !team_fits) use_mc = !off;
-        else if (c.kernel == BCMPC_KERNEL_AUTO) use_mc = on || (!off && !team_fits && c.num_paths <= kMcAutoMaxK);
-    }
-    if (use_mc) use_team = false;
     if (use_team && !team_fits) {
         delete e;
         return fail(BCMPC_ERR_UNSUPPORTED, "team kernel: 2-layer net, hidden <= 512 (LayerNorm: <= 256; with a "
@@ -482,32 +450,16 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                                            "net: 512, tanh, LayerNorm with S <= 23), S + A <= 32, "
                                            "ceil(K / 128) * 8 * members workgroups <= the device's CUs");
     }
-    if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !use_rr && !g_no_team && !use_mc) {
+    if (c.kernel == BCMPC_KERNEL_AUTO && team_fits && !g_no_team) {
         const char* ev = std::getenv("BCMPC_TEAM");
         use_team = !(ev && ev[0] == '0');
     }
-    if (use_mc) {
-        e->split = true;
-        e->nc = 1;
-        e->kernel = BCMPC_KERNEL_TEAM;
-        e->mc = true;
-        e->nw = 4;
-        e->team_kind = 0;
-        e->mc_nteam = mc_teams(c.num_paths, ncu);
-        e->mc_ncol = mc_columns_per_team(c.num_paths, ncu);
-        kern = e->kernel;
-    } else if (use_team) {
+    if (use_team) {
         e->split = true;
         e->nc = 1;
         e->kernel = BCMPC_KERNEL_TEAM;
         e->nw = e->HP / 16 / team_layer0_tiles(e->HP, tkind);
         e->team_kind = tkind;
-        kern = e->kernel;
-    } else if (use_rr) {
-        e->split = true;
-        e->nc = 4;
-        e->kernel = BCMPC_KERNEL_SPLITR;
-        e->nw = 4;
         kern = e->kernel;
     } else if (split) {
         // widest workgroup (most candidates per weight read) that still gives every CU work and fits LDS
@@ -624,12 +576,6 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         e->w_off[1] = off; off += (size_t)2 * T * T * 64 * 4;
         e->w_off[2] = off; off += (size_t)2 * 2 * T * 64 * 4;
         e->b_off[0] = 0; e->b_off[1] = e->HP; e->b_off[2] = 3 * e->HP; boff = 3 * e->HP + 32 + 8 * 32;   // (same size as the split layout)
-    } else if (kern == BCMPC_KERNEL_SPLITR) {
-        // one slot image (pack_rr_image) streamed by every workgroup; layers 1, 2 are inside it
-        off = rr_image_bytes(e->HP) / sizeof(float);
-        e->w_off[0] = 0; e->w_off[1] = off; e->w_off[2] = off;
-        for (int l = 0; l < L; ++l) { e->b_off[l] = boff; boff += e->HP; }
-        e->b_off[L] = boff; boff += 32;
     } else {
         e->w_off[0] = off; off += (size_t)T * 2 * 64 * 4;                   // [S+A -> h]
         for (int l = 1; l < L; ++l) { e->w_off[l] = off; off += (size_t)T * T * 64 * 4; }
@@ -666,9 +612,7 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { g_last_error = "event create failed"; return cleanup(BCMPC_ERR_HIP); }
     if (e->kernel == BCMPC_KERNEL_TEAM) {
         const size_t tb = team_buf_bytes(c.num_paths, e->HP, e->team_kind);
-        const size_t mb = e->mc ? mc_state_bytes(c.num_paths, ncu) : 0;
-        if ((mb && hipMalloc(&e->d_mc_state, mb) != hipSuccess) ||
-            (tb && hipMalloc(&e->d_team, tb) != hipSuccess) ||
+        if ((tb && hipMalloc(&e->d_team, tb) != hipSuccess) ||
             (tb && hipMemset(e->d_team, 0, tb) != hipSuccess) ||
             hipMalloc(&e->d_team_ctl, 4 * sizeof(unsigned)) != hipSuccess ||
             hipMemset(e->d_team_ctl, 0, 4 * sizeof(unsigned)) != hipSuccess ||
@@ -736,7 +680,7 @@ int bcmpc_destroy(bcmpc_engine* e) {
                     (void*)e->d_actions, (void*)e->d_costs, (void*)e->d_result, (void*)e->d_pw, (void*)e->d_pb,
                     (void*)e->d_first, (void*)e->d_gpow, (void*)e->d_mu, (void*)e->d_sigma, (void*)e->d_elite,
                     (void*)e->d_count, (void*)e->d_amin_c, (void*)e->d_amin_i,
-                    (void*)e->d_amin_ticket, (void*)e->d_team, (void*)e->d_team_ctl, (void*)e->d_mc_state, (void*)e->d_mt_io, (void*)e->d_mt_bounds, (void*)e->d_mt_xs,
+                    (void*)e->d_amin_ticket, (void*)e->d_team, (void*)e->d_team_ctl, (void*)e->d_mt_io, (void*)e->d_mt_bounds, (void*)e->d_mt_xs,
                     (void*)e->d_mt_polys, (void*)e->d_mt_chunks, (void*)e->d_mt_part})
         if (p) (void)hipFree(p);
     if (e->h_result) (void)hipHostFree(e->h_result);
@@ -878,22 +822,6 @@ int bcmpc_set_weights(bcmpc_engine* e, const bcmpc_weights* w, uint64_t version)
         }
         e->mean_reward = w->mean_reward[0];
         e->std_reward = w->std_reward[0];
-    } else if (e->kernel == BCMPC_KERNEL_SPLITR) {
-        // rollout_rr: per-layer x3 fragment pairs (TWp = 1), then the slot image
-        const int P = T / 2;
-        std::vector<_Float16> l0((size_t)T * 1024), l1((size_t)T * P * 1024), lo((size_t)2 * P * 1024);
-        const float s0 = x3_scale(w->kernels[0], (size_t)(S + A) * h);
-        const float s1 = x3_scale(w->kernels[1], (size_t)h * h);
-        const float so = x3_scale(w->kernels[2], (size_t)h * S);
-        pack_x3_layer(w->kernels[0], S + A, h, 1, T, 1, s0, l0.data());
-        pack_x3_layer(w->kernels[1], h, h, P, T, 1, s1, l1.data());
-        pack_x3_layer(w->kernels[2], h, S, P, 2, 1, so, lo.data());
-        pack_rr_image(l0.data(), l1.data(), lo.data(), HP, reinterpret_cast<_Float16*>(hw.data()));
-        e->winv[0] = 1.0f / s0;                            // (layer 0's input scale is per candidate)
-        e->winv[1] = (1.0f / s1) / 4096.0f;                // hidden inputs are tanh x 2^12
-        e->winv[2] = (1.0f / so) / 4096.0f;
-        for (int l = 0; l < L; ++l) std::memcpy(hb.data() + e->b_off[l], w->biases[l], sizeof(float) * h);
-        std::memcpy(hb.data() + e->b_off[L], w->biases[L], sizeof(float) * S);
     } else if (e->split) {
         // same sizes as the f32 layout (4 bytes per weight: two halves)
         _Float16* hh = reinterpret_cast<_Float16*>(hw.data());
@@ -1470,8 +1398,8 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         return !(v && v[0] == '0');
     }();
     const bool fused = d_result && !cem &&
-                       (e->kernel == BCMPC_KERNEL_TEAM ? team_fused && !e->mc
-                                                       : e->split && e->kernel != BCMPC_KERNEL_SPLITR && fa && fa[0] == '1');
+                       (e->kernel == BCMPC_KERNEL_TEAM ? team_fused
+                                                       : e->split && fa && fa[0] == '1');
     if (fused) {
         a.fused_argmin = 1;
         a.amin = m;
@@ -1491,12 +1419,13 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         // BCMPC_TEAM_SPINS (tests): exchange polls before a member gives up; -1: the launch is skipped and
         // reported as a team that gave up (forces the fallback path deterministically)
         const char* sv = std::getenv("BCMPC_TEAM_SPINS");
+        if (sv && *sv) announce_test_hook("BCMPC_TEAM_SPINS", sv);
         a.team_spins = sv && *sv ? std::max(-1, std::atoi(sv)) : 0;
         if (const int rc = team_order_before(c.device, st, e->stream)) return rc;
         // diagnostics: TEAM_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_tst = nullptr;
         static size_t tst_n = 0;
-        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr && !e->mc;
+        const bool stamps = diag_env("BCMPC_X3_STAMPS") != nullptr;
         const size_t nwv = (size_t)(e->HP / 16 / team_layer0_tiles(e->HP, e->team_kind));
         const size_t blocks = (size_t)team_blocks(c.num_paths, e->HP, e->team_kind);
         if (stamps) {
@@ -1511,40 +1440,6 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
         if (a.team_spins < 0) {
             __atomic_store_n(e->h_team_err, 1u, __ATOMIC_RELEASE);
             team_skipped = true;                      // (no tail ran: the argmin launch raises the done word)
-        } else if (e->mc) {
-            a.mc_state = e->d_mc_state;
-            a.mc_ncol = e->mc_ncol;
-            a.mc_nteam = e->mc_nteam;
-            // diagnostics: MC_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
-            static uint64_t* d_mst = nullptr;
-            static size_t mst_n = 0;
-            const bool mst = std::getenv("BCMPC_X3_STAMPS") != nullptr;
-            const size_t mblocks = (size_t)e->mc_nteam * mc_members();
-            if (mst) {
-                if (mst_n < mblocks * 40) {
-                    if (d_mst) (void)hipFree(d_mst);
-                    mst_n = mblocks * 40;
-                    HIP_TRY(hipMalloc(&d_mst, mst_n * sizeof(uint64_t)));
-                }
-                HIP_TRY(hipMemsetAsync(d_mst, 0, mst_n * sizeof(uint64_t), st));
-                a.stamps = d_mst;
-            }
-            HIP_TRY(launch_rollout_mc(a, st));
-            if (mst) {
-                std::vector<uint64_t> hs(mblocks * 40);
-                HIP_TRY(hipMemcpyAsync(hs.data(), d_mst, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-                HIP_TRY(hipStreamSynchronize(st));
-                const char* names[10] = {"loads+publish", "l0l1mm+c", "ccheck", "cstore", "l1epi", "barrier", "-", "-", "-",
-                                         "prologue"};
-                const double nint = (double)std::max(4, e->mc_ncol) * (c.horizon + 1) + 2;
-                std::fprintf(stderr, "mc stamps (per interval, s_memtime ticks; %.0f intervals):", nint);
-                for (int k = 0; k < 10; ++k) {
-                    double sm = 0;
-                    for (size_t i = 0; i < mblocks * 4; ++i) sm += (double)hs[i * 10 + k];
-                    std::fprintf(stderr, " %s=%.0f", names[k], sm / (mblocks * 4) / (k == 9 ? 1.0 : nint));
-                }
-                std::fprintf(stderr, "\n");
-            }
         } else {
             HIP_TRY(launch_rollout_team(a, e->HP, st));
         }
@@ -1556,7 +1451,7 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             HIP_TRY(hipStreamSynchronize(st));
             const char* names[10] = {"tail", "fill", "l0in", "layer0", "slabbar", "l1mm", "l1epi", "out+bar",
                                      "xchg", "prologue"};
-            if (const char* dump = std::getenv("BCMPC_STAMP_DUMP")) {   // raw [blocks][waves][10] records
+            if (const char* dump = diag_env("BCMPC_STAMP_DUMP")) {   // raw [blocks][waves][10] records
                 if (FILE* f = std::fopen(dump, "ab")) {
                     const int32_t hdr[4] = {(int32_t)blocks, (int32_t)nwv, c.horizon, (int32_t)c.num_paths};
                     std::fwrite(hdr, sizeof(hdr), 1, f);
@@ -1579,41 +1474,11 @@ static int rollout_impl(bcmpc_engine* e, const double* d_state, int64_t stride, 
             }
             std::fprintf(stderr, "\n");
         }
-    } else if (e->kernel == BCMPC_KERNEL_SPLITR) {
-        // diagnostics: RR_STAMP variant builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
-        static uint64_t* d_rst = nullptr;
-        static size_t rst_n = 0;
-        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
-        const int cpb = rr_candidates_per_block(), nwv = cpb / 16;
-        const size_t blocks = (size_t)((c.num_paths + cpb - 1) / cpb);
-        if (stamps) {
-            if (rst_n < blocks * nwv * 10) {
-                if (d_rst) (void)hipFree(d_rst);
-                rst_n = blocks * nwv * 10;
-                HIP_TRY(hipMalloc(&d_rst, rst_n * sizeof(uint64_t)));
-            }
-            HIP_TRY(hipMemsetAsync(d_rst, 0, rst_n * sizeof(uint64_t), st));
-            a.stamps = d_rst;
-        }
-        HIP_TRY(launch_rollout_rr(a, e->HP, st));
-        if (stamps) {
-            std::vector<uint64_t> h(blocks * nwv * 10);
-            HIP_TRY(hipMemcpyAsync(h.data(), d_rst, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            const char* names[6] = {"barrier", "layer0", "layer1", "head/tail", "dma-wait", "dma-issue"};
-            std::fprintf(stderr, "rr stamps (per step, s_memtime ticks):");
-            for (int k = 0; k < 6; ++k) {
-                double sum = 0;
-                for (size_t b = 0; b < blocks * nwv; ++b) sum += (double)h[b * 10 + k];
-                std::fprintf(stderr, " %s=%.0f", names[k], sum / (blocks * nwv) / c.horizon);
-            }
-            std::fprintf(stderr, "\n");
-        }
     } else if (e->split) {
         // diagnostics: X3_STAMP builds record per-phase cycles per wave (BCMPC_X3_STAMPS=1 prints them)
         static uint64_t* d_st = nullptr;
         static size_t st_n = 0;
-        const bool stamps = std::getenv("BCMPC_X3_STAMPS") != nullptr;
+        const bool stamps = diag_env("BCMPC_X3_STAMPS") != nullptr;
         const int nw = e->nw;
         const size_t blocks = (size_t)((c.num_paths + 16 * e->nc - 1) / (16 * e->nc));
         if (stamps) {
@@ -2689,14 +2554,10 @@ int bcmpc_engine_layout(const bcmpc_engine* e, char* buf, int32_t cap) {
         case BCMPC_KERNEL_GROUP2:
         case BCMPC_KERNEL_GROUP4:
         case BCMPC_KERNEL_GROUP8: std::snprintf(s, sizeof(s), "rollout_grp<%d,NW=%d> fp32", e->HP, e->nw); break;
-        case BCMPC_KERNEL_SPLITR: std::snprintf(s, sizeof(s), "rollout_rr<%d> split", e->HP); break;
         case BCMPC_KERNEL_TEAM:
-            if (e->mc)
-                std::snprintf(s, sizeof(s), "rollout_mc<%d,T=%d,teams=%d,cols=%d> split", e->HP, mc_members(),
-                              e->mc_nteam, e->mc_ncol);
-            else
-                std::snprintf(s, sizeof(s), "rollout_team<%d,kind=%d%s> split", e->HP, e->team_kind,
-                              e->team_defer ? ",deferLN" : "");
+            std::snprintf(s, sizeof(s), "rollout_team<%d,kind=%d%s> split", e->HP, e->team_kind,
+                          e->team_defer ? ",deferLN" : "");
+            break;
             break;
         default:
             if (e->pp)

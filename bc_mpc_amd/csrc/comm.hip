@@ -287,7 +287,10 @@ int bcmpc_comm_init(const uint8_t* id, int32_t nranks, int32_t rank, int32_t dev
     if (hipSetDevice(device) != hipSuccess) return comm_fail(BCMPC_ERR_HIP, "hipSetDevice failed");
     bcmpc_comm* c = new bcmpc_comm();
     c->nranks = nranks; c->rank = rank; c->device = device;
-    if (const char* v = std::getenv("BCMPC_COMM_FORCE_FLAGS")) c->force_flags = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("BCMPC_COMM_FORCE_FLAGS")) {     // (test hook: announced on stderr)
+        c->force_flags = std::max(0, std::atoi(v));
+        announce_test_hook("BCMPC_COMM_FORCE_FLAGS", v);
+    }
     auto release = [&]() {
         if (c->d_send) (void)hipFree(c->d_send);
         if (c->d_gather) (void)hipFree(c->d_gather);

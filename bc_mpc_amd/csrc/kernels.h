@@ -105,10 +105,6 @@ struct RolloutArgs {
     // (team kernel, the reward net with LayerNorm heads) [8 members][32 rows]: sum over member t's head
     // rows of the gamma-folded, scaled output weights (the centring correction, rollout_team.hip)
     const float* head_rs;
-    // (multi-column team kernel, rollout_mc.hip) per-member state scratch [columns][T][4 waves][3][64] f64,
-    // columns per team and teams
-    double* mc_state;
-    int32_t mc_ncol, mc_nteam;
 };
 
 struct SelectArgs {                          // top-E of (cost, index) pairs, NaN last, ties -> lower index
@@ -164,6 +160,7 @@ hipError_t launch_mt_draw(const MtDrawArgs& a, hipStream_t st);
 
 // ---- library-owned min-loc exchange (comm.hip) ----
 int set_error(int code, const std::string& msg);          // bcmpc_last_error() text (capi.cpp)
+void announce_test_hook(const char* name, const char* value);   // stderr, once per hook per process (capi.cpp)
 int comm_exchange(bcmpc_comm* c, bcmpc_result* d_result, int maximize, hipStream_t st, std::string* err,
                   const unsigned* d_team_err);
 bool comm_any_flags(bcmpc_comm* c);
@@ -192,9 +189,6 @@ size_t x3_f16_lds(int hidden_padded, int n_layers, int nc, int nw, int action_di
 bool x3_pp_ok(int hidden_padded, int n_layers, int state_dim, int action_dim);   // rollout_pp's shapes
 hipError_t launch_rollout_x3(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
 hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st);
-size_t rr_image_bytes(int hidden_padded);
-int rr_candidates_per_block();
-hipError_t launch_rollout_rr(const RolloutArgs& a, int hidden_padded, hipStream_t st);
 // rollout_team.hip; kind: 0 the plain delta net, 1 + fused policy, 2 the reward net (+ policy)
 int team_members(int hidden_padded, int kind);          // workgroups per candidate column (0: unsupported)
 // the team kernel's deferred last LayerNorm (relu + LN delta net at T = 1; rollout_team.hip DEFER): the host
@@ -208,13 +202,6 @@ int64_t team_blocks(int64_t K, int hidden_padded, int kind);
 size_t team_buf_bytes(int64_t K, int hidden_padded, int kind);
 bool team_rw_ln_built();                                // the reward net's LayerNorm heads are in this build
 hipError_t launch_rollout_team(const RolloutArgs& a, int hidden_padded, hipStream_t st);
-// rollout_mc.hip: the multi-column team kernel (plain tanh delta net, hidden 512, split precision)
-bool mc_shape_ok(int hidden_padded, int n_layers, int state_dim, int action_dim, int horizon);
-int mc_members();                                        // workgroups per team (T)
-int mc_teams(int64_t K, int n_cu);                       // teams launched (a multiple of 8)
-int mc_columns_per_team(int64_t K, int n_cu);
-size_t mc_state_bytes(int64_t K, int n_cu);
-hipError_t launch_rollout_mc(const RolloutArgs& a, hipStream_t st);
 hipError_t launch_argmin(const ArgminArgs& a, hipStream_t st);
 hipError_t launch_select(const SelectArgs& a, hipStream_t st);
 hipError_t launch_refit(const RefitArgs& a, hipStream_t st);

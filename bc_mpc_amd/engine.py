@@ -168,7 +168,7 @@ class RolloutEngine:
             split_ok = ((plain or (model == "delta" and not policy_hidden and hidden <= 512))
                         and (model == "delta" or state_dim >= 16)
                         and (not policy_hidden or 448 < hidden <= top)
-                        and kernel in ("auto", "split1", "split2", "split4", "splitr", "team"))
+                        and kernel in ("auto", "split1", "split2", "split4", "team"))
             # the small-K team kernel also takes relu / LayerNorm dynamics under a fused policy (hidden
             # <= 256: train_mpc_ppo.py's 2x256 relu + LN net) and the LayerNorm reward net (the run.sh
             # recipe) when its grid is resident: tried in split, fp32 when bcmpc_create refuses

@@ -1073,10 +1073,10 @@ def main():
     info = eng.info()
     kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
                    "group8": "rollout_grp<NW=8>", "split1": "rollout_x3<NC=1>", "split2": "rollout_x3<NC=2>",
-                   "split4": "rollout_x3<NC=4>", "splitr": "rollout_rr (resident columns, LDS weight ring)",
+                   "split4": "rollout_x3<NC=4>",
                    "team": "rollout_team (weights in registers, one column per team of workgroups)"}.get(
         info["kernel"], info["kernel"]) + f" (hidden padded {info['hidden_padded']}, {act})"
-    if info["layout"].startswith(("rollout_mc", "rollout_pp")):
+    if info["layout"].startswith("rollout_pp"):
         kernel_name = info["layout"] + f" (hidden padded {info['hidden_padded']}, {act})"
     lib_comm = None
     if (world > 1 and backend == "nccl" and not wl.get("cem") and args.actions == "device"

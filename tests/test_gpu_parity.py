@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 ATOL, RTOL = 1e-4, 1e-5
 
 
-KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4", "splitr", "team"]
+KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4", "team"]
 
 
 def team_ok(hidden, ln, n_layers, K, S=20, A=6):
@@ -40,9 +40,6 @@ def team_ok(hidden, ln, n_layers, K, S=20, A=6):
 def _skip_unsupported(g: Golden, kernel: str):
     if kernel == "group8" and g.meta["hidden"] <= 64:
         pytest.skip("group8 needs >= 8 hidden tiles")
-    if kernel == "splitr" and (g.meta["act"] != "tanh" or g.meta["ln"] or g.weights.n_layers != 2
-                               or g.meta["hidden"] > 512):
-        pytest.skip("splitr: the 2-layer tanh delta net, hidden <= 512")
     if kernel == "team" and not team_ok(g.meta["hidden"], g.meta["ln"], g.weights.n_layers, g.K, g.S, g.A):
         pytest.skip("team: the 2-layer delta net at small K (grid resident)")
     if kernel.startswith("split"):
@@ -220,7 +217,16 @@ def test_non_fused_cost_goes_through_trajectory_mode():
     assert ctrl.last_index == i and np.array_equal(a, want)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "solo", "group8", "split4", "split1", "splitr"])
+def test_retired_splitr_kernel_is_refused():
+    """The resident-column kernel (rollout_rr.hip, opt-in only, slower than the slab kernel at every K: DESIGN.md
+    6.5) was retired in round 6: asking for it fails loudly instead of running another layout."""
+    from bc_mpc_amd import _lib
+    from bc_mpc_amd.engine import RolloutEngine
+    with pytest.raises(_lib.BcmpcError, match="retired"):
+        RolloutEngine(20, 6, 500, 2, "tanh", False, 20, 4096, kernel="splitr")
+
+
+@pytest.mark.parametrize("kernel", ["auto", "solo", "group8", "split4", "split1"])
 def test_full_size_cfg3_properties(kernel):
     """K=65536, H=20, 2x500 tanh (BASELINE cfg3 dims) at full size: shard
     invariance (bitwise), argmin consistency, determinism, and a 256-candidate

@@ -26,16 +26,16 @@ for spec in "$@"; do
     ( $H -mllvm -amdgpu-sched-strategy=iterative-ilp -DX3_PART=1 $flags -c $src -o build/variants/rollout_x3_plain_$name.o &&
       $H -mllvm -amdgpu-sched-strategy=max-ilp -DX3_PART=2 $flags -c $src -o build/variants/rollout_x3_$name.o &&
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
-          build/rollout.o build/rollout_grp.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o build/rollout_rr.o build/rollout_team.o build/rollout_mc.o build/variants/rollout_x3_$name.o build/variants/rollout_x3_plain_$name.o build/variants/capi.o -ldl ) &
+          build/rollout.o build/rollout_grp.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o build/rollout_team.o build/variants/rollout_x3_$name.o build/variants/rollout_x3_plain_$name.o build/variants/capi.o -ldl ) &
   elif [ $X3 = 1 ]; then
     ( $H -DX3_ONLY=${X3W:-512} -DX3_ONLY_NC=${X3NC:-4} $flags -c $src -o build/variants/rollout_x3_$name.o &&
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
-          build/rollout.o build/rollout_grp.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o build/rollout_rr.o build/rollout_team.o build/rollout_mc.o build/variants/rollout_x3_$name.o build/variants/capi.o -ldl ) &
+          build/rollout.o build/rollout_grp.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o build/rollout_team.o build/variants/rollout_x3_$name.o build/variants/capi.o -ldl ) &
   else
     ( $H $flags -c bc_mpc_amd/csrc/rollout.hip -o build/variants/rollout_$name.o &&
       $H $flags -c bc_mpc_amd/csrc/rollout_grp.hip -o build/variants/rollout_grp_$name.o &&
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/variants/libbcmpc_$name.so \
-          build/variants/rollout_$name.o build/variants/rollout_grp_$name.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o build/rollout_x3.o build/rollout_x3_plain.o build/rollout_rr.o build/rollout_team.o build/rollout_mc.o \
+          build/variants/rollout_$name.o build/variants/rollout_grp_$name.o build/cem.o build/fit.o build/mt19937.o build/mt_jump.o build/mt_device.o build/comm.o build/rollout_x3.o build/rollout_x3_plain.o build/rollout_team.o \
           build/variants/capi.o -ldl ) &
   fi
 done
