@@ -493,6 +493,10 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
                 // the two-group pipelined kernel (rollout_pp): 128 candidates per workgroup, 4 waves per
                 // group own 8 hidden tiles each (weights packed 8 tiles per wave)
                 e->pp = true;
+                // FOLD's input range: layer 0's normalised input goes to f16 without a power-of-two scale,
+                // clamped to +-65504 (a dim normalising beyond saturates; the first tanh has saturated long
+                // before) and below 6.1e-5 subnormal (< 6e-8 absolute error); the fold check below bounds
+                // only the weights.  Pinned by tests/test_gpu_f16.py::test_f16_pp_fold_input_range
                 const char* ef = std::getenv("BCMPC_PP_FOLD");
                 e->pp_fold = !(ef && ef[0] == '0');
                 nc = 8;

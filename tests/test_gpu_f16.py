@@ -234,3 +234,36 @@ def test_f16_refuses_other_nets():
         RolloutEngine(20, 6, 256, 2, "relu", True, 7, 400, precision="f16")
     with pytest.raises(Exception):
         RolloutEngine(20, 6, 500, 2, "tanh", False, 7, 400, precision="f16", kernel="team")
+
+
+@pytest.mark.parametrize("dim,std", [(3, 1e-6), (9, 1e5)])
+def test_f16_pp_fold_input_range(monkeypatch, dim, std):
+    """rollout_pp's folded layer 0 (BCMPC_PP_FOLD, the default) converts the normalised input to f16 WITHOUT a
+    power-of-two scale, clamped to +-65504: a state dim with a near-zero std_obs normalises to
+    ~1e5 and saturates, one with a huge std_obs normalises below f16's normal range.  Saturation is benign
+    here because the first layer's tanh saturates long before (|x W| >> 1 at x = 65504), and a subnormal
+    input is off by less than 6e-8 absolute: the f16 bar holds against the oracle, which uses the unclamped
+    f32 input."""
+    from bc_mpc_amd.engine import MLPSpec, RolloutEngine
+    from oracle import mpc_oracle as orc
+    monkeypatch.setenv("BCMPC_F16_PP", "1")
+    K, H = 512, 5
+    w = orc.synthetic_weights(20, 6, 500, 2, "tanh", False)
+    norm = [np.array(a, copy=True) for a in orc.synthetic_normalization()]
+    norm[1][dim] = std                                  # std_obs
+    state = orc.synthetic_state(orc.synthetic_normalization())
+    eng = RolloutEngine(20, 6, 500, 2, "tanh", False, H, K, precision="f16")
+    eng.set_weights(MLPSpec(w.kernels, w.biases, "tanh"), norm, 1)
+    layout = eng.info()["layout"]
+    assert layout.startswith("rollout_pp<512,fold"), layout
+    acts = np.random.RandomState(5).uniform(-1, 1, (H, K, 6))
+    x = abs((state[dim] - norm[0][dim]) / (std + 1e-10))
+    assert (x > 65504) if std < 1 else (x < 6.2e-5), x
+    res = eng.get_action(state, acts, return_costs=True)
+    want, paths = orc.rollout(orc.NumpyDynamics(w, norm), state, acts)
+    near = np.zeros(K, dtype=bool)
+    for hh in range(H + 1):
+        s = paths[hh]
+        near |= (np.abs(s[:, 5] - 0.2) < F16_NEAR) | (np.abs(s[:, 6]) < F16_NEAR) | (np.abs(s[:, 7]) < F16_NEAR)
+    _check(res.costs, want, near, H, f"pp fold, std_obs[{dim}]={std:g} (|x|={x:.3g})")
+    eng.close()
