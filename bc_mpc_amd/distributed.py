@@ -187,7 +187,8 @@ class RecordExchange:
         self.group = group
         self.maximize = int(bool(maximize))
         self.device = torch.device("cuda", int(device))
-        self.backend = dist.get_backend(group) if self.size > 1 else "none"
+        self.collective = dist.is_available() and dist.is_initialized()   # (a 1-rank group gathers too)
+        self.backend = dist.get_backend(group) if self.collective else "none"
         nb = ctypes_sizeof_result()
         self.d_result = torch.zeros(nb, dtype=torch.uint8, device=self.device)
         self.d_all = torch.zeros(max(1, self.size) * nb, dtype=torch.uint8, device=self.device)
@@ -202,7 +203,7 @@ class RecordExchange:
         import torch.distributed as dist
         from . import _lib
         with torch.cuda.stream(stream):
-            if self.size > 1:
+            if self.collective:
                 if self.backend == "nccl":
                     dist.all_gather_into_tensor(self.d_all, self.d_result, group=self.group)
                 else:                                  # gloo: host tensors
