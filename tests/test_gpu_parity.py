@@ -220,9 +220,8 @@ def test_non_fused_cost_goes_through_trajectory_mode():
 def test_retired_splitr_kernel_is_refused():
     """The resident-column kernel (rollout_rr.hip, opt-in only, slower than the slab kernel at every K: DESIGN.md
     6.5) was retired in round 6: asking for it fails loudly instead of running another layout."""
-    from bc_mpc_amd import _lib
     from bc_mpc_amd.engine import RolloutEngine
-    with pytest.raises(_lib.BcmpcError, match="retired"):
+    with pytest.raises(ValueError, match="retired"):
         RolloutEngine(20, 6, 500, 2, "tanh", False, 20, 4096, kernel="splitr")
 
 
