@@ -91,7 +91,7 @@ F16_MFMA_PEAK_TFLOPS = 2516.6     # dense f16/bf16 MFMA: 512 MAC/clk/SIMD x 1024
 # f32-equivalent (algorithmic) ceiling is a third of the f16 peak
 SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
-TRAFFIC_FILE = "r05_traffic_per_launch.json"
+TRAFFIC_FILE = "r06_traffic_per_launch.json"
 
 
 def flop_per_cand_step(hidden, L, S=S_DIM, A=A_DIM, policy=None, reward=False):

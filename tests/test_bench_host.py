@@ -53,8 +53,8 @@ def test_roofline_line_counts_every_cem_pass():
 def test_committed_traffic_file_covers_the_bench_lines():
     path = os.path.join(REPO, "profiles", bench.TRAFFIC_FILE)
     tr = json.load(open(path))
-    for key in ("cfg3:split:device", "cfg3:f16:device", "cfg2:split:device", "cfg4_shard:split:device",
-                "cfg5:split:device"):
+    for key in ("cfg3:split:device", "cfg3:f16:device", "cfg2:split:device", "ns_shard:split:device",
+                "cfg4_shard:split:device", "cfg5:split:device"):
         assert key in tr, key
         rec = tr[key]
         # every XCD misses the packed weights into its own L2: measured bytes >= the algorithmic ones
