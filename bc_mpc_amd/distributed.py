@@ -125,11 +125,39 @@ def better(a: Sequence[float], b: Sequence[float]) -> bool:
 
 
 def select(records: np.ndarray) -> np.ndarray:
-    best = records[0]
-    for r in records[1:]:
-        if better(r, best):
-            best = r
-    return best
+    """The winning record under ``better``'s order, vectorised: the first NaN cost by index if any valid record
+    has one, else the smallest cost, ties to the lower index; records[0] when none is valid."""
+    r = np.asarray(records, dtype=np.float64)
+    valid = r[:, 0] > 0.5
+    if not valid.any():
+        return r[0]
+    cost = r[:, 1]
+    nan = valid & np.isnan(cost)
+    cand = nan if nan.any() else valid & (cost == np.min(cost[valid & ~np.isnan(cost)]))
+    rows = np.flatnonzero(cand)
+    return r[rows[np.argmin(r[rows, 2])]]
+
+
+_STAGING = {}
+
+
+def _staging(backend, dev, n, ws, group):
+    """Per (group, device, record size) buffers of the host-staged exchange, kept across control steps:
+    under nccl a pinned host record, its device copy, the gathered device records and their pinned host
+    copy (so both copies are asynchronous on the device's current stream and one synchronisation ends
+    the step); under gloo the host record and the gathered host records."""
+    import torch
+    key = (id(group), backend, str(dev), n, ws)
+    b = _STAGING.get(key)
+    if b is None:
+        f64 = torch.float64
+        if backend == "nccl":
+            b = (torch.zeros(n, dtype=f64).pin_memory(), torch.zeros(n, dtype=f64, device=dev),
+                 torch.zeros(ws * n, dtype=f64, device=dev), torch.zeros(ws * n, dtype=f64).pin_memory())
+        else:
+            b = (torch.zeros(n, dtype=f64), None, torch.zeros(ws * n, dtype=f64), None)
+        _STAGING[key] = b
+    return b
 
 
 def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optional[np.ndarray],
@@ -137,27 +165,37 @@ def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optiona
     """One collective per control step; returns the global (cost, index, first_action).
     ``device``: the GPU this rank's engine runs on -- under nccl (RCCL) the record goes through
     that device, so each rank's collective uses its own GPU even when the caller never called
-    torch.cuda.set_device (default: torch's current device)."""
+    torch.cuda.set_device (default: torch's current device).  The record's copies go through pinned
+    buffers kept per group and device (``_staging``): H2D, the all-gather and the D2H are enqueued
+    back to back on that device's current stream, one synchronisation, the selection vectorised on the
+    host (the host-staged tail's cost per step)."""
     import torch
     import torch.distributed as dist
     rank, ws = world(group)
-    rec = np.zeros(3 + action_dim, dtype=np.float64)
+    n = 3 + action_dim
+    if ws == 1:
+        fa = np.zeros(action_dim) if first_action is None else np.asarray(first_action, dtype=np.float64).copy()
+        return float(cost), int(index), fa
+    backend = dist.get_backend(group)
+    dev = (torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
+           if backend == "nccl" else torch.device("cpu"))
+    h_rec, d_rec, out, h_out = _staging(backend, dev, n, ws, group)
+    rec = h_rec.numpy()
     rec[0] = 1.0 if valid else 0.0
     rec[1] = cost
     rec[2] = float(index)
-    if first_action is not None:
-        rec[3:] = first_action
-    if ws == 1:
-        return float(rec[1]), int(rec[2]), rec[3:].copy()
-    backend = dist.get_backend(group)
+    rec[3:] = 0.0 if first_action is None else first_action
     if backend == "nccl":
-        dev = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev)
+            d_rec.copy_(h_rec, non_blocking=True)
+            dist.all_gather_into_tensor(out, d_rec, group=group)
+            h_out.copy_(out, non_blocking=True)
+            stream.synchronize()
+        recs = h_out.numpy().reshape(ws, n)
     else:
-        dev = torch.device("cpu")
-    t = torch.from_numpy(rec).to(dev)
-    out = torch.empty(ws * rec.size, dtype=torch.float64, device=dev)
-    dist.all_gather_into_tensor(out, t, group=group)
-    recs = out.view(ws, rec.size).cpu().numpy()
+        dist.all_gather_into_tensor(out, h_rec, group=group)
+        recs = out.numpy().reshape(ws, n)
     best = select(recs)
     if best[0] < 0.5:
         raise ValueError("attempt to get argmin of an empty sequence")

@@ -241,3 +241,26 @@ def test_seed_stream_is_the_one_at_a_time_sequence():
     t = _SeedStream(1)
     t.set_state(st)
     assert [t.next() for _ in range(79)] == want[71:]
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_vectorised_select_matches_the_pairwise_order(seed):
+    """distributed.select (vectorised) == a left fold of distributed.better over the same records: invalid
+    records lose, the first NaN (by index) wins, else the smallest cost, ties to the lower index."""
+    rs = np.random.RandomState(seed)
+    n = int(rs.randint(1, 12))
+    recs = np.zeros((n, 9))
+    recs[:, 0] = rs.rand(n) < 0.8
+    recs[:, 1] = np.round(rs.standard_normal(n), 0)            # many ties
+    recs[:, 2] = rs.permutation(1000)[:n]
+    recs[:, 3:] = rs.standard_normal((n, 6))
+    if seed % 4 == 0:
+        recs[rs.randint(0, n, size=2), 1] = np.nan
+    if seed % 7 == 0:
+        recs[:, 1] = np.inf
+    want = recs[0]
+    for r in recs[1:]:
+        if dd.better(r, want):
+            want = r
+    got = dd.select(recs)
+    assert np.array_equal(got, want, equal_nan=True)
