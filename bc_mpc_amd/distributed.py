@@ -173,7 +173,7 @@ def allgather_minloc(valid: bool, cost: float, index: int, first_action: Optiona
     import torch.distributed as dist
     rank, ws = world(group)
     n = 3 + action_dim
-    if ws == 1:
+    if not (dist.is_available() and dist.is_initialized()):      # (a 1-rank group still gathers: tests)
         fa = np.zeros(action_dim) if first_action is None else np.asarray(first_action, dtype=np.float64).copy()
         return float(cost), int(index), fa
     backend = dist.get_backend(group)

@@ -47,6 +47,12 @@ for model in ("delta", "reward"):
         cost, index, first = ex.exchange(stream)
         assert (index, cost) == (want.best_index, want.best_cost), (model, seed, index, cost, want)
         assert np.array_equal(first[:6], want.first_action)
+        # the host-staged exchange the controllers use (distributed.allgather_minloc): the record goes
+        # through the pinned staging buffers, the 1-rank RCCL all-gather and the vectorised select unchanged
+        sign = -1.0 if model == "reward" else 1.0
+        c2, i2, f2 = bd.allgather_minloc(True, sign * want.best_cost, want.best_index, want.first_action, 6,
+                                         device=0)
+        assert (sign * c2, i2) == (want.best_cost, want.best_index) and np.array_equal(f2, want.first_action)
     eng.close()
     print(model, "ok")
 dist.destroy_process_group()

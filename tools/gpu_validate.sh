@@ -8,7 +8,7 @@
 #     timed    kernel trace of the headline's timed launches only   -> $OUT/trace_timed/
 #     traffic  PMC FETCH_SIZE / WRITE_SIZE passes per workload      -> $OUT/traffic_*/
 #     issue    PMC issue / wait / memory-path passes over $PMC_ARGS -> $OUT/pmc_*/
-#     rehearse 2-rank gloo rehearsal of bench.py on the one card, the ranks started by bench.py --gpus 2
+#     rehearse $RANKS-rank (default 2) gloo rehearsal of bench.py on the one card, the ranks started by bench.py --gpus N
 #              itself (no WORLD_SIZE: its child torch.distributed.run)  -> $OUT/rehearsal.json
 #     ab       tools/ab_libs.sh $AB_WL $AB_STEPS $AB_LIBS (AB_ARGS: extra bench arguments) -> $OUT/ab.txt
 #   TAG    output directory gpurun_out/$TAG
@@ -74,8 +74,8 @@ for step in $STEPS; do
       python3 "$R/tools/pmc_issue.py" "$OUT" "$PMC_KERNEL" ${PMC_CANDSTEPS:-1310720} > "$OUT/pmc_summary.txt" 2>&1 || true
       cat "$OUT/pmc_summary.txt" ;;
     rehearse)
-      BCMPC_DIST_BACKEND=gloo BCMPC_BENCH_DEVICE=0 timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 1 \
-          --no-cpu-baseline $BENCH_ARGS > "$OUT/rehearsal.json" 2> "$OUT/rehearsal.err" || stop rehearse $?
+      BCMPC_DIST_BACKEND=gloo BCMPC_BENCH_DEVICE=0 timeout -k 10 400 python bench.py --gpus ${RANKS:-2} --steps 5 \
+          --warmup 1 --no-cpu-baseline $BENCH_ARGS > "$OUT/rehearsal.json" 2> "$OUT/rehearsal.err" || stop rehearse $?
       tail -c 600 "$OUT/rehearsal.json" ;;
     ab)
       ROUNDS=${ROUNDS:-2} AB_ARGS=${AB_ARGS:-} bash tools/ab_libs.sh ${AB_WL:-cfg3} ${AB_STEPS:-30} $AB_LIBS \
