@@ -92,6 +92,10 @@ CASES = [
          inject="philox", rng_seed=0x5EED_1234_ABCD, cand_offset=1000),
     dict(name="ragged_k1", K=1, H=4, hidden=64, L=2, act="tanh", ln=False, seed=12),
     dict(name="ragged_k17_h1", K=17, H=1, hidden=64, L=2, act="relu", ln=False, seed=13),
+    # round 6: train_mpc_ppo.py's 2x256 relu + LayerNorm net (:52, :74-75, :539) at cfg2's K and H (synthetic
+    # weights: vars.pkl is refused by every allowed loader, PROVENANCE.json), and the same net without LN
+    dict(name="ppo_net_k4096_h20_relu_ln", K=4096, H=20, hidden=256, L=2, act="relu", ln=True, seed=14),
+    dict(name="ppo_net_k4096_h20_relu", K=4096, H=20, hidden=256, L=2, act="relu", ln=False, seed=15),
 ]
 
 STORE_WEIGHTS_MAX_HIDDEN = 128
@@ -459,6 +463,15 @@ def main():
                                     "deterministic branch, ppo_bc_policy.py:54-88,174-185; TF/baselines absent)"),
                   f, indent=1)
     if os.environ.get("GEN_PROVENANCE_ONLY"):
+        return
+    only = set(filter(None, os.environ.get("GEN_ONLY", "").split(",")))   # (regenerate just these cases)
+    if only:
+        for c in CASES:
+            if c["name"] in only:
+                out = run_case(c)
+                np.savez_compressed(os.path.join(HERE, f"{c['name']}.npz"), **out)
+                print(f"{c['name']:32s} K={c['K']:5d} H={c['H']:3d} argmin={int(out['argmin']):5d} "
+                      f"gap={float(out['top2_gap']):.4g} near={int(out['near_threshold'].sum())}")
         return
     for c in REWARD_CASES + POLICY_REWARD_CASES:
         out = (run_policy_reward_case if c.get("explore") is not None else run_reward_case)(c)
