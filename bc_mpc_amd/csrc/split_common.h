@@ -1,5 +1,5 @@
 // split_common.h -- helpers shared by the split-f16 rollout kernels (rollout_x3.hip,
-// rollout_rr.hip): the hi/lo f16 operand split, the tanh epilogue on element pairs and
+// rollout_team.hip): the hi/lo f16 operand split, the tanh epilogue on element pairs and
 // the cross-row lane exchanges.  Internal to libbcmpc.
 #pragma once
 #include <hip/hip_runtime.h>

@@ -83,10 +83,9 @@ typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")  
     BCMPC_KERNEL_SPLIT1 = 5,    /* BCMPC_PREC_SPLIT_F16: one workgroup = 1 x 16 candidates  */
     BCMPC_KERNEL_SPLIT2 = 6,    /*                                      2 x 16 candidates  */
     BCMPC_KERNEL_SPLIT4 = 7,    /*                                      4 x 16 candidates  */
-    BCMPC_KERNEL_SPLITR = 8,    /* BCMPC_PREC_SPLIT_F16, 2-layer tanh NNDynamicsModel, hidden
-                                   <= 512, no policy: one wave = 16 candidates with its
-                                   layer-1 input in registers, weights streamed through an
-                                   LDS ring, two workgroups per CU (rollout_rr.hip)          */
+    BCMPC_KERNEL_SPLITR = 8,    /* retired in round 6 (the resident-column rollout_rr, slower
+                                   than SPLIT4 at every K): bcmpc_create returns
+                                   BCMPC_ERR_UNSUPPORTED; the value stays reserved            */
     BCMPC_KERNEL_TEAM = 9       /* BCMPC_PREC_SPLIT_F16, small K: 2-layer NNDynamicsModel (tanh
                                    / relu, LayerNorm up to hidden 256), and at hidden 449..512
                                    (tanh) with a fused policy (<= 2 x 128) and / or the
