@@ -172,6 +172,27 @@ class NumpyDynamics:
         return unnormalized_state + unnormalized_state_delta
 
 
+class NumpyDynamicsF64(NumpyDynamics):
+    """The same net evaluated in f64 (matmuls, activation, LayerNorm), the output rounded to f32 as the
+    reference's feed / fetch do -- NOT the reference's arithmetic: a yardstick for how strongly a fixture's
+    dynamics amplify the MLP's f32 rounding over the horizon (``conditioning`` in tests/golden/, round 6).
+    Any implementation that rounds differently from TF's f32 order inherits at least that spread."""
+
+    def mlp(self, x32: np.ndarray) -> np.ndarray:
+        w = self.weights
+        out = np.asarray(x32, dtype=np.float64)
+        for li in range(w.n_layers):
+            out = out @ w.kernels[li].astype(np.float64) + w.biases[li].astype(np.float64)
+            out = np.tanh(out) if w.activation == "tanh" else np.maximum(out, 0.0)
+            if w.layer_norm:
+                m = out.mean(axis=-1, keepdims=True)
+                v = np.square(out - m).mean(axis=-1, keepdims=True)
+                out = (out - m) / np.sqrt(v + LN_EPS) * w.ln_gamma[li].astype(np.float64) + \
+                    w.ln_beta[li].astype(np.float64)
+        out = out @ w.kernels[-1].astype(np.float64) + w.biases[-1].astype(np.float64)
+        return out.astype(np.float32)
+
+
 # ----------------------------------------------------------------------------
 # controllers.py restatement (MPCcontroller, controllers.py:26-88)
 # ----------------------------------------------------------------------------

@@ -94,8 +94,10 @@ CASES = [
     dict(name="ragged_k17_h1", K=17, H=1, hidden=64, L=2, act="relu", ln=False, seed=13),
     # round 6: train_mpc_ppo.py's 2x256 relu + LayerNorm net (:52, :74-75, :539) at cfg2's K and H (synthetic
     # weights: vars.pkl is refused by every allowed loader, PROVENANCE.json), and the same net without LN
-    dict(name="ppo_net_k4096_h20_relu_ln", K=4096, H=20, hidden=256, L=2, act="relu", ln=True, seed=14),
-    dict(name="ppo_net_k4096_h20_relu", K=4096, H=20, hidden=256, L=2, act="relu", ln=False, seed=15),
+    dict(name="ppo_net_k4096_h20_relu_ln", K=4096, H=20, hidden=256, L=2, act="relu", ln=True, seed=14,
+         conditioning=True),
+    dict(name="ppo_net_k4096_h20_relu", K=4096, H=20, hidden=256, L=2, act="relu", ln=False, seed=15,
+         conditioning=True),
 ]
 
 STORE_WEIGHTS_MAX_HIDDEN = 128
@@ -218,6 +220,11 @@ def run_case(c):
                 out[f"ln_b{i}"] = w.ln_beta[i]
     if captured["states"].nbytes <= STORE_STATES_MAX:
         out["states"] = captured["states"]
+    if c.get("conditioning"):
+        # how far the same net evaluated in f64 lands from the reference's f32 costs, per candidate: the
+        # spread any other rounding order inherits on these dynamics (oracle.NumpyDynamicsF64)
+        c64, _ = orc.rollout(orc.NumpyDynamicsF64(w, norm), state, captured["actions"])
+        out["conditioning"] = np.abs(c64 - costs)
     # sanity: the build's oracle restatement reproduces the reference bit-exactly
     rc, _ = orc.rollout(dyn, state, captured["actions"])
     assert np.array_equal(rc, costs, equal_nan=True), c["name"]

@@ -58,15 +58,22 @@ def _engine(g: Golden, K=None, H=None, cost="cheetah", kernel="auto"):
     return eng
 
 
-def assert_costs_close(got, want, near=None, label="", env=ENV_PLAIN):
+COND_K = 4.0     # multiples of a fixture's conditioning (its f64-vs-reference spread) added to the tolerance
+
+
+def assert_costs_close(got, want, near=None, label="", env=ENV_PLAIN, cond=None):
     """The stated tolerance AND the achieved envelope ``env`` (conftest.envelope), except exact +-10
-    flips of near-threshold candidates."""
+    flips of near-threshold candidates.  ``cond`` (fixtures that hold it): per candidate, the spread between
+    the reference's f32 costs and the same net in f64 arithmetic -- where the dynamics amplify rounding
+    that much, no other rounding order can be held closer, so COND_K times it widens that candidate's bar."""
     assert got.shape == want.shape
     nan_g, nan_w = np.isnan(got), np.isnan(want)
     assert np.array_equal(nan_g, nan_w), f"{label}: NaN pattern differs"
     ok = ~nan_w
     diff = np.abs(got[ok] - want[ok])
     tol = np.minimum(ATOL + RTOL * np.abs(want[ok]), env)
+    if cond is not None:
+        tol = tol + COND_K * cond[ok]
     bad = diff > tol
     if near is not None:
         nr = near[ok]
@@ -81,7 +88,7 @@ def argmin_is_decidable(g: Golden) -> bool:
     best = g.costs[g.argmin]
     if np.isnan(best):
         return True
-    return g.top2_gap > 2 * (ATOL + RTOL * abs(best)) and not g.near[g.argmin]
+    return g.top2_gap > 2 * (ATOL + RTOL * abs(best) + COND_K * float(np.max(g.cond))) and not g.near[g.argmin]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -99,7 +106,7 @@ def test_engine_matches_reference_fixture(name, kernel):
         res = eng.get_action(g.state, g.actions(), return_costs=True)
         offset = 0
     assert_costs_close(res.costs, g.costs, g.near, f"{name}/{kernel}",
-                       env=envelope(g.meta["ln"], g.weights.n_layers, g.meta["hidden"], g.H))
+                       env=envelope(g.meta["ln"], g.weights.n_layers, g.meta["hidden"], g.H), cond=g.cond)
     assert res.best_index - offset == int(np.argmin(res.costs))
     if argmin_is_decidable(g):
         assert res.best_index - offset == g.argmin
