@@ -193,6 +193,43 @@ class NumpyDynamicsF64(NumpyDynamics):
         return out.astype(np.float32)
 
 
+class NumpyDynamicsChunked(NumpyDynamics):
+    """The reference's f32 MLP with every dense layer's k-sum split into ``chunks`` partial f32 GEMMs added in
+    f32 (in reverse chunk order with ``reverse``): the same arithmetic type as TF's, another summation order --
+    a second yardstick beside NumpyDynamicsF64 for a fixture's rounding spread (``conditioning``)."""
+
+    def __init__(self, weights, normalization, chunks=4, reverse=False):
+        super().__init__(weights, normalization)
+        self.chunks, self.reverse = int(chunks), bool(reverse)
+
+    def _mm(self, a, W):
+        q = np.linspace(0, a.shape[1], self.chunks + 1).astype(int)
+        acc = np.zeros((a.shape[0], W.shape[1]), np.float32)
+        order = range(self.chunks)[::-1] if self.reverse else range(self.chunks)
+        for i in order:
+            acc = (acc + (a[:, q[i]:q[i + 1]] @ W[q[i]:q[i + 1]]).astype(np.float32)).astype(np.float32)
+        return acc
+
+    def mlp(self, x32: np.ndarray) -> np.ndarray:
+        w = self.weights
+        out = x32
+        for li in range(w.n_layers):
+            out = _act(self._mm(out, w.kernels[li]) + w.biases[li], w.activation)
+            if w.layer_norm:
+                out = layer_norm_tf1(out, w.ln_gamma[li], w.ln_beta[li])
+        return (self._mm(out, w.kernels[-1]) + w.biases[-1]).astype(np.float32)
+
+
+def conditioning(weights, normalization, state, action_paths, costs) -> np.ndarray:
+    """Per candidate, the largest |cost - costs| over four other roundings of the same net (f64 arithmetic;
+    f32 with the k-sums in 4 chunks, 4 chunks reversed, 2 chunks): how far these dynamics carry a change of
+    rounding order over the horizon -- any implementation that does not replay TF's own f32 order inherits
+    that spread (tests/golden, round 6)."""
+    dyns = [NumpyDynamicsF64(weights, normalization), NumpyDynamicsChunked(weights, normalization, 4),
+            NumpyDynamicsChunked(weights, normalization, 4, reverse=True), NumpyDynamicsChunked(weights, normalization, 2)]
+    return np.max([np.abs(rollout(d, state, action_paths)[0] - costs) for d in dyns], axis=0)
+
+
 # ----------------------------------------------------------------------------
 # controllers.py restatement (MPCcontroller, controllers.py:26-88)
 # ----------------------------------------------------------------------------

@@ -66,11 +66,11 @@ class Golden:
         self.argmin = int(z["argmin"])
         self.opt_action = z["opt_action"]
         self.near = z["near_threshold"]
-        # per-candidate |f64-arithmetic cost - reference cost| (oracle.NumpyDynamicsF64), where the fixture holds
-        # it: the rounding spread these dynamics amplify over the horizon (zero: not measured, not needed).  One
-        # other rounding order is one sample of that spread, so each candidate's value is floored at the
-        # fixture's 90th percentile (a reordered f32 oracle -- k-chunked sums -- then lands inside 4x of it on
-        # every candidate of both round-6 fixtures; per candidate alone it exceeds 4x on 63 of 4,096)
+        # per candidate, the largest |cost - reference cost| over four other roundings of the same net
+        # (oracle.conditioning), where the fixture holds it: the rounding spread these dynamics amplify over the
+        # horizon (zero: not measured, not needed).  A few samples of a spread, so each candidate's value is
+        # floored at the fixture's 90th percentile (a fifth order -- k-sums in 8 chunks -- then lands inside 4x
+        # of it on every candidate, tests/test_oracle_golden.py)
         if "conditioning" in z.files:
             c = np.asarray(z["conditioning"], dtype=np.float64)
             self.cond = np.maximum(c, np.quantile(c[np.isfinite(c)], 0.9))

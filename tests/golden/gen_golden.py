@@ -221,10 +221,9 @@ def run_case(c):
     if captured["states"].nbytes <= STORE_STATES_MAX:
         out["states"] = captured["states"]
     if c.get("conditioning"):
-        # how far the same net evaluated in f64 lands from the reference's f32 costs, per candidate: the
-        # spread any other rounding order inherits on these dynamics (oracle.NumpyDynamicsF64)
-        c64, _ = orc.rollout(orc.NumpyDynamicsF64(w, norm), state, captured["actions"])
-        out["conditioning"] = np.abs(c64 - costs)
+        # how far other rounding orders of the same net land from the reference's f32 costs, per candidate:
+        # the spread any implementation that does not replay TF's own order inherits (oracle.conditioning)
+        out["conditioning"] = orc.conditioning(w, norm, state, captured["actions"], costs)
     # sanity: the build's oracle restatement reproduces the reference bit-exactly
     rc, _ = orc.rollout(dyn, state, captured["actions"])
     assert np.array_equal(rc, costs, equal_nan=True), c["name"]
