@@ -203,6 +203,11 @@ class NumpyDynamicsChunked(NumpyDynamics):
         self.chunks, self.reverse = int(chunks), bool(reverse)
 
     def _mm(self, a, W):
+        if self.chunks <= 0:                       # one product at a time in k order (a sequential f32 chain)
+            acc = np.zeros((a.shape[0], W.shape[1]), np.float32)
+            for k in range(a.shape[1]):
+                acc = (acc + (a[:, k:k + 1] * W[k]).astype(np.float32)).astype(np.float32)
+            return acc
         q = np.linspace(0, a.shape[1], self.chunks + 1).astype(int)
         acc = np.zeros((a.shape[0], W.shape[1]), np.float32)
         order = range(self.chunks)[::-1] if self.reverse else range(self.chunks)
@@ -221,12 +226,13 @@ class NumpyDynamicsChunked(NumpyDynamics):
 
 
 def conditioning(weights, normalization, state, action_paths, costs) -> np.ndarray:
-    """Per candidate, the largest |cost - costs| over four other roundings of the same net (f64 arithmetic;
-    f32 with the k-sums in 4 chunks, 4 chunks reversed, 2 chunks): how far these dynamics carry a change of
-    rounding order over the horizon -- any implementation that does not replay TF's own f32 order inherits
-    that spread (tests/golden, round 6)."""
+    """Per candidate, the largest |cost - costs| over five other roundings of the same net (f64 arithmetic;
+    f32 with the k-sums in 4 chunks, 4 chunks reversed, 2 chunks, and one product at a time in k order): how
+    far these dynamics carry a change of rounding order over the horizon -- any implementation that does not
+    replay TF's own f32 order inherits that spread (tests/golden, round 6)."""
     dyns = [NumpyDynamicsF64(weights, normalization), NumpyDynamicsChunked(weights, normalization, 4),
-            NumpyDynamicsChunked(weights, normalization, 4, reverse=True), NumpyDynamicsChunked(weights, normalization, 2)]
+            NumpyDynamicsChunked(weights, normalization, 4, reverse=True), NumpyDynamicsChunked(weights, normalization, 2),
+            NumpyDynamicsChunked(weights, normalization, 0)]
     return np.max([np.abs(rollout(d, state, action_paths)[0] - costs) for d in dyns], axis=0)
 
 

@@ -66,7 +66,7 @@ class Golden:
         self.argmin = int(z["argmin"])
         self.opt_action = z["opt_action"]
         self.near = z["near_threshold"]
-        # per candidate, the largest |cost - reference cost| over four other roundings of the same net
+        # per candidate, the largest |cost - reference cost| over five other roundings of the same net
         # (oracle.conditioning), where the fixture holds it: the rounding spread these dynamics amplify over the
         # horizon (zero: not measured, not needed).  A few samples of a spread, so each candidate's value is
         # floored at the fixture's 90th percentile (a fifth order -- k-sums in 8 chunks -- then lands inside 4x
