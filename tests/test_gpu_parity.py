@@ -58,7 +58,10 @@ def _engine(g: Golden, K=None, H=None, cost="cheetah", kernel="auto"):
     return eng
 
 
-COND_K = 4.0     # multiples of a fixture's conditioning (its f64-vs-reference spread) added to the tolerance
+# multiples of a fixture's conditioning (its rounding spread, conftest.Golden.cond) added to the tolerance: the
+# kernels' deviation on the relu + LayerNorm H = 20 fixture reaches 4.3x it at worst (the f32 solo kernel's
+# sequential k chains; group4 2.2x, split4 2.3x, team 2.9x: profiles/r06_cond_ratios.txt)
+COND_K = 6.0
 
 
 def assert_costs_close(got, want, near=None, label="", env=ENV_PLAIN, cond=None):
