@@ -219,8 +219,7 @@ def dropin_parity_p50(K_global, H, hidden, L, act, ln, kernels, biases, ln_g, ln
     ctrl = MPCcontroller(_Env(), dyn, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K_global,
                          device=device)
     np.random.seed(0)                                  # train_mpc_ppo.py:499
-    for _ in range(3):
-        ctrl.get_action(state)
+    pre = prewarm(lambda i: ctrl.get_action(state), fixed_calls=20 if world > 1 else None)
     ts = []
     for _ in range(calls):
         if world > 1:
@@ -233,7 +232,7 @@ def dropin_parity_p50(K_global, H, hidden, L, act, ln, kernels, biases, ln_g, ln
     out = {"p50_ms": p50 * 1e3, "p90_ms": float(np.percentile(ts, 90)) * 1e3, "calls": calls,
            "cand_steps_per_s": K_global * H / p50, "K_global": K_global, "horizon": H,
            "rng": "numpy legacy MT19937 stream (np.random.seed(0)), drawn by the library",
-           "mt_path": os.environ.get("BCMPC_MT_PATH", "default")}
+           "mt_path": os.environ.get("BCMPC_MT_PATH", "default"), "prewarm": pre}
     ctrl._engine.close()
     return out
 
@@ -284,8 +283,7 @@ def dropin_small_k(name, wl, prob, device, calls=200, gap_us=50.0):
         ctrl = MPCcontroller(_Env(), dyn, horizon=H, cost_fn=cheetah_cost_fn, num_simulated_paths=K, device=device)
         kind = "MPCcontroller"
     np.random.seed(0)                                  # train_mpc_ppo.py:499
-    for _ in range(10):
-        ctrl.get_action(prob["state"])
+    prewarm(lambda i: ctrl.get_action(prob["state"]))
     ts, tg = [], []
     for _ in range(calls):
         t0 = time.perf_counter()
@@ -382,6 +380,37 @@ def make_engine(wl, prob, device, precision, K=None):
 SMALL_K = ("ppo_defaults", "ppo_mpc_default", "runsh_recipe", "cfg1")
 
 
+PREWARM_S = float(os.environ.get("BCMPC_BENCH_PREWARM_S", "0.25"))
+
+
+def prewarm(step, ctx=None, budget_s=None, fixed_calls=None, seed_base=1 << 40):
+    """Run the line's own control step for about ``budget_s`` before its warmup steps.  After idle -- process
+    start, or the seconds of CPU baseline between two lines -- the GPU's clocks ramp over the first ~40 ms of
+    work: at cfg3 the launches take 2.34 → 1.79 ms over the first 20 (`profiles/r06_cold_ramp.txt`), so a line
+    whose few warmup steps fall inside that ramp would time its first steps at the idle clocks.  The prewarm
+    calls do the same work as the timed steps (other seeds), are untimed, and are reported in the line's
+    ``prewarm`` record.  With ``ctx`` (several ranks) the call count is agreed on (every step holds a
+    collective); ``fixed_calls`` sets it outright."""
+    import math
+    import torch
+    budget_s = PREWARM_S if budget_s is None else budget_s
+    t0 = time.perf_counter()
+    done = 0
+    if fixed_calls is None:
+        step(seed_base)
+        done = 1
+        calls = max(0, int(math.ceil(budget_s / max(time.perf_counter() - t0, 1e-6))) - 1)
+        if ctx is not None:
+            calls = int(ctx.allreduce(calls, "max"))
+    else:
+        calls = int(fixed_calls)
+    for i in range(calls):
+        step(seed_base + done + i)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    return {"calls": done + calls, "seconds": time.perf_counter() - t0}
+
+
 def pmc_traffic(key):
     """HBM bytes per launch measured by the PMC passes of this round (profiles/TRAFFIC_FILE), or None."""
     try:
@@ -427,6 +456,7 @@ def cfg2_line(device, calls=100, warmup=10, cpu_seconds=4.0, dropin_calls=20, wi
     wl = WORKLOADS["cfg2"]
     prob = synthetic_problem(wl)
     eng = make_engine(wl, prob, device, "auto")
+    pre = prewarm(lambda i: eng.get_action(prob["state"], None, seed=0xC2 + i))
     ts = []
     for i in range(warmup + calls):
         t0 = time.perf_counter()
@@ -443,7 +473,8 @@ def cfg2_line(device, calls=100, warmup=10, cpu_seconds=4.0, dropin_calls=20, wi
            "value": wl["K"] * wl["H"] / float(np.median(ts)), "unit": "candidate-steps/s",
            "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
            "roofline": roofline_line(wl["K"], wl["H"], fpcs, float(np.mean(ks)), eng.precision,
-                                     traffic_key="cfg2:split:device" if eng.precision == "split" else None)}
+                                     traffic_key="cfg2:split:device" if eng.precision == "split" else None),
+           "prewarm": pre}
     eng.close()
     if dropin_calls:
         d = dropin_parity_p50(wl["K"], wl["H"], wl["hidden"], wl["L"], wl["act"], False, prob["kernels"],
@@ -477,6 +508,7 @@ def workload_line(name, device, steps=20, warmup=3, cpu_seconds=4.0, with_cpu=Tr
         def call(i):
             return eng.get_action(prob["state"], None, seed=0xC4 + i)
     eng.set_timing(True)
+    pre = prewarm(call)
     for i in range(warmup):
         call(i)
     ts, ks = [], []
@@ -492,7 +524,8 @@ def workload_line(name, device, steps=20, warmup=3, cpu_seconds=4.0, with_cpu=Tr
     row = {"K": K, "H": H, "net": net_label(wl, prob), "kernel": info["layout"], "precision": prec,
            "value": K * H * iters / float(np.median(ts)), "unit": "candidate-steps/s", "steps": steps,
            "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
-           "roofline": roofline_line(K, H, fpcs, float(np.mean(ks)), prec, iters=iters, traffic_key=key)}
+           "roofline": roofline_line(K, H, fpcs, float(np.mean(ks)), prec, iters=iters, traffic_key=key),
+           "prewarm": pre}
     if cem:
         row["cem"] = dict(cem, n_elite=n_elite)
         row["roofline"]["kernel_note"] = ("HIP events around the whole device-side CEM call: 4 rollout passes + "
@@ -587,6 +620,7 @@ def small_k_lines(device, calls=200, warmup=20, cpu_seconds=3.0, with_cpu=True):
                         os.environ["BCMPC_TEAM"] = old
             # p50 of the product path (no event markers: bcmpc_engine_set_timing off, its default), then
             # the kernel's HIP-event time over a second, timed pass
+            prewarm(lambda i: eng.get_action(prob["state"], None, seed=0x5EED + i))
             ts, ks = [], []
             for i in range(warmup + calls):
                 t0 = time.perf_counter()
@@ -630,6 +664,7 @@ def f16_line(wl, prob, device, steps=50, warmup=5, name="cfg3"):
     K, H = wl["K"], wl["H"]
     eng = make_engine(wl, prob, device, "f16")
     eng.set_timing(True)
+    pre = prewarm(lambda i: eng.get_action(prob["state"], None, seed=0xF16 + i))
     for i in range(warmup):
         eng.get_action(prob["state"], None, seed=0xF16 + i)
     ts, ks = [], []
@@ -671,6 +706,7 @@ def f16_line(wl, prob, device, steps=50, warmup=5, name="cfg3"):
             "roofline": {"bound": "mfma", "achieved": tf, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": tf / F16_MFMA_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_source": f"profiles/{TRAFFIC_FILE}"},
+            "prewarm": pre,
             "argmin_agreement": {"seeds": 16, "top1_equal": agree,
                                  "reference": "the split (f32-grade) engine's argmin on the same actions",
                                  "regret_median": float(np.median(regret)), "regret_max": float(np.max(regret)),
@@ -874,6 +910,7 @@ def scale_line(ctx, name, K_global, steps, warmup, precision="auto", scaling="st
     else:
         step, carrier = rollout_stepper(ctx, eng, prob["state"], lo, prob["reward"])
         kms = lambda: eng.last_kernel_ms()[0]          # noqa: E731
+    pre = prewarm(step, ctx)
     el, ts, ks = timed_loop(ctx, step, steps, warmup, kms)
     H = wl["H"]
     fpcs = flop_per_cand_step(wl["hidden"], wl["L"])
@@ -885,7 +922,7 @@ def scale_line(ctx, name, K_global, steps, warmup, precision="auto", scaling="st
            "ms_per_step": el / steps * 1e3, "p50_ms": float(np.median(ts) * 1e3),
            "kernel": eng.info()["layout"], "precision": eng.precision,
            "kernel_ms": kern, "collective": carrier,
-           "roofline": roofline_line(hi - lo, H, fpcs, kern, eng.precision, iters=iters)}
+           "roofline": roofline_line(hi - lo, H, fpcs, kern, eng.precision, iters=iters), "prewarm": pre}
     row["roofline"]["per"] = "the slowest rank's shard launch (max over ranks)"
     if cem:
         row["cem"] = dict(cem, n_elite=n_elite)
@@ -972,6 +1009,7 @@ def exchange_cost(device, K=8192, H=20, calls=200, warmup=20, n_rec=8):
 
     # the three tails pick the same winner
     assert device_select(7) == ga(7).best_index == int(host_staged(7)[2])
+    prewarm(ga)
     out = {"K": K, "H": H, "records": n_rec, "get_action_p50_ms": p50(ga), "host_staged_p50_ms": p50(host_staged),
            "device_select_p50_ms": p50(device_select), "calls": calls}
     out["host_staged_overhead_us"] = (out["host_staged_p50_ms"] - out["get_action_p50_ms"]) * 1e3
@@ -1119,6 +1157,7 @@ def main():
         carrier = "none (1 rank)" if world == 1 else f"torch {backend} all-gather + device select"
 
     kms = (lambda: eng.last_kernel_ms()[0]) if not (cem and world > 1) else None
+    pre = prewarm(step, ctx)                           # (untimed: the GPU's clock ramp after idle, see prewarm)
     elapsed, step_s, kern_ms = timed_loop(ctx, step, args.steps, args.warmup, kms)
 
     scale = None
@@ -1200,6 +1239,8 @@ def main():
                      "per": "one rank's shard launch (the slowest rank's, max over ranks)"},
         "cpu_baseline": None,
         "small_k": None,
+        "prewarm": dict(pre, note="untimed control steps of the same workload before the W warmup steps: the GPU's "
+                                  "clocks ramp over the first ~40 ms of work after idle (profiles/r06_cold_ramp.txt)"),
     }
     if scale is not None:
         out["scale"] = scale

@@ -3,6 +3,7 @@ BASELINE.json's configs, the roofline record (traffic per launch x passes for th
 traffic file the bench quotes, and the CPU-baseline record's thread choice (the oracle at a tiny K).  The GPU
 lines themselves run in the driver's bench and in tests/test_gpu_*.py."""
 import json
+import time
 import os
 
 import numpy as np
@@ -138,3 +139,16 @@ def test_ns_shard_is_the_north_star_per_gpu_shard():
     assert "K=65536" in base["north_star"] and "8" in base["north_star"]
     ns = bench.WORKLOADS["ns_shard"]
     assert ns["K"] * 8 == 65536 and ns["H"] == 20 and (ns["hidden"], ns["L"], ns["act"]) == (500, 2, "tanh")
+
+
+def test_prewarm_runs_the_step_for_its_budget_with_fresh_seeds():
+    seen = []
+
+    def step(i):
+        seen.append(i)
+        time.sleep(0.002)
+    rec = bench.prewarm(step, budget_s=0.02)
+    assert rec["calls"] == len(seen) and 5 <= len(seen) <= 15 and rec["seconds"] >= 0.015
+    assert len(set(seen)) == len(seen) and min(seen) >= 1 << 40          # never a timed step's seed
+    seen.clear()
+    assert bench.prewarm(step, fixed_calls=7)["calls"] == 7 == len(seen)
