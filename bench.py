@@ -397,9 +397,13 @@ def prewarm(step, ctx=None, budget_s=None, fixed_calls=None, seed_base=1 << 40):
     t0 = time.perf_counter()
     done = 0
     if fixed_calls is None:
-        step(seed_base)
-        done = 1
-        calls = max(0, int(math.ceil(budget_s / max(time.perf_counter() - t0, 1e-6))) - 1)
+        step(seed_base)                                # (the first call carries one-time costs: not the estimate)
+        t1 = time.perf_counter()
+        step(seed_base + 1)
+        step(seed_base + 2)
+        done = 3
+        per = (time.perf_counter() - t1) / 2
+        calls = max(0, int(math.ceil((budget_s - (time.perf_counter() - t0)) / max(per, 1e-6))))
         if ctx is not None:
             calls = int(ctx.allreduce(calls, "max"))
     else:

@@ -148,7 +148,7 @@ def test_prewarm_runs_the_step_for_its_budget_with_fresh_seeds():
         seen.append(i)
         time.sleep(0.002)
     rec = bench.prewarm(step, budget_s=0.02)
-    assert rec["calls"] == len(seen) and 5 <= len(seen) <= 15 and rec["seconds"] >= 0.015
+    assert rec["calls"] == len(seen) and 8 <= len(seen) <= 15 and rec["seconds"] >= 0.018
     assert len(set(seen)) == len(seen) and min(seen) >= 1 << 40          # never a timed step's seed
     seen.clear()
     assert bench.prewarm(step, fixed_calls=7)["calls"] == 7 == len(seen)
