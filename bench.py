@@ -424,13 +424,31 @@ def pmc_traffic(key):
         return None
 
 
-def roofline_line(K, H, fpcs, kernel_ms, precision, iters=1, traffic_key=None):
+# what the PMC passes name as the limiter below the MFMA roofline, per line
+LIMITER = {
+    "cfg3": "the lock-step chain of one 64-candidate group per CU (MFMA pipe busy 0.60; profiles/r05_pmc_x3_issue.txt)",
+    "cfg4_shard": "as cfg3 (same kernel, two workgroups per CU over the launch)",
+    "cfg2": "the per-CU weight stream of 16-candidate groups (L1->L2 41.5 B/clk/CU at 242 cycles, MFMA busy 0.27; "
+            "profiles/r05_pmc_cfg2_issue.txt)",
+    "ns_shard": "the per-CU weight stream of 32-candidate groups (L1->L2 40.4 B/clk/CU at 210 cycles, MFMA busy 0.47; "
+                "profiles/r06_pmc_ns_shard_issue.txt)",
+    "cfg5": "the per-CU vector-memory path of the 3x1024 net's fragment stream (48 B/clk/CU, L2 hit 96.7%; "
+            "profiles/r03_pmc_cfg5/summary.txt)",
+    "f16": "vector issue (VALU 0.49 + MFMA 0.43 of SIMD-cycles, two transcendentals per tanh; "
+           "profiles/r05_pmc_pp_issue.txt)",
+}
+
+
+def roofline_line(K, H, fpcs, kernel_ms, precision, iters=1, traffic_key=None, limiter=None):
     """The MFMA roofline of one launch: algorithmic FLOPs (K x H x flop_per_cand_step) / HIP-event kernel
-    time, against the peak of the precision the engine computes in."""
+    time, against the peak of the precision the engine computes in; ``limiter``: the LIMITER key naming what
+    the counters show binding below it."""
     peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "f16": F16_MFMA_PEAK_TFLOPS}.get(precision, SPLIT_PEAK_TFLOPS)
     tf = K * H * iters * fpcs / (kernel_ms / 1e3) / 1e12
     out = {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s", "frac": tf / peak,
            "flop_per_launch": K * H * iters * fpcs}
+    if limiter in LIMITER:
+        out["limiter"] = LIMITER[limiter]
     if traffic_key:
         t = pmc_traffic(traffic_key)
         # (the PMC passes measure one rollout launch; a CEM call is `iters` of them)
@@ -477,7 +495,8 @@ def cfg2_line(device, calls=100, warmup=10, cpu_seconds=4.0, dropin_calls=20, wi
            "value": wl["K"] * wl["H"] / float(np.median(ts)), "unit": "candidate-steps/s",
            "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
            "roofline": roofline_line(wl["K"], wl["H"], fpcs, float(np.mean(ks)), eng.precision,
-                                     traffic_key="cfg2:split:device" if eng.precision == "split" else None),
+                                     traffic_key="cfg2:split:device" if eng.precision == "split" else None,
+                                     limiter="cfg2"),
            "prewarm": pre}
     eng.close()
     if dropin_calls:
@@ -528,7 +547,8 @@ def workload_line(name, device, steps=20, warmup=3, cpu_seconds=4.0, with_cpu=Tr
     row = {"K": K, "H": H, "net": net_label(wl, prob), "kernel": info["layout"], "precision": prec,
            "value": K * H * iters / float(np.median(ts)), "unit": "candidate-steps/s", "steps": steps,
            "p50_ms": float(np.median(ts) * 1e3), "kernel_ms": float(np.mean(ks)),
-           "roofline": roofline_line(K, H, fpcs, float(np.mean(ks)), prec, iters=iters, traffic_key=key),
+           "roofline": roofline_line(K, H, fpcs, float(np.mean(ks)), prec, iters=iters, traffic_key=key,
+                                     limiter=name),
            "prewarm": pre}
     if cem:
         row["cem"] = dict(cem, n_elite=n_elite)
@@ -708,7 +728,7 @@ def f16_line(wl, prob, device, steps=50, warmup=5, name="cfg3"):
             "kernel": kern, "layout": layout, "value": K * H / float(np.mean(ts)), "unit": "candidate-steps/s",
             "p50_ms": float(np.percentile(ts, 50) * 1e3), "kernel_ms_avg": float(np.mean(ks)),
             "roofline": {"bound": "mfma", "achieved": tf, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tf / F16_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                         "frac": tf / F16_MFMA_PEAK_TFLOPS, "traffic": traffic, "limiter": LIMITER["f16"],
                          "traffic_source": f"profiles/{TRAFFIC_FILE}"},
             "prewarm": pre,
             "argmin_agreement": {"seeds": 16, "top1_equal": agree,
@@ -1240,6 +1260,9 @@ def main():
                                               "whole device-side CEM call)" if cem else ""),
                      "flop_per_launch": K * H * fpcs,
                      "flop_per_cand_step": fpcs,
+                     "limiter": LIMITER.get("cfg3" if (args.workload == "cfg3" and world == 1) else
+                                            "ns_shard" if (args.workload == "cfg3" and K <= 8192) else
+                                            args.workload, ""),
                      "per": "one rank's shard launch (the slowest rank's, max over ranks)"},
         "cpu_baseline": None,
         "small_k": None,
