@@ -1117,6 +1117,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs (N ranks on one GPU): BCMPC_DIST_BACKEND=gloo BCMPC_BENCH_DEVICE=0
     backend = os.environ.get("BCMPC_DIST_BACKEND", "nccl")
+    if "BCMPC_BENCH_DEVICE" not in os.environ and local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible "
+                         f"(one rank per GPU; a rehearsal on one card sets BCMPC_BENCH_DEVICE=0 and "
+                         f"BCMPC_DIST_BACKEND=gloo)")
     local = int(os.environ.get("BCMPC_BENCH_DEVICE", local))
     if world > 1:
         torch.cuda.set_device(local)
