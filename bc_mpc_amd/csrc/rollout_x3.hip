@@ -2079,6 +2079,11 @@ hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc
     }
 }
 #endif
+#ifdef X3_ONLY   // (variant builds carry no single-pass layouts: capi.cpp still links their shape queries)
+bool x3_f16_layout_ok(int, int, int) { return false; }
+size_t x3_f16_lds(int, int, int, int, int) { return 0; }
+bool x3_pp_ok(int, int, int, int) { return false; }
+#endif
 
 #if X3_PART == 1 && !defined(X3_ONLY)
 hipError_t launch_rollout_x3_plain(const RolloutArgs& a, int hidden_padded, int nc, hipStream_t st) {
