@@ -2083,6 +2083,7 @@ hipError_t launch_rollout_x3_f16(const RolloutArgs& a, int hidden_padded, int nc
 bool x3_f16_layout_ok(int, int, int) { return false; }
 size_t x3_f16_lds(int, int, int, int, int) { return 0; }
 bool x3_pp_ok(int, int, int, int) { return false; }
+hipError_t launch_rollout_x3_f16(const RolloutArgs&, int, int, hipStream_t) { return hipErrorInvalidValue; }
 #endif
 
 #if X3_PART == 1 && !defined(X3_ONLY)
