@@ -40,6 +40,8 @@ def test_headline_line_contract():
     assert (K, H) == (65536, 20) and d["config"]["K_global"] == 65536 and d["config"]["ranks"] == 1
     assert d["value"] == pytest.approx(K * H / (d["ms_per_step"] / 1e3), rel=1e-6)
     assert d["summary"]["headline"]["frac"] == pytest.approx(d["roofline"]["frac"], abs=1e-4)
+    assert list(d)[-1] == "summary"                              # (survives the driver's stdout tail)
+    assert d["prewarm"]["calls"] >= 3 and d["prewarm"]["seconds"] > 0   # untimed, reported (bench.prewarm)
     r = d["roofline"]
     assert r["bound"] == "mfma" and 0 < r["frac"] < 1
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
