@@ -35,7 +35,7 @@ PREC_FP32, PREC_SPLIT_F16, PREC_F16 = 0, 1, 2
 # "f16": single-pass f16 MFMA (BASELINE cfg3's bf16-class GEMM), not the fp32 tolerance
 PRECISIONS = {"fp32": PREC_FP32, "split": PREC_SPLIT_F16, "f16": PREC_F16}
 KERNELS = {"auto": 0, "solo": 1, "group2": 2, "group4": 3, "group8": 4, "split1": 5, "split2": 6, "split4": 7, "splitr": 8, "team": 9}
-# ("splitr" stays in the enum for the ABI; bcmpc_create refuses it since round 6)
+# ("splitr" and "group2" stay in the enum for the ABI; bcmpc_create refuses them since round 6)
 
 
 class Config(ctypes.Structure):

@@ -45,7 +45,7 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 int kern_waves(int kern) {
-    return kern == BCMPC_KERNEL_GROUP8 ? 8 : kern == BCMPC_KERNEL_GROUP4 ? 4 : kern == BCMPC_KERNEL_GROUP2 ? 2 : 1;
+    return kern == BCMPC_KERNEL_GROUP8 ? 8 : kern == BCMPC_KERNEL_GROUP4 ? 4 : 1;
 }
 
 int padded_hidden(int h) {
@@ -382,6 +382,9 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
     } else if (c.kernel >= BCMPC_KERNEL_SPLIT1) {
         return fail(BCMPC_ERR_ARG, "split kernels need precision SPLIT_F16");
     }
+    if (c.kernel == BCMPC_KERNEL_GROUP2)
+        return fail(BCMPC_ERR_UNSUPPORTED, "the group2 layout (2-wave f32 groups, A/B only, never chosen by auto) "
+                                           "was retired; use auto, group4 or group8");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (c.device < 0 || c.device >= ndev) return fail(BCMPC_ERR_ARG, "device ordinal out of range");
@@ -548,7 +551,6 @@ int bcmpc_create(const bcmpc_config* cfg, bcmpc_engine** out) {
         if (c.kernel != BCMPC_KERNEL_AUTO) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group kernel does not fit this shape"); }
         kern = BCMPC_KERNEL_SOLO;
     }
-    if (kern == BCMPC_KERNEL_GROUP2 && e->HP > 512) { delete e; return fail(BCMPC_ERR_UNSUPPORTED, "group2 kernel supports hidden <= 512"); }
     if (kern == BCMPC_KERNEL_SOLO && (e->wpb < 1 || e->HP > 512)) {
         delete e;
         return fail(BCMPC_ERR_UNSUPPORTED, "solo kernel supports hidden <= 512 and needs LDS for its slabs");
@@ -2555,7 +2557,6 @@ int bcmpc_engine_layout(const bcmpc_engine* e, char* buf, int32_t cap) {
     char s[160];
     switch (e->kernel) {
         case BCMPC_KERNEL_SOLO: std::snprintf(s, sizeof(s), "rollout_fp32<%d> fp32", e->HP); break;
-        case BCMPC_KERNEL_GROUP2:
         case BCMPC_KERNEL_GROUP4:
         case BCMPC_KERNEL_GROUP8: std::snprintf(s, sizeof(s), "rollout_grp<%d,NW=%d> fp32", e->HP, e->nw); break;
         case BCMPC_KERNEL_TEAM:

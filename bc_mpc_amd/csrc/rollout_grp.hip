@@ -58,7 +58,6 @@ namespace bcmpc {
 constexpr int grp_waves_per_eu(int HP, int NW, int PHP = 0, bool RW = false) {
     return RW ? (NW == 8 ? 4 : 2)                      // reward net: 2 groups/CU (LDS), all resident
          : PHP > 0 ? (NW == 8 ? 4 : HP >= 512 ? 2 : 3)  // fused policy: more live state per wave
-         : NW == 2 ? 2
          : NW == 8 ? (HP >= 768 ? 3 : 4)
          : (HP >= 768 ? 2 : HP >= 512 ? GRP_WPE512 : 4);
 }
@@ -640,7 +639,6 @@ size_t grp_lds_bytes(int hidden_padded, int n_layers, int nw, int policy_hidden_
 
 hipError_t launch_rollout_grp(const RolloutArgs& a, int hidden_padded, int nw, hipStream_t st) {
     switch (nw) {
-        case 2: return launch_grp_nw<2>(a, hidden_padded, st);
         case 4: return launch_grp_nw<4>(a, hidden_padded, st);
         case 8: return launch_grp_nw<8>(a, hidden_padded, st);
         default: return hipErrorInvalidValue;

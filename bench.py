@@ -1146,7 +1146,7 @@ def main():
     eng = make_engine(wl, prob, local, args.precision, K=K)
     eng.set_timing(True)                               # the roofline's HIP events inside the timed region
     info = eng.info()
-    kernel_name = {"solo": "rollout_fp32", "group2": "rollout_grp<NW=2>", "group4": "rollout_grp<NW=4>",
+    kernel_name = {"solo": "rollout_fp32", "group4": "rollout_grp<NW=4>",
                    "group8": "rollout_grp<NW=8>", "split1": "rollout_x3<NC=1>", "split2": "rollout_x3<NC=2>",
                    "split4": "rollout_x3<NC=4>",
                    "team": "rollout_team (weights in registers, one column per team of workgroups)"}.get(

@@ -77,7 +77,8 @@ typedef enum bcmpc_precision {
 typedef enum bcmpc_kernel {     /* rollout kernel layout (DESIGN.md "kernels")              */
     BCMPC_KERNEL_AUTO = 0,
     BCMPC_KERNEL_SOLO = 1,      /* one wave owns 16 candidates, activations in VGPRs     */
-    BCMPC_KERNEL_GROUP2 = 2,    /* 2 waves share 16 candidates through an LDS slab       */
+    BCMPC_KERNEL_GROUP2 = 2,    /* retired in round 6 (A/B only, never chosen by auto):
+                                   bcmpc_create returns BCMPC_ERR_UNSUPPORTED             */
     BCMPC_KERNEL_GROUP4 = 3,    /* 4 waves share 16 candidates                           */
     BCMPC_KERNEL_GROUP8 = 4,    /* 8 waves share 16 candidates (small K)                 */
     BCMPC_KERNEL_SPLIT1 = 5,    /* BCMPC_PREC_SPLIT_F16: one workgroup = 1 x 16 candidates  */

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 ATOL, RTOL = 1e-4, 1e-5
 
 
-KERNELS = ["solo", "group2", "group4", "group8", "split1", "split2", "split4", "team"]
+KERNELS = ["solo", "group4", "group8", "split1", "split2", "split4", "team"]
 
 
 def team_ok(hidden, ln, n_layers, K, S=20, A=6):
@@ -227,12 +227,14 @@ def test_non_fused_cost_goes_through_trajectory_mode():
     assert ctrl.last_index == i and np.array_equal(a, want)
 
 
-def test_retired_splitr_kernel_is_refused():
+@pytest.mark.parametrize("kernel", ["splitr", "group2"])
+def test_retired_kernels_are_refused(kernel):
     """The resident-column kernel (rollout_rr.hip, opt-in only, slower than the slab kernel at every K: DESIGN.md
-    6.5) was retired in round 6: asking for it fails loudly instead of running another layout."""
+    6.5) and the 2-wave f32 group layout (A/B only, never chosen by auto) were retired in round 6: asking for
+    either fails loudly instead of running another layout."""
     from bc_mpc_amd.engine import RolloutEngine
     with pytest.raises(ValueError, match="retired"):
-        RolloutEngine(20, 6, 500, 2, "tanh", False, 20, 4096, kernel="splitr")
+        RolloutEngine(20, 6, 500, 2, "tanh", False, 20, 4096, kernel=kernel)
 
 
 @pytest.mark.parametrize("kernel", ["auto", "solo", "group8", "split4", "split1"])
