@@ -98,6 +98,9 @@ CASES = [
          conditioning=True),
     dict(name="ppo_net_k4096_h20_relu", K=4096, H=20, hidden=256, L=2, act="relu", ln=False, seed=15,
          conditioning=True),
+    # BASELINE cfg5's 3x1024 tanh net (the CEM workload's dynamics) at a small K
+    dict(name="cfg5_net_3x1024_tanh", K=256, H=10, hidden=1024, L=3, act="tanh", ln=False, seed=16,
+         conditioning=True),
 ]
 
 STORE_WEIGHTS_MAX_HIDDEN = 128

@@ -40,6 +40,10 @@ def team_ok(hidden, ln, n_layers, K, S=20, A=6):
 def _skip_unsupported(g: Golden, kernel: str):
     if kernel == "group8" and g.meta["hidden"] <= 64:
         pytest.skip("group8 needs >= 8 hidden tiles")
+    if kernel == "solo" and g.meta["hidden"] > 512:
+        pytest.skip("solo: hidden <= 512")
+    if kernel == "split4" and g.meta["hidden"] > 512:
+        pytest.skip("split kernel at hidden > 512: 32-candidate groups at most (the hi + lo slab, 160-KiB LDS)")
     if kernel == "team" and not team_ok(g.meta["hidden"], g.meta["ln"], g.weights.n_layers, g.K, g.S, g.A):
         pytest.skip("team: the 2-layer delta net at small K (grid resident)")
     if kernel.startswith("split"):
