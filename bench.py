@@ -1282,10 +1282,14 @@ def main():
     # measured launch is the 1-GPU one, so the N > 1 shard (a smaller K) has none
     prof = os.path.join(REPO, "profiles", TRAFFIC_FILE)
     out["roofline"]["traffic_source"] = f"profiles/{TRAFFIC_FILE}"
-    if os.path.exists(prof) and world == 1:
+    # (N > 1: the rank's shard is measured by the 1-GPU line of the same 2x500 tanh net at that K, if any)
+    shard_wl = args.workload if world == 1 else {65536: "cfg3", 32768: "cfg4_shard", 8192: "ns_shard",
+                                                 4096: "cfg2"}.get(K) if args.workload == "cfg3" else None
+    if os.path.exists(prof) and shard_wl:
         try:
-            key = args.workload + {"fp32": "", "f16": ":f16"}.get(eng.precision, ":split") + \
+            key = shard_wl + {"fp32": "", "f16": ":f16"}.get(eng.precision, ":split") + \
                 (":device" if args.actions == "device" else "")
+            out["roofline"]["traffic_key"] = key
             tr = json.load(open(prof)).get(key)
             if tr:
                 out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
