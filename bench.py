@@ -1278,8 +1278,7 @@ def main():
     if lib_line is not None:
         out["library_comm"] = lib_line
     # PMC HBM traffic per launch of THIS round's kernels (tools/gpu_validate.sh traffic: rocprofv3 --pmc FETCH_SIZE /
-    # WRITE_SIZE in separate passes, the gfx950 FETCH_SIZE x2 correction calibrated on the action tensor); the
-    # measured launch is the 1-GPU one, so the N > 1 shard (a smaller K) has none
+    # WRITE_SIZE in separate passes, the gfx950 FETCH_SIZE x2 correction calibrated on the action tensor)
     prof = os.path.join(REPO, "profiles", TRAFFIC_FILE)
     out["roofline"]["traffic_source"] = f"profiles/{TRAFFIC_FILE}"
     # (N > 1: the rank's shard is measured by the 1-GPU line of the same 2x500 tanh net at that K, if any)
